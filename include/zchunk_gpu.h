@@ -1,0 +1,166 @@
+/*
+ * zchunk_gpu.h — C ABI of the MI355X (gfx950) Zarr chunk-codec path.
+ *
+ * This is the drop-in boundary for the reference's chunk codec path
+ * (sci-rs/zarr v0.0.1).  Every entry point below replaces one piece of the
+ * reference; the file:line it replaces is cited next to it.  All arguments
+ * are plain pointers and sizes; no torch / HIP C++ types appear in the
+ * signatures (`stream` is an opaque hipStream_t passed as void*).
+ *
+ * Reference interface being replaced (paths relative to the reference root):
+ *   - trait Compression { decoder(R)->Box<dyn Read>; encoder(W)->Box<dyn Write> }
+ *       src/compression/mod.rs:30-34, dispatch mod.rs:72-108
+ *   - enum CompressionType {Raw, Bzip2, Gzip, Lz4, Xz}  src/compression/mod.rs:40-51
+ *   - DefaultChunkReader::read_chunk / read_chunk_into   src/chunk.rs:270-301
+ *   - DefaultChunkWriter::write_chunk                    src/chunk.rs:306-323
+ *   - ReadableDataChunk::read_data (exact-N read, byte order, bool rule)
+ *                                                        src/chunk.rs:103-116,163-222
+ *   - WriteableDataChunk::write_data                     src/chunk.rs:118-140,169-237
+ *
+ * Semantics kept from the reference (see DESIGN.md "Parity contract"):
+ *   - decode produces EXACTLY num_elements*elem_size bytes (read_exact,
+ *     chunk.rs:112-113): a longer stream is truncated silently, a shorter one
+ *     is ZCG_ERR_UNEXPECTED_EOF (tests.rs:191-219).
+ *   - big-endian dtypes are byte-swapped per element (byteorder read_*_into);
+ *     single-byte types and bool ignore endianness (data_type.rs:425-432).
+ *   - bool: decoded byte != 0 -> 1 (chunk.rs:175-190).
+ *   - encode requires the element count to equal product(chunk_shape)
+ *     (chunk.rs:309-318) -> ZCG_ERR_INVALID_DATA otherwise.
+ *   - only the first gzip member / LZ4 frame / xz stream / bzip2 stream is
+ *     decoded (single-stream decoders of flate2/lz4-rs/xz2/bzip2).
+ *
+ * Threading: one zcg_ctx per device; a ctx is not shared across host threads
+ * without external locking.  Work on distinct streams is independent.
+ */
+#ifndef ZCHUNK_GPU_H
+#define ZCHUNK_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ZCG_ABI_VERSION 1
+
+/* CompressionType variants (src/compression/mod.rs:40-51).  Numbering is
+ * this ABI's own; the JSON codec ids are mapped by the host layer. */
+enum zcg_codec {
+    ZCG_CODEC_RAW = 0,   /* raw.rs:13-24 */
+    ZCG_CODEC_BZIP2 = 1, /* bzip.rs:16-46 */
+    ZCG_CODEC_GZIP = 2,  /* gzip.rs:16-57 */
+    ZCG_CODEC_LZ4 = 3,   /* lz.rs:45-93 */
+    ZCG_CODEC_XZ = 4     /* xz.rs:15-43 */
+};
+
+/* Per-chunk status words; map 1:1 onto std::io::ErrorKind of the reference. */
+enum zcg_status {
+    ZCG_OK = 0,
+    ZCG_ERR_UNEXPECTED_EOF = 1, /* io::ErrorKind::UnexpectedEof (short stream) */
+    ZCG_ERR_INVALID_DATA = 2,   /* corrupt stream / wrong element count        */
+    ZCG_ERR_INVALID_INPUT = 3,  /* dtype mismatch (chunk.rs:261-264), bad args */
+    ZCG_ERR_UNSUPPORTED = 4,    /* e.g. LZ4 dictionary frames                  */
+    ZCG_ERR_OUTPUT_TOO_SMALL = 5, /* encode: dst capacity below the stream size */
+    ZCG_ERR_RUNTIME = 100       /* HIP runtime failure (see zcg_last_error)     */
+};
+
+/* Decode verification flags (zcg_compression.flags).  The reference's
+ * read_exact never reaches the gzip trailer / LZ4 content checksum on a
+ * full-length read, so these default OFF. */
+#define ZCG_FLAG_VERIFY_GZIP_CRC 0x1u
+#define ZCG_FLAG_VERIFY_LZ4_CONTENT_CHECKSUM 0x2u
+#define ZCG_FLAG_SKIP_LZ4_BLOCK_CHECKSUM 0x4u
+
+/* CompressionType + its configuration (camelCase JSON keys in the reference). */
+typedef struct zcg_compression {
+    int32_t codec;            /* enum zcg_codec                                 */
+    int32_t gzip_level;       /* gzip.rs:16-20, -1 / out of [0,9] -> 6 (28-34)  */
+    int32_t lz4_block_size;   /* lz.rs:45-50, rounded to 64K/256K/1M/4M (55-65) */
+    int32_t bzip2_block_size; /* bzip.rs:16-21, 1..9                            */
+    int32_t xz_preset;        /* xz.rs:15-20                                    */
+    uint32_t flags;           /* ZCG_FLAG_*                                     */
+} zcg_compression;
+
+/* Effective element type (data_type.rs:417-432). */
+typedef struct zcg_dtype {
+    uint8_t elem_size;  /* 1, 2, 4 or 8 */
+    uint8_t big_endian; /* 1 for '>' types of size > 1 */
+    uint8_t is_bool;    /* 1 for "bool" */
+    uint8_t reserved;
+} zcg_dtype;
+
+/* What one batch shares: the array's codec, dtype and chunk element count
+ * (ArrayMetadata, lib.rs:382-402; get_chunk_num_elements lib.rs:474-480). */
+typedef struct zcg_array {
+    zcg_compression compression;
+    zcg_dtype dtype;
+    uint64_t chunk_num_elements;
+} zcg_array;
+
+/* One chunk of a batch.  All pointers are DEVICE pointers, caller-owned.
+ *  decode: src = compressed stream (src_len bytes), dst = N*elem_size bytes
+ *  encode: src = N*elem_size bytes of native (little-endian) elements,
+ *          dst = output buffer of capacity dst_cap bytes                  */
+typedef struct zcg_chunk {
+    const void* src;
+    uint64_t src_len;
+    void* dst;
+    uint64_t dst_cap;
+} zcg_chunk;
+
+typedef struct zcg_ctx zcg_ctx;
+
+/* ---- context -------------------------------------------------------- */
+int zcg_abi_version(void);
+zcg_ctx* zcg_create(int device);
+void zcg_destroy(zcg_ctx* ctx);
+const char* zcg_last_error(const zcg_ctx* ctx);
+/* Effective parameters the reference would use (gzip.rs:28-34, lz.rs:55-65). */
+int32_t zcg_effective_gzip_level(int32_t level);
+int32_t zcg_effective_lz4_block_size(int32_t block_size);
+int zcg_codec_on_gpu(int32_t codec, int encode);
+
+/* ---- device-resident batch API (the hot path) ------------------------
+ * Replaces N calls of DefaultChunk::read_chunk_into (chunk.rs:288-301) with
+ * one batched, stream-ordered launch sequence.  `d_chunks` and `d_status`
+ * are device arrays of n entries.  Asynchronous on `stream`; returns a
+ * zcg_status for argument/launch errors only — per-chunk results land in
+ * d_status.  Workspace is grown on first use of a given batch shape
+ * (hipMalloc), so steady-state calls do no allocation and are capturable. */
+int zcg_decode_batch(zcg_ctx* ctx, const zcg_array* array, const zcg_chunk* d_chunks,
+                     uint32_t n, int32_t* d_status, void* stream);
+
+/* Replaces N calls of DefaultChunk::write_chunk (chunk.rs:306-323).
+ * d_out_len[i] receives the encoded stream length of chunk i. */
+int zcg_encode_batch(zcg_ctx* ctx, const zcg_array* array, const zcg_chunk* d_chunks,
+                     uint32_t n, uint64_t* d_out_len, int32_t* d_status, void* stream);
+
+/* Upper bound of an encoded chunk of `src_len` bytes for this codec. */
+uint64_t zcg_encode_bound(const zcg_compression* c, uint64_t src_len);
+
+/* Bytes of device workspace a batch of this shape needs (informational). */
+uint64_t zcg_workspace_bytes(const zcg_array* array, uint32_t n, int encode);
+
+/* ---- host-memory conveniences (one read_chunk / write_chunk) ---------
+ * zcg_read_chunk == DefaultChunkReader::read_chunk body (chunk.rs:270-286)
+ * on host buffers: H2D of the stream, GPU decode, D2H of the elements.
+ * `dst` receives N*elem_size bytes (host-native order). */
+int zcg_read_chunk(zcg_ctx* ctx, const zcg_array* array, const void* src, uint64_t src_len,
+                   void* dst);
+/* zcg_write_chunk == DefaultChunkWriter::write_chunk (chunk.rs:306-323):
+ * `n_elements` must equal array->chunk_num_elements (else INVALID_DATA). */
+int zcg_write_chunk(zcg_ctx* ctx, const zcg_array* array, const void* elems,
+                    uint64_t n_elements, void* out, uint64_t out_cap, uint64_t* out_len);
+
+/* Host-resident batch (e2e path): pinned staging, H2D, decode, D2H.
+ * srcs/src_lens/dsts/status are host arrays of n entries. */
+int zcg_read_chunks_host(zcg_ctx* ctx, const zcg_array* array, uint32_t n,
+                         const void* const* srcs, const uint64_t* src_lens, void* const* dsts,
+                         int32_t* status);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* ZCHUNK_GPU_H */

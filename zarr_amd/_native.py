@@ -1,0 +1,147 @@
+"""ctypes binding of ``libzchunk_gpu.so`` (C ABI: ``include/zchunk_gpu.h``).
+
+The product path has no CPU fallback: if the HIP library is missing or no
+GPU is visible, every compute call raises :class:`NativeUnavailable`.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libzchunk_gpu.so")
+
+OK, UNEXPECTED_EOF, INVALID_DATA, INVALID_INPUT, UNSUPPORTED, OUTPUT_TOO_SMALL = 0, 1, 2, 3, 4, 5
+RUNTIME = 100
+
+FLAG_VERIFY_GZIP_CRC = 0x1
+FLAG_VERIFY_LZ4_CONTENT_CHECKSUM = 0x2
+FLAG_SKIP_LZ4_BLOCK_CHECKSUM = 0x4
+
+STATUS_NAMES = {OK: "Ok", UNEXPECTED_EOF: "UnexpectedEof", INVALID_DATA: "InvalidData",
+                INVALID_INPUT: "InvalidInput", UNSUPPORTED: "Unsupported",
+                OUTPUT_TOO_SMALL: "OutputTooSmall", RUNTIME: "Runtime"}
+
+EXPORTED_SYMBOLS = (
+    "zcg_abi_version", "zcg_create", "zcg_destroy", "zcg_last_error",
+    "zcg_effective_gzip_level", "zcg_effective_lz4_block_size", "zcg_codec_on_gpu",
+    "zcg_decode_batch", "zcg_encode_batch", "zcg_encode_bound", "zcg_workspace_bytes",
+    "zcg_read_chunk", "zcg_write_chunk", "zcg_read_chunks_host",
+)
+
+
+class NativeUnavailable(RuntimeError):
+    pass
+
+
+class Compression(ctypes.Structure):
+    _fields_ = [("codec", ctypes.c_int32), ("gzip_level", ctypes.c_int32),
+                ("lz4_block_size", ctypes.c_int32), ("bzip2_block_size", ctypes.c_int32),
+                ("xz_preset", ctypes.c_int32), ("flags", ctypes.c_uint32)]
+
+
+class DType(ctypes.Structure):
+    _fields_ = [("elem_size", ctypes.c_uint8), ("big_endian", ctypes.c_uint8),
+                ("is_bool", ctypes.c_uint8), ("reserved", ctypes.c_uint8)]
+
+
+class Array(ctypes.Structure):
+    _fields_ = [("compression", Compression), ("dtype", DType),
+                ("chunk_num_elements", ctypes.c_uint64)]
+
+
+class Chunk(ctypes.Structure):
+    _fields_ = [("src", ctypes.c_void_p), ("src_len", ctypes.c_uint64),
+                ("dst", ctypes.c_void_p), ("dst_cap", ctypes.c_uint64)]
+
+
+assert ctypes.sizeof(Compression) == 24 and ctypes.sizeof(Array) == 40
+assert ctypes.sizeof(Chunk) == 32
+
+_lib = None
+_lock = threading.Lock()
+
+
+def load_library(path: str = LIB_PATH):
+    """Load the HIP library (without touching the GPU)."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(path):
+            raise NativeUnavailable(
+                f"{path} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+        try:  # share torch's HIP runtime when torch is present (one libamdhip64 per process)
+            import torch  # noqa: F401
+        except Exception:
+            pass
+        L = ctypes.CDLL(path)
+        vp, u32, u64, i32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int32
+        L.zcg_abi_version.restype = ctypes.c_int
+        L.zcg_create.argtypes = [ctypes.c_int]
+        L.zcg_create.restype = vp
+        L.zcg_destroy.argtypes = [vp]
+        L.zcg_last_error.argtypes = [vp]
+        L.zcg_last_error.restype = ctypes.c_char_p
+        L.zcg_effective_gzip_level.argtypes = [i32]
+        L.zcg_effective_gzip_level.restype = i32
+        L.zcg_effective_lz4_block_size.argtypes = [i32]
+        L.zcg_effective_lz4_block_size.restype = i32
+        L.zcg_codec_on_gpu.argtypes = [i32, ctypes.c_int]
+        L.zcg_codec_on_gpu.restype = ctypes.c_int
+        L.zcg_decode_batch.argtypes = [vp, ctypes.POINTER(Array), vp, u32, vp, vp]
+        L.zcg_decode_batch.restype = ctypes.c_int
+        L.zcg_encode_batch.argtypes = [vp, ctypes.POINTER(Array), vp, u32, vp, vp, vp]
+        L.zcg_encode_batch.restype = ctypes.c_int
+        L.zcg_encode_bound.argtypes = [ctypes.POINTER(Compression), u64]
+        L.zcg_encode_bound.restype = u64
+        L.zcg_workspace_bytes.argtypes = [ctypes.POINTER(Array), u32, ctypes.c_int]
+        L.zcg_workspace_bytes.restype = u64
+        L.zcg_read_chunk.argtypes = [vp, ctypes.POINTER(Array), vp, u64, vp]
+        L.zcg_read_chunk.restype = ctypes.c_int
+        L.zcg_write_chunk.argtypes = [vp, ctypes.POINTER(Array), vp, u64, vp, u64,
+                                      ctypes.POINTER(u64)]
+        L.zcg_write_chunk.restype = ctypes.c_int
+        L.zcg_read_chunks_host.argtypes = [vp, ctypes.POINTER(Array), u32, vp, vp, vp, vp]
+        L.zcg_read_chunks_host.restype = ctypes.c_int
+        _lib = L
+        return L
+
+
+class Context:
+    """One ``zcg_ctx`` (one GPU)."""
+
+    def __init__(self, device: int = 0):
+        self.lib = load_library()
+        self.device = device
+        self.handle = self.lib.zcg_create(device)
+        if not self.handle:
+            raise NativeUnavailable(f"zcg_create({device}) failed: no HIP device visible")
+
+    def last_error(self) -> str:
+        return (self.lib.zcg_last_error(self.handle) or b"").decode()
+
+    def close(self):
+        if self.handle:
+            self.lib.zcg_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+_contexts = {}
+
+
+def context(device: int = 0) -> Context:
+    with _lock:
+        ctx = _contexts.get(device)
+    if ctx is None:
+        ctx = Context(device)
+        with _lock:
+            _contexts[device] = ctx
+    return ctx

@@ -1,0 +1,286 @@
+// zcg_api.cpp — C ABI of include/zchunk_gpu.h: context, dispatch by
+// CompressionType (the reference's `match *self` in
+// src/compression/mod.rs:72-108), workspace, and the host-memory
+// conveniences that implement one DefaultChunk::read_chunk / write_chunk
+// (src/chunk.rs:270-323) around the device batch kernels.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "zcg_common.h"
+
+using namespace zcg;
+
+struct zcg_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;  // internal stream of the host conveniences
+    std::string err;
+    void* ws = nullptr;  // device workspace of the batch kernels
+    size_t ws_bytes = 0;
+    // host-convenience staging
+    void* d_buf = nullptr;
+    size_t d_buf_bytes = 0;
+    void* h_pin = nullptr;
+    size_t h_pin_bytes = 0;
+};
+
+namespace {
+
+int fail(zcg_ctx* ctx, hipError_t e, const char* what) {
+    if (ctx) {
+        ctx->err = std::string(what) + ": " + hipGetErrorString(e);
+    }
+    return ZCG_ERR_RUNTIME;
+}
+
+bool dtype_ok(const zcg_dtype& d) {
+    if (d.is_bool) return d.elem_size == 1;
+    return d.elem_size == 1 || d.elem_size == 2 || d.elem_size == 4 || d.elem_size == 8;
+}
+
+int ensure_dev(zcg_ctx* ctx, void** p, size_t* have, size_t need) {
+    if (*have >= need && *p) return ZCG_OK;
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    *have = 0;
+    size_t sz = need < 4096 ? 4096 : need;
+    hipError_t e = hipMalloc(p, sz);
+    if (e != hipSuccess) return fail(ctx, e, "hipMalloc");
+    *have = sz;
+    return ZCG_OK;
+}
+
+int ensure_pin(zcg_ctx* ctx, size_t need) {
+    if (ctx->h_pin_bytes >= need && ctx->h_pin) return ZCG_OK;
+    if (ctx->h_pin) (void)hipHostFree(ctx->h_pin);
+    ctx->h_pin = nullptr;
+    ctx->h_pin_bytes = 0;
+    size_t sz = need < 4096 ? 4096 : need;
+    hipError_t e = hipHostMalloc(&ctx->h_pin, sz, hipHostMallocDefault);
+    if (e != hipSuccess) return fail(ctx, e, "hipHostMalloc");
+    ctx->h_pin_bytes = sz;
+    return ZCG_OK;
+}
+
+size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+}  // namespace
+
+extern "C" {
+
+int zcg_abi_version(void) { return ZCG_ABI_VERSION; }
+
+zcg_ctx* zcg_create(int device) {
+    int cnt = 0;
+    if (hipGetDeviceCount(&cnt) != hipSuccess || device < 0 || device >= cnt) return nullptr;
+    zcg_ctx* ctx = new zcg_ctx();
+    ctx->device = device;
+    (void)hipSetDevice(device);
+    if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete ctx;
+        return nullptr;
+    }
+    return ctx;
+}
+
+void zcg_destroy(zcg_ctx* ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->ws) (void)hipFree(ctx->ws);
+    if (ctx->d_buf) (void)hipFree(ctx->d_buf);
+    if (ctx->h_pin) (void)hipHostFree(ctx->h_pin);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+const char* zcg_last_error(const zcg_ctx* ctx) { return ctx ? ctx->err.c_str() : "no context"; }
+
+int32_t zcg_effective_gzip_level(int32_t level) { return (level < 0 || level > 9) ? 6 : level; }
+
+int32_t zcg_effective_lz4_block_size(int32_t bs) {
+    if (bs <= 65536) return 65536;
+    if (bs <= 262144) return 262144;
+    if (bs <= 1048576) return 1048576;
+    return 4194304;
+}
+
+int zcg_codec_on_gpu(int32_t codec, int encode) {
+    switch (codec) {
+    case ZCG_CODEC_RAW: return 1;
+    case ZCG_CODEC_LZ4: return encode ? 0 : 1;
+    case ZCG_CODEC_GZIP: return encode ? 0 : 1;
+    default: return 0;
+    }
+}
+
+uint64_t zcg_encode_bound(const zcg_compression* c, uint64_t n) {
+    switch (c->codec) {
+    case ZCG_CODEC_RAW: return n;
+    case ZCG_CODEC_GZIP:  // stored-block worst case + header/trailer
+        return n + 5 * (n / 16383 + 1) + 18 + 64;
+    case ZCG_CODEC_LZ4: {
+        const uint64_t b = (uint64_t)zcg_effective_lz4_block_size(c->lz4_block_size);
+        return 15 + (n / b + 1) * (b + 8) + 8;
+    }
+    default: return n + n / 8 + 65536;
+    }
+}
+
+uint64_t zcg_workspace_bytes(const zcg_array* a, uint32_t n, int encode) {
+    (void)a; (void)n; (void)encode;
+    return 0;
+}
+
+int zcg_decode_batch(zcg_ctx* ctx, const zcg_array* a, const zcg_chunk* d_chunks, uint32_t n,
+                     int32_t* d_status, void* stream) {
+    if (!ctx || !a || (n && (!d_chunks || !d_status))) return ZCG_ERR_INVALID_INPUT;
+    if (!dtype_ok(a->dtype)) return ZCG_ERR_INVALID_INPUT;
+    if (n == 0) return ZCG_OK;
+    (void)hipSetDevice(ctx->device);
+    hipStream_t s = (hipStream_t)stream;
+    hipError_t e;
+    switch (a->compression.codec) {
+    case ZCG_CODEC_RAW: e = launch_raw(a, d_chunks, n, d_status, nullptr, 0, s); break;
+    case ZCG_CODEC_LZ4: e = launch_lz4_decode(a, d_chunks, n, d_status, s); break;
+    case ZCG_CODEC_GZIP: e = launch_inflate(a, d_chunks, n, d_status, s); break;
+    case ZCG_CODEC_BZIP2:
+    case ZCG_CODEC_XZ:
+        ctx->err = "codec has no GPU decoder in this build";
+        return ZCG_ERR_UNSUPPORTED;
+    default: return ZCG_ERR_INVALID_INPUT;
+    }
+    if (e != hipSuccess) return fail(ctx, e, "decode launch");
+    return ZCG_OK;
+}
+
+int zcg_encode_batch(zcg_ctx* ctx, const zcg_array* a, const zcg_chunk* d_chunks, uint32_t n,
+                     uint64_t* d_out_len, int32_t* d_status, void* stream) {
+    if (!ctx || !a || (n && (!d_chunks || !d_status || !d_out_len))) return ZCG_ERR_INVALID_INPUT;
+    if (!dtype_ok(a->dtype)) return ZCG_ERR_INVALID_INPUT;
+    if (n == 0) return ZCG_OK;
+    (void)hipSetDevice(ctx->device);
+    hipStream_t s = (hipStream_t)stream;
+    hipError_t e;
+    switch (a->compression.codec) {
+    case ZCG_CODEC_RAW: e = launch_raw(a, d_chunks, n, d_status, d_out_len, 1, s); break;
+    default:
+        ctx->err = "codec has no GPU encoder in this build";
+        return ZCG_ERR_UNSUPPORTED;
+    }
+    if (e != hipSuccess) return fail(ctx, e, "encode launch");
+    return ZCG_OK;
+}
+
+int zcg_read_chunks_host(zcg_ctx* ctx, const zcg_array* a, uint32_t n, const void* const* srcs,
+                         const uint64_t* src_lens, void* const* dsts, int32_t* status) {
+    if (!ctx || !a) return ZCG_ERR_INVALID_INPUT;
+    if (!dtype_ok(a->dtype)) return ZCG_ERR_INVALID_INPUT;
+    if (n == 0) return ZCG_OK;
+    (void)hipSetDevice(ctx->device);
+    const uint64_t D = a->chunk_num_elements * (uint64_t)a->dtype.elem_size;
+    // device layout: [desc n][status n][src blobs (256-aligned)][dst n*D]
+    size_t off_desc = 0;
+    size_t off_stat = align_up(off_desc + sizeof(zcg_chunk) * n, 256);
+    size_t off_src = align_up(off_stat + sizeof(int32_t) * n, 256);
+    std::vector<size_t> so(n);
+    size_t p = off_src;
+    for (uint32_t i = 0; i < n; i++) { so[i] = p; p = align_up(p + src_lens[i], 256); }
+    size_t off_dst = p;
+    size_t total = align_up(off_dst + (size_t)D * n, 256);
+    int r = ensure_dev(ctx, &ctx->d_buf, &ctx->d_buf_bytes, total);
+    if (r) return r;
+    r = ensure_pin(ctx, total);
+    if (r) return r;
+    uint8_t* hp = (uint8_t*)ctx->h_pin;
+    uint8_t* dp = (uint8_t*)ctx->d_buf;
+    zcg_chunk* hd = (zcg_chunk*)(hp + off_desc);
+    for (uint32_t i = 0; i < n; i++) {
+        memcpy(hp + so[i], srcs[i], src_lens[i]);
+        hd[i].src = dp + so[i];
+        hd[i].src_len = src_lens[i];
+        hd[i].dst = dp + off_dst + (size_t)D * i;
+        hd[i].dst_cap = D;
+    }
+    hipError_t e = hipMemcpyAsync(dp, hp, off_dst, hipMemcpyHostToDevice, ctx->stream);
+    if (e != hipSuccess) return fail(ctx, e, "H2D");
+    r = zcg_decode_batch(ctx, a, (const zcg_chunk*)(dp + off_desc), n, (int32_t*)(dp + off_stat),
+                         ctx->stream);
+    if (r) return r;
+    e = hipMemcpyAsync(hp + off_stat, dp + off_stat, sizeof(int32_t) * n, hipMemcpyDeviceToHost,
+                       ctx->stream);
+    if (e == hipSuccess && D)
+        e = hipMemcpyAsync(hp + off_dst, dp + off_dst, (size_t)D * n, hipMemcpyDeviceToHost,
+                           ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess) return fail(ctx, e, "D2H");
+    const int32_t* hs = (const int32_t*)(hp + off_stat);
+    for (uint32_t i = 0; i < n; i++) {
+        status[i] = hs[i];
+        if (hs[i] == ZCG_OK && D) memcpy(dsts[i], hp + off_dst + (size_t)D * i, D);
+    }
+    return ZCG_OK;
+}
+
+int zcg_read_chunk(zcg_ctx* ctx, const zcg_array* a, const void* src, uint64_t src_len,
+                   void* dst) {
+    int32_t st = ZCG_OK;
+    void* const dsts[1] = {dst};
+    const void* const srcs[1] = {src};
+    int r = zcg_read_chunks_host(ctx, a, 1, srcs, &src_len, dsts, &st);
+    return r ? r : st;
+}
+
+int zcg_write_chunk(zcg_ctx* ctx, const zcg_array* a, const void* elems, uint64_t n_elements,
+                    void* out, uint64_t out_cap, uint64_t* out_len) {
+    if (!ctx || !a || !out_len) return ZCG_ERR_INVALID_INPUT;
+    *out_len = 0;
+    if (!dtype_ok(a->dtype)) return ZCG_ERR_INVALID_INPUT;
+    if (n_elements != a->chunk_num_elements) return ZCG_ERR_INVALID_DATA;  // chunk.rs:309-318
+    if (!zcg_codec_on_gpu(a->compression.codec, 1)) {
+        ctx->err = "codec has no GPU encoder in this build";
+        return ZCG_ERR_UNSUPPORTED;
+    }
+    (void)hipSetDevice(ctx->device);
+    const uint64_t nb = n_elements * (uint64_t)a->dtype.elem_size;
+    const uint64_t cap = zcg_encode_bound(&a->compression, nb);
+    // device layout: [desc][status][out_len][src nb][dst cap]
+    size_t off_stat = 256, off_len = 512, off_src = 1024;
+    size_t off_dst = align_up(off_src + nb, 256);
+    size_t total = align_up(off_dst + cap, 256);
+    int r = ensure_dev(ctx, &ctx->d_buf, &ctx->d_buf_bytes, total);
+    if (r) return r;
+    r = ensure_pin(ctx, total);
+    if (r) return r;
+    uint8_t* hp = (uint8_t*)ctx->h_pin;
+    uint8_t* dp = (uint8_t*)ctx->d_buf;
+    zcg_chunk* hd = (zcg_chunk*)hp;
+    hd->src = dp + off_src;
+    hd->src_len = nb;
+    hd->dst = dp + off_dst;
+    hd->dst_cap = cap;
+    memcpy(hp + off_src, elems, nb);
+    hipError_t e = hipMemcpyAsync(dp, hp, off_dst, hipMemcpyHostToDevice, ctx->stream);
+    if (e != hipSuccess) return fail(ctx, e, "H2D");
+    r = zcg_encode_batch(ctx, a, (const zcg_chunk*)dp, 1, (uint64_t*)(dp + off_len),
+                         (int32_t*)(dp + off_stat), ctx->stream);
+    if (r) return r;
+    e = hipMemcpyAsync(hp + off_stat, dp + off_stat, off_src - off_stat, hipMemcpyDeviceToHost,
+                       ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess) return fail(ctx, e, "D2H");
+    const int32_t st = *(int32_t*)(hp + off_stat);
+    const uint64_t len = *(uint64_t*)(hp + off_len);
+    if (st != ZCG_OK) return st;
+    if (len > out_cap) return ZCG_ERR_OUTPUT_TOO_SMALL;
+    e = hipMemcpy(out, dp + off_dst, len, hipMemcpyDeviceToHost);
+    if (e != hipSuccess) return fail(ctx, e, "D2H");
+    *out_len = len;
+    return ZCG_OK;
+}
+
+}  // extern "C"
