@@ -187,6 +187,15 @@ static int zr_gzip_header(const uint8_t* s, uint64_t n, uint64_t* hdr_len) {
     return ZR_OK;
 }
 
+/* flate2 read::GzDecoder = bufread::GzDecoder over BufReader::with_capacity
+ * (32 KiB, r): the header is consumed from the buffered reader, then
+ * zio::read hands zlib whatever fill_buf() returns (the rest of the current
+ * 32 KiB window of the stream) with the remaining destination; read_exact
+ * repeats until N bytes exist.  zlib keeps decoding the next symbol(s) after
+ * the output is full as long as their bits are in the current window (LEN ->
+ * LIT/MATCH leave only on `left == 0`), so a corrupt code right after byte N
+ * is still an error in the reference: the windows are restated exactly. */
+#define ZR_BUFREADER 32768u
 static int zr_decode_gzip(const uint8_t* src, uint64_t n, uint8_t* dst, uint64_t dlen,
                           int verify_crc) {
     uint64_t h = 0;
@@ -195,94 +204,141 @@ static int zr_decode_gzip(const uint8_t* src, uint64_t n, uint8_t* dst, uint64_t
     z_stream z;
     memset(&z, 0, sizeof z);
     if (inflateInit2(&z, -15) != Z_OK) return ZR_INVALID_DATA;
-    z.next_in = (Bytef*)(src + h);
-    z.avail_in = (uInt)(n - h);
-    z.next_out = dst;
-    z.avail_out = (uInt)dlen;
-    int r = inflate(&z, Z_NO_FLUSH);
-    uint64_t got = dlen - z.avail_out;
-    uint64_t used = h + (n - h - z.avail_in);
-    inflateEnd(&z);
-    if (got == dlen) {
-        if (verify_crc && r == Z_STREAM_END) {
-            if (used + 8 > n) return ZR_EOF;
-            uint32_t c = (uint32_t)crc32(0L, dst, (uInt)dlen);
-            uint32_t sc = src[used] | (src[used + 1] << 8) | (src[used + 2] << 16) |
-                          ((uint32_t)src[used + 3] << 24);
-            if (c != sc) return ZR_INVALID_DATA;
-        }
-        return ZR_OK;
+    uint64_t pos = h, got = 0;
+    int r = Z_OK;
+    while (got < dlen) {
+        if (pos >= n) { r = Z_BUF_ERROR; break; }               /* eof: read() -> 0 */
+        uint64_t wend = (pos / ZR_BUFREADER + 1) * ZR_BUFREADER;  /* fill_buf() */
+        if (wend > n) wend = n;
+        z.next_in = (Bytef*)(src + pos);
+        z.avail_in = (uInt)(wend - pos);
+        z.next_out = dst + got;
+        z.avail_out = (uInt)(dlen - got);
+        r = inflate(&z, Z_NO_FLUSH);
+        uint64_t used = (wend - pos) - z.avail_in;
+        pos += used;
+        got = dlen - z.avail_out;
+        if (r == Z_STREAM_END) break;
+        if (r != Z_OK && r != Z_BUF_ERROR) break;
     }
-    /* fewer than N bytes: stream end (flate2 then reads the trailer and
-     * read() returns 0) or input exhausted -> read_exact UnexpectedEof */
-    if (r == Z_STREAM_END || r == Z_BUF_ERROR || r == Z_OK) return ZR_EOF;
-    return ZR_INVALID_DATA;
+    inflateEnd(&z);
+    if (r != Z_OK && r != Z_BUF_ERROR && r != Z_STREAM_END) return ZR_INVALID_DATA;
+    if (got < dlen) return ZR_EOF;
+    if (verify_crc && r == Z_STREAM_END) {
+        if (pos + 8 > n) return ZR_EOF;
+        uint32_t c = (uint32_t)crc32(0L, dst, (uInt)dlen);
+        uint32_t sc = src[pos] | (src[pos + 1] << 8) | (src[pos + 2] << 16) |
+                      ((uint32_t)src[pos + 3] << 24);
+        if (c != sc) return ZR_INVALID_DATA;
+    }
+    return ZR_OK;
 }
 
 /* ---------------- Lz4 decode: lz4-rs Decoder (LZ4F_decompress) -------- */
+/* lz4-rs 1.23 Decoder: a 32 KiB buffer refilled with min(32 KiB, next)
+ * bytes, where `next` starts at 11 and tracks LZ4F_decompress's size hint;
+ * read() returns as soon as it produced output, read_exact loops.  So LZ4F
+ * only ever sees the bytes its hint asked for: the content checksum after
+ * the end mark is never fed on an exact-N read, while the next block header
+ * usually is (it rides with the last piece of the block). */
 static int zr_decode_lz4(const uint8_t* src, uint64_t n, uint8_t* dst, uint64_t dlen) {
     LZ4F_dctx* d = NULL;
     if (LZ4F_isError(LZ4F_createDecompressionContext(&d, LZ4F_VERSION))) return ZR_INVALID_DATA;
-    uint64_t in = 0, out = 0;
+    uint64_t rpos = 0;                 /* reader position in src */
+    uint64_t pos = 0, len = 0;         /* lz4-rs buf window [pos, len) */
+    const uint8_t* buf = NULL;
+    size_t next = 11;
+    uint64_t out = 0;
     int st = ZR_OK;
-    while (out < dlen) {
-        size_t ds = dlen - out, ss = n - in;
-        size_t r = LZ4F_decompress(d, dst + out, &ds, src + in, &ss, NULL);
-        if (LZ4F_isError(r)) { st = ZR_INVALID_DATA; break; }
-        in += ss;
-        out += ds;
-        if (r == 0) { /* frame complete: lz4-rs then returns 0 -> read_exact EOF */
-            if (out < dlen) st = ZR_EOF;
-            break;
+    while (out < dlen && st == ZR_OK) {       /* read_exact -> read() */
+        if (next == 0) { st = ZR_EOF; break; }  /* frame finished: read() -> 0 */
+        uint64_t dst_off = 0;
+        while (dst_off == 0) {
+            if (pos >= len) {
+                size_t need = next < 32768 ? next : 32768;
+                uint64_t k = (n - rpos) < need ? (n - rpos) : need;
+                if (k == 0) break;          /* reader eof: read() returns 0 */
+                buf = src + rpos;
+                rpos += k;
+                pos = 0;
+                len = k;
+                next -= k;
+            }
+            while (out + dst_off < dlen && pos < len) {
+                size_t ss = len - pos, ds = dlen - out - dst_off;
+                size_t r = LZ4F_decompress(d, dst + out + dst_off, &ds, buf + pos, &ss, NULL);
+                if (LZ4F_isError(r)) { st = ZR_INVALID_DATA; break; }
+                pos += ss;
+                dst_off += ds;
+                if (r == 0) { next = 0; break; }
+                if (next < r) next = r;
+            }
+            if (st != ZR_OK || next == 0) break;
         }
-        if (ss == 0 && ds == 0) { st = ZR_EOF; break; }
+        if (st != ZR_OK) break;
+        if (dst_off == 0) { st = ZR_EOF; break; }
+        out += dst_off;
     }
     LZ4F_freeDecompressionContext(d);
     return st;
 }
 
-/* ---------------- Bzip2 decode: bzip2 BzDecoder ----------------------- */
+/* ---------------- Bzip2 decode: bzip2 read::BzDecoder -----------------
+ * bufread::BzDecoder over BufReader::with_capacity(32 KiB): libbz2 is handed
+ * the current 32 KiB window of the stream and the remaining destination.
+ * (libbz2 verifies a block CRC and decodes the next block header/tables as
+ * soon as a block's output completes, even with the output full — the
+ * windowed feeding decides how much of that it can see.) */
 static int zr_decode_bzip2(const uint8_t* src, uint64_t n, uint8_t* dst, uint64_t dlen) {
     bz_stream b;
     memset(&b, 0, sizeof b);
     if (BZ2_bzDecompressInit(&b, 0, 0) != BZ_OK) return ZR_INVALID_DATA;
-    b.next_in = (char*)src;
-    b.avail_in = (unsigned)n;
-    b.next_out = (char*)dst;
-    b.avail_out = (unsigned)dlen;
+    uint64_t pos = 0, got = 0;
     int st = ZR_OK;
-    for (;;) {
+    while (got < dlen) {
+        if (pos >= n) { st = ZR_EOF; break; }
+        uint64_t wend = (pos / ZR_BUFREADER + 1) * ZR_BUFREADER;
+        if (wend > n) wend = n;
+        b.next_in = (char*)(src + pos);
+        b.avail_in = (unsigned)(wend - pos);
+        b.next_out = (char*)(dst + got);
+        b.avail_out = (unsigned)(dlen - got);
         int r = BZ2_bzDecompress(&b);
-        if (r == BZ_STREAM_END) { if (b.avail_out) st = ZR_EOF; break; }
+        pos += (wend - pos) - b.avail_in;
+        got = dlen - b.avail_out;
+        if (r == BZ_STREAM_END) { if (got < dlen) st = ZR_EOF; break; }
         if (r != BZ_OK) { st = ZR_INVALID_DATA; break; }
-        if (b.avail_out == 0) break;
-        if (b.avail_in == 0) { st = ZR_EOF; break; }
     }
     BZ2_bzDecompressEnd(&b);
     return st;
 }
 
-/* ---------------- Xz decode: xz2 XzDecoder (stream decoder, CRC64) ---- */
+/* ---------------- Xz decode: xz2 read::XzDecoder (stream decoder) ------
+ * bufread::XzDecoder over BufReader::with_capacity(32 KiB), stream decoder
+ * with memlimit u64::MAX and no flags (single .xz stream, CRC64 checked by
+ * liblzma as blocks complete); same windowed feeding as above. */
 static int zr_decode_xz(const uint8_t* src, uint64_t n, uint8_t* dst, uint64_t dlen) {
     lzma_stream s;
     memset(&s, 0, sizeof s);
     if (lzma_stream_decoder(&s, UINT64_MAX, 0) != LZMA_OK) return ZR_INVALID_DATA;
-    s.next_in = src;
-    s.avail_in = n;
-    s.next_out = dst;
-    s.avail_out = dlen;
+    uint64_t pos = 0, got = 0;
     int st = ZR_OK;
-    for (;;) {
-        int r = lzma_code(&s, LZMA_RUN);
-        if (r == LZMA_STREAM_END) { if (s.avail_out) st = ZR_EOF; break; }
+    while (got < dlen) {
+        int eof = pos >= n;
+        uint64_t wend = eof ? n : (pos / ZR_BUFREADER + 1) * ZR_BUFREADER;
+        if (wend > n) wend = n;
+        s.next_in = src + pos;
+        s.avail_in = wend - pos;
+        s.next_out = dst + got;
+        s.avail_out = dlen - got;
+        int r = lzma_code(&s, eof ? LZMA_FINISH : LZMA_RUN);
+        uint64_t used = (wend - pos) - s.avail_in;
+        uint64_t made = (dlen - got) - s.avail_out;
+        pos += used;
+        got += made;
+        if (r == LZMA_STREAM_END) { if (got < dlen) st = ZR_EOF; break; }
         if (r != LZMA_OK) { st = (r == 10 /*BUF_ERROR*/) ? ZR_EOF : ZR_INVALID_DATA; break; }
-        if (s.avail_out == 0) break;
-        if (s.avail_in == 0) {
-            r = lzma_code(&s, LZMA_RUN);
-            if (r == LZMA_STREAM_END && s.avail_out == 0) break;
-            st = (r == LZMA_OK || r == 10) ? ZR_EOF : (r == LZMA_STREAM_END ? ZR_EOF : ZR_INVALID_DATA);
-            break;
-        }
+        if (eof && made == 0) { st = ZR_EOF; break; }
     }
     lzma_end(&s);
     return st;

@@ -314,3 +314,42 @@ def test_batch_api_device_resident(codec):
     out = packed.dst.cpu().numpy().reshape(packed.n, D)
     for i in range(packed.n):
         assert out[i].tobytes() == vals[i % n_unique].tobytes(), i
+
+
+def test_gzip_lookahead_after_n_bytes():
+    """zlib validates the symbols after byte N that lie in flate2's current
+    32 KiB input window: corruptions there must classify like the oracle."""
+    payload = rw(150000).tobytes()
+    s = gzip_wrap(deflate(payload, 6), payload)
+    rng = np.random.default_rng(11)
+    for D in (40000, 100001, 149999):
+        # find roughly where byte D is produced: scan corruptions in a band
+        for pos in rng.integers(12, len(s) - 8, 40):
+            bad = bytearray(s)
+            bad[int(pos)] ^= int(rng.integers(1, 256))
+            check("gzip", bytes(bad), "u1", D)
+    fixed = gzip_wrap(deflate(payload[:20000], 6, zlib.Z_FIXED), payload[:20000])
+    for pos in range(len(fixed) - 40, len(fixed) - 8):
+        for x in (0x01, 0x80, 0xFF):
+            bad = bytearray(fixed)
+            bad[pos] ^= x
+            check("gzip", bytes(bad), "u1", 20000)
+
+
+def test_lz4_next_header_after_n_bytes():
+    """LZ4F reads the block header that follows a block ending exactly at N."""
+    payload = rw(65536 * 3).tobytes()
+    st, s = zref.encode(zref.LZ4, 65536, np.frombuffer(payload, np.uint8))
+    hdr = 7
+    pos, blocks = hdr, []
+    while True:
+        bs = struct.unpack_from("<I", s, pos)[0]
+        blocks.append(pos)
+        if bs == 0:
+            break
+        pos += 4 + (bs & 0x7FFFFFFF)
+    for k in range(1, len(blocks)):
+        for val in (0x7FFFFFFF, 0x00010001, 0x80010000, 0):
+            bad = bytearray(s)
+            struct.pack_into("<I", bad, blocks[k], val)
+            check("lz4", bytes(bad), "u1", 65536 * k)

@@ -130,6 +130,7 @@ struct BitIn {
     u64 buf;      // bit buffer (LSB = next bit)
     u32 cnt;      // valid bits in buf
     u64 consumed; // bits consumed from the stream start
+    u64 limit;    // bits that may be consumed (input end, or look-ahead window end)
 };
 
 __device__ __forceinline__ void bi_refill(BitIn& b) {
@@ -148,6 +149,7 @@ __device__ __forceinline__ void bi_refill(BitIn& b) {
         b.pos += 4;
     }
 }
+__device__ __forceinline__ bool bi_has(const BitIn& b, u32 k) { return b.consumed + k <= b.limit; }
 __device__ __forceinline__ u32 bi_peek(BitIn& b, u32 k) { return (u32)(b.buf & ((1ull << k) - 1)); }
 __device__ __forceinline__ void bi_drop(BitIn& b, u32 k) {
     b.buf >>= k;
@@ -159,25 +161,6 @@ __device__ __forceinline__ u32 bi_bits(BitIn& b, u32 k) {  // k <= 32
     u32 v = bi_peek(b, k);
     bi_drop(b, k);
     return v;
-}
-__device__ __forceinline__ bool bi_overrun(const BitIn& b) { return b.consumed > b.n * 8; }
-
-// Canonical bit-serial decode for codes longer than the table width.
-__device__ u32 slow_decode(BitIn& b, const HuffLds* h, bool dist) {
-    int code = 0, first = 0, index = 0;
-    bi_refill(b);
-    for (int l = 1; l <= 15; l++) {
-        code |= (int)bi_peek(b, 1);
-        bi_drop(b, 1);
-        const int cnt = h->count[l];
-        if (code - cnt < first) return sym_entry(h->sym[index + (code - first)], l, dist) & 0x0FFFFFFFu;
-        index += cnt;
-        first += cnt;
-        first <<= 1;
-        code <<= 1;
-        if (b.cnt == 0) bi_refill(b);
-    }
-    return mk_entry(0, K_BAD, 0, 0);
 }
 
 struct InfOut {
@@ -232,6 +215,192 @@ __device__ __forceinline__ void put_match(InfOut& o, u32 len, u32 dist) {
     o.P = P + len;
 }
 
+// Result of a bit-level step: ok, ran out of bits (EOF in the main decode,
+// "zlib waits for input" in the look-ahead), or corrupt.
+enum : int { R_OK = 0, R_EXHAUSTED = 1, R_INVALID = 2 };
+
+// Decode one symbol: primary table, else canonical bit-serial decode.
+__device__ __forceinline__ int decode_sym(BitIn& b, const u32* tab, int tbits, const HuffLds* h,
+                                          bool dist, u32* out) {
+    bi_refill(b);
+    u32 e = __builtin_amdgcn_readfirstlane(tab[bi_peek(b, tbits)]);
+    u32 l = e >> 28;
+    if (l != 0) {
+        if (!bi_has(b, l)) return R_EXHAUSTED;
+        bi_drop(b, l);
+        *out = e;
+        return R_OK;
+    }
+    if (((e >> 24) & 15) == K_BAD) {  // unused slot of an incomplete (1-bit) code
+        if (!bi_has(b, 1)) return R_EXHAUSTED;
+        return R_INVALID;
+    }
+    int code = 0, first = 0, index = 0;
+    for (int len = 1; len <= 15; len++) {
+        if (!bi_has(b, 1)) return R_EXHAUSTED;
+        bi_refill(b);
+        code |= (int)bi_peek(b, 1);
+        bi_drop(b, 1);
+        const int cnt = h->count[len];
+        if (code - cnt < first) {
+            *out = sym_entry(h->sym[index + (code - first)], len, dist);
+            return R_OK;
+        }
+        index += cnt;
+        first += cnt;
+        first <<= 1;
+        code <<= 1;
+    }
+    return R_INVALID;
+}
+
+// Dynamic block header (RFC 1951 3.2.7) -> tables; zlib's validity rules.
+__device__ int read_dynamic(BitIn& b, u8* lens, HuffLds* lh, u32* ltab, HuffLds* dh, u32* dtab) {
+    const int lane = lane_id();
+    if (!bi_has(b, 14)) return R_EXHAUSTED;
+    const u32 nlen = bi_bits(b, 5) + 257, ndist = bi_bits(b, 5) + 1, ncode = bi_bits(b, 4) + 4;
+    if (nlen > 286 || ndist > 30) return R_INVALID;  // "too many length or distance symbols"
+    u8 cl[19];
+    for (int i = 0; i < 19; i++) cl[i] = 0;
+    if (!bi_has(b, 3 * ncode)) return R_EXHAUSTED;
+    for (u32 i = 0; i < ncode; i++) cl[c_clen_order[i]] = (u8)bi_bits(b, 3);
+    {  // code-length code must be complete ("invalid code lengths set")
+        u32 cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        for (int i = 0; i < 19; i++) cnt[cl[i]]++;
+        int left = 1;
+        for (int l = 1; l <= 7; l++) { left <<= 1; left -= cnt[l]; if (left < 0) break; }
+        if (left != 0) return R_INVALID;
+    }
+    __syncthreads();
+    for (u32 i = lane; i < 19; i += 64) lens[i] = cl[i];
+    __syncthreads();
+    build_table(lens, 19, lh, ltab, 7, false);
+    u32 idx = 0;
+    u8 prev = 0;
+    while (idx < nlen + ndist) {
+        u32 e;
+        int r = decode_sym(b, ltab, 7, lh, false, &e);
+        if (r != R_OK) return r;
+        const u32 sym = e & 0xFFFF;
+        if (sym < 16) {
+            if (lane == 0) lens[idx] = (u8)sym;
+            prev = (u8)sym;
+            idx++;
+            continue;
+        }
+        u32 rep;
+        u8 v = 0;
+        if (sym == 16) {
+            if (idx == 0) return R_INVALID;  // "invalid bit length repeat"
+            if (!bi_has(b, 2)) return R_EXHAUSTED;
+            v = prev;
+            rep = 3 + bi_bits(b, 2);
+        } else if (sym == 17) {
+            if (!bi_has(b, 3)) return R_EXHAUSTED;
+            rep = 3 + bi_bits(b, 3);
+        } else {
+            if (!bi_has(b, 7)) return R_EXHAUSTED;
+            rep = 11 + bi_bits(b, 7);
+        }
+        if (idx + rep > nlen + ndist) return R_INVALID;
+        if (lane == 0)
+            for (u32 k = 0; k < rep; k++) lens[idx + k] = v;
+        idx += rep;
+        prev = v;
+    }
+    __syncthreads();
+    u8 dl = 0;
+    if ((u32)lane < ndist) dl = lens[nlen + lane];
+    __syncthreads();
+    for (u32 i = nlen + lane; i < 288; i += 64) lens[i] = 0;
+    if ((u32)lane < 32) lens[288 + lane] = (u32)lane < ndist ? dl : 0;
+    __syncthreads();
+    if (lens[256] == 0) return R_INVALID;  // "invalid code -- missing end-of-block"
+    if (build_table(lens, 288, lh, ltab, INF_LBITS, false) != 0) return R_INVALID;
+    if (build_table(lens + 288, 30, dh, dtab, INF_DBITS, true) != 0) return R_INVALID;
+    return R_OK;
+}
+
+__device__ void fixed_tables(u8* lens, HuffLds* lh, u32* ltab, HuffLds* dh, u32* dtab) {
+    const int lane = lane_id();
+    __syncthreads();
+    for (u32 i = lane; i < 320; i += 64)
+        lens[i] = i < 144 ? 8 : i < 256 ? 9 : i < 280 ? 7 : i < 288 ? 8 : 5;
+    __syncthreads();
+    build_table(lens, 288, lh, ltab, INF_LBITS, false);
+    build_table(lens + 288, 30, dh, dtab, INF_DBITS, true);
+}
+
+// Block header: 3 bits, then stored-length check / table construction.
+// *type receives BTYPE; for stored blocks *slen the LEN field.
+__device__ int read_block_header(BitIn& b, bool* last, u32* type, u32* slen, u8* lens, HuffLds* lh,
+                                 u32* ltab, HuffLds* dh, u32* dtab) {
+    if (!bi_has(b, 3)) return R_EXHAUSTED;
+    const u32 hdr = bi_bits(b, 3);
+    *last = hdr & 1;
+    *type = hdr >> 1;
+    if (*type == 0) {
+        const u32 pad = (u32)((8 - (b.consumed & 7)) & 7);  // to byte boundary
+        if (!bi_has(b, pad + 32)) return R_EXHAUSTED;
+        bi_bits(b, pad);
+        const u32 len = bi_bits(b, 16), nlen = bi_bits(b, 16);
+        if ((len ^ 0xFFFF) != nlen) return R_INVALID;  // "invalid stored block lengths"
+        *slen = len;
+        return R_OK;
+    }
+    if (*type == 3) return R_INVALID;  // "invalid block type"
+    if (*type == 1) { fixed_tables(lens, lh, ltab, dh, dtab); return R_OK; }
+    return read_dynamic(b, lens, lh, ltab, dh, dtab);
+}
+
+// zlib keeps decoding after the output is full until it needs to emit a
+// byte (LIT / MATCH with left == 0) or needs input it was not given: the
+// next literal/length code, length extra bits, distance code, distance
+// extra bits, and whole block headers are validated.  The input it was
+// given is the rest of flate2's current 32 KiB BufReader window.
+__device__ int inf_lookahead(BitIn& b, bool last, bool at_header, u8* lens, HuffLds* lh,
+                             u32* ltab, HuffLds* dh, u32* dtab) {
+    for (;;) {
+        if (at_header) {  // after a stored block: straight to the next header
+            at_header = false;
+            if (last) return R_OK;
+            u32 type = 0, slen = 0;
+            int r = read_block_header(b, &last, &type, &slen, lens, lh, ltab, dh, dtab);
+            if (r != R_OK) return r;
+            if (type == 0) {
+                if (slen != 0) return R_OK;
+                at_header = true;
+                continue;
+            }
+        }
+        u32 e;
+        int r = decode_sym(b, ltab, INF_LBITS, lh, false, &e);
+        if (r != R_OK) return r;
+        const u32 kind = (e >> 24) & 15;
+        if (kind == K_LIT) return R_OK;
+        if (kind == K_BAD) return R_INVALID;  // "invalid literal/length code"
+        if (kind == K_LEN) {
+            const u32 ex = (e >> 16) & 0xFF;
+            if (!bi_has(b, ex)) return R_EXHAUSTED;
+            if (ex) bi_bits(b, ex);
+            u32 de;
+            r = decode_sym(b, dtab, INF_DBITS, dh, true, &de);
+            if (r != R_OK) return r;
+            if (((de >> 24) & 15) != K_DIST) return R_INVALID;  // "invalid distance code"
+            return R_OK;  // DISTEXT then MATCH: zlib leaves there (left == 0)
+        }
+        // end of block: the next block header is parsed without output
+        for (;;) {
+            if (last) return R_OK;  // stream end
+            u32 type = 0, slen = 0;
+            r = read_block_header(b, &last, &type, &slen, lens, lh, ltab, dh, dtab);
+            if (r != R_OK) return r;
+            if (type != 0) break;         // decode symbols of the new block
+            if (slen != 0) return R_OK;   // COPY with left == 0: leave
+        }
+    }
+}
+
 __global__ __launch_bounds__(64) void inflate_kernel(const zcg_chunk* __restrict__ chunks, u32 n,
                                                      u64 D, DType t, u32 vflags,
                                                      i32* __restrict__ status) {
@@ -283,164 +452,97 @@ __global__ __launch_bounds__(64) void inflate_kernel(const zcg_chunk* __restrict
     }
     if (st != ZCG_OK) { if (lane == 0) status[c] = st; return; }
 
-    BitIn b{s + h, n_in - h, 0, 0, 0, 0};
+    BitIn b{s + h, n_in - h, 0, 0, 0, 0, (n_in - h) * 8};
     InfOut o{ring, 0, 0, (u8*)ch.dst, D, t};
     bool last = false;
-    while (st == ZCG_OK && !last && o.P < D) {
-        u32 hdr = bi_bits(b, 3);
-        last = hdr & 1;
-        const u32 type = hdr >> 1;
-        if (bi_overrun(b)) { st = ZCG_ERR_UNEXPECTED_EOF; break; }
-        if (type == 0) {  // stored
-            bi_drop(b, b.cnt & 7);  // to byte boundary
-            const u32 len = bi_bits(b, 16), nlen = bi_bits(b, 16);
-            if (bi_overrun(b)) { st = ZCG_ERR_UNEXPECTED_EOF; break; }
-            if ((len ^ 0xFFFF) != nlen) { st = ZCG_ERR_INVALID_DATA; break; }
-            // the bit buffer holds whole bytes now; drain it, then copy directly
+    bool boundary = false;  // output filled exactly at a symbol boundary
+    bool after_stored = false;
+    int r = R_OK;
+    while (r == R_OK && o.P < D) {
+        if (last) { r = R_EXHAUSTED; break; }  // stream ended before N bytes
+        u32 type = 0, slen = 0;
+        r = read_block_header(b, &last, &type, &slen, lens, &lh, ltab, &dh, dtab);
+        if (r != R_OK) break;
+        if (type == 0) {  // stored: drain whole bytes of the bit buffer, then copy
             u32 done = 0;
-            while (done < len && b.cnt >= 8 && o.P < D) {
+            while (done < slen && b.cnt >= 8 && o.P < D) {
+                if (!bi_has(b, 8)) { r = R_EXHAUSTED; break; }
                 put_lit(o, bi_bits(b, 8));
                 done++;
                 inf_maybe_flush(o);
             }
-            if (done == len) continue;  // short block served from the bit buffer
-            if (o.P >= D) break;        // output full: the rest is never read
-            u64 in0 = b.pos;            // bit buffer is empty here
-            while (done < len && o.P < D) {
-                u32 k = len - done;
-                const u64 room = INF_FLUSH - (o.P - o.F);
-                if (k > room) k = (u32)room;
-                if (k > 64 * 64) k = 64 * 64;
-                if ((u64)k > D - o.P) k = (u32)(D - o.P);
-                if (in0 + k > b.n) { st = ZCG_ERR_UNEXPECTED_EOF; break; }
-                for (u32 i = lane; i < k; i += 64) ring[(o.P + i) & (INF_RING - 1)] = b.src[in0 + i];
-                __builtin_amdgcn_wave_barrier();
-                o.P += k; in0 += k; done += k;
-                inf_maybe_flush(o);
+            if (r != R_OK) break;
+            if (done < slen && o.P < D) {
+                u64 in0 = b.pos;  // bit buffer is empty here
+                while (done < slen && o.P < D) {
+                    u32 k = slen - done;
+                    const u64 room = INF_FLUSH - (o.P - o.F);
+                    if (k > room) k = (u32)room;
+                    if (k > 64 * 64) k = 64 * 64;
+                    if ((u64)k > D - o.P) k = (u32)(D - o.P);
+                    if (in0 + k > b.n) { r = R_EXHAUSTED; break; }
+                    for (u32 i = lane; i < k; i += 64)
+                        ring[(o.P + i) & (INF_RING - 1)] = b.src[in0 + i];
+                    __builtin_amdgcn_wave_barrier();
+                    o.P += k; in0 += k; done += k;
+                    inf_maybe_flush(o);
+                }
+                b.pos = in0; b.buf = 0; b.cnt = 0; b.consumed = in0 * 8;
             }
-            if (st != ZCG_OK || done < len) break;
-            b.pos = in0; b.buf = 0; b.cnt = 0; b.consumed = in0 * 8;
+            boundary = (done == slen);
+            after_stored = true;
             continue;
         }
-        if (type == 3) { st = ZCG_ERR_INVALID_DATA; break; }
-        if (type == 1) {  // fixed Huffman
-            for (u32 i = lane; i < 320; i += 64)
-                lens[i] = i < 144 ? 8 : i < 256 ? 9 : i < 280 ? 7 : i < 288 ? 8 : 5;
-            __syncthreads();
-            build_table(lens, 288, &lh, ltab, INF_LBITS, false);
-            build_table(lens + 288, 30, &dh, dtab, INF_DBITS, true);
-        } else {  // dynamic
-            const u32 nlen = bi_bits(b, 5) + 257, ndist = bi_bits(b, 5) + 1, ncode = bi_bits(b, 4) + 4;
-            if (nlen > 286 || ndist > 30) { st = ZCG_ERR_INVALID_DATA; break; }
-            u8 cl[19];
-            for (int i = 0; i < 19; i++) cl[i] = 0;
-            for (u32 i = 0; i < ncode; i++) cl[c_clen_order[i]] = (u8)bi_bits(b, 3);
-            if (bi_overrun(b)) { st = ZCG_ERR_UNEXPECTED_EOF; break; }
-            // code-length code: must be complete (zlib CODES)
-            for (u32 i = lane; i < 19; i += 64) lens[i] = cl[i];
-            __syncthreads();
-            {
-                u32 cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-                for (int i = 0; i < 19; i++) cnt[cl[i]]++;
-                int left = 1;
-                for (int l = 1; l <= 7; l++) { left <<= 1; left -= cnt[l]; if (left < 0) break; }
-                if (left != 0) { st = ZCG_ERR_INVALID_DATA; break; }
-            }
-            build_table(lens, 19, &lh, ltab, 7, false);  // symbols 0..18 map to K_LIT entries
-            u32 idx = 0;
-            u8 prev = 0;
-            bool bad = false;
-            while (idx < nlen + ndist) {
-                bi_refill(b);
-                const u32 e = __builtin_amdgcn_readfirstlane(ltab[bi_peek(b, 7)]);
-                const u32 l = e >> 28;
-                if (l == 0) { bad = true; break; }
-                bi_drop(b, l);
-                const u32 sym = e & 0xFFFF;
-                if (sym < 16) {
-                    if (lane == 0) lens[idx] = (u8)sym;
-                    prev = (u8)sym;
-                    idx++;
-                } else {
-                    u32 rep;
-                    u8 v = 0;
-                    if (sym == 16) {
-                        if (idx == 0) { bad = true; break; }
-                        v = prev;
-                        rep = 3 + bi_bits(b, 2);
-                    } else if (sym == 17) {
-                        rep = 3 + bi_bits(b, 3);
-                    } else {
-                        rep = 11 + bi_bits(b, 7);
-                    }
-                    if (idx + rep > nlen + ndist) { bad = true; break; }
-                    for (u32 r = 0; r < rep; r++) if (lane == 0) lens[idx + r] = v;
-                    idx += rep;
-                    prev = v;
-                }
-            }
-            if (bad) { st = ZCG_ERR_INVALID_DATA; break; }
-            if (bi_overrun(b)) { st = ZCG_ERR_UNEXPECTED_EOF; break; }
-            __syncthreads();
-            // distance lengths move to lens[288..]
-            u8 dl = 0;
-            if ((u32)lane < ndist) dl = lens[nlen + lane];
-            __syncthreads();
-            for (u32 i = nlen + lane; i < 288; i += 64) lens[i] = 0;
-            if ((u32)lane < 32) lens[288 + lane] = (u32)lane < ndist ? dl : 0;
-            __syncthreads();
-            if (lens[256] == 0) { st = ZCG_ERR_INVALID_DATA; break; }  // missing end-of-block
-            if (build_table(lens, 288, &lh, ltab, INF_LBITS, false) != 0) { st = ZCG_ERR_INVALID_DATA; break; }
-            if (build_table(lens + 288, 30, &dh, dtab, INF_DBITS, true) != 0) {
-                st = ZCG_ERR_INVALID_DATA;
-                break;
-            }
-        }
-        // ---- block body ---------------------------------------------------
+        // ---- Huffman block body ---------------------------------------------
+        after_stored = false;
         for (;;) {
-            if (o.P >= D) break;
-            bi_refill(b);
-            u32 e = __builtin_amdgcn_readfirstlane(ltab[bi_peek(b, INF_LBITS)]);
-            u32 l = e >> 28;
-            if (l == 0) {
-                if (((e >> 24) & 15) == K_BAD) { st = ZCG_ERR_INVALID_DATA; break; }
-                e = slow_decode(b, &lh, false);
-            } else {
-                bi_drop(b, l);
-            }
+            if (o.P >= D) { boundary = true; break; }
+            u32 e;
+            r = decode_sym(b, ltab, INF_LBITS, &lh, false, &e);
+            if (r != R_OK) break;
             const u32 kind = (e >> 24) & 15;
             if (kind == K_LIT) {
                 put_lit(o, e & 0xFF);
             } else if (kind == K_LEN) {
                 const u32 ex = (e >> 16) & 0xFF;
+                if (!bi_has(b, ex)) { r = R_EXHAUSTED; break; }
                 u32 len = (e & 0xFFFF) + (ex ? bi_bits(b, ex) : 0);
-                bi_refill(b);
-                u32 de = __builtin_amdgcn_readfirstlane(dtab[bi_peek(b, INF_DBITS)]);
-                u32 dlx = de >> 28;
-                if (dlx == 0) {
-                    if (((de >> 24) & 15) == K_BAD) { st = ZCG_ERR_INVALID_DATA; break; }
-                    de = slow_decode(b, &dh, true);
-                } else {
-                    bi_drop(b, dlx);
-                }
-                if (((de >> 24) & 15) != K_DIST) { st = ZCG_ERR_INVALID_DATA; break; }
+                u32 de;
+                r = decode_sym(b, dtab, INF_DBITS, &dh, true, &de);
+                if (r != R_OK) break;
+                if (((de >> 24) & 15) != K_DIST) { r = R_INVALID; break; }
                 const u32 dex = (de >> 16) & 0xFF;
+                if (!bi_has(b, dex)) { r = R_EXHAUSTED; break; }
                 const u32 dist = (de & 0xFFFF) + (dex ? bi_bits(b, dex) : 0);
-                if (bi_overrun(b)) { st = ZCG_ERR_UNEXPECTED_EOF; break; }
-                if (dist > o.P) { st = ZCG_ERR_INVALID_DATA; break; }  // too far back
-                if (o.P + len > D) len = (u32)(D - o.P);
+                if (dist > o.P) { r = R_INVALID; break; }  // "invalid distance too far back"
+                if (o.P + len > D) {  // MATCH leaves with left == 0: no look-ahead
+                    put_match(o, (u32)(D - o.P), dist);
+                    boundary = false;
+                    break;
+                }
                 put_match(o, len, dist);
             } else if (kind == K_EOB) {
                 break;
             } else {
-                st = ZCG_ERR_INVALID_DATA;
+                r = R_INVALID;
                 break;
             }
-            if (bi_overrun(b)) { st = ZCG_ERR_UNEXPECTED_EOF; break; }
             inf_maybe_flush(o);
         }
     }
-    if (st == ZCG_OK && o.P < D) st = ZCG_ERR_UNEXPECTED_EOF;
+    if (r == R_OK && o.P >= D && boundary) {
+        // look-ahead bounded by the 32 KiB window holding the last consumed bit
+        const u64 last_byte = h + (b.consumed ? (b.consumed - 1) / 8 : 0);
+        u64 wend = (last_byte / 32768 + 1) * 32768;
+        if (wend > n_in) wend = n_in;
+        b.limit = (wend - h) * 8;
+        if (b.limit >= b.consumed) {
+            int la = inf_lookahead(b, last, after_stored, lens, &lh, ltab, &dh, dtab);
+            if (la == R_INVALID) r = R_INVALID;
+        }
+    }
+    if (r == R_INVALID) st = ZCG_ERR_INVALID_DATA;
+    else if (r == R_EXHAUSTED || o.P < D) st = ZCG_ERR_UNEXPECTED_EOF;
     if (st == ZCG_OK) {
         while (D - o.F > INF_FLUSH) inf_flush(o, o.F + INF_FLUSH);
         inf_flush(o, D);

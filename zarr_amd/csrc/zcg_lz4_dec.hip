@@ -76,14 +76,14 @@ __device__ __forceinline__ u32 get_byte(const u32x4& w, u32 idx) {
 // 16 bytes of the period-d pattern b[0..d) starting at phase `ph`.
 __device__ __forceinline__ u32x4 pattern16(const u32x4& b, u32 d, u32 ph) {
     u32 r[4];
+    u32 j = ph;  // ph < d
 #pragma unroll
     for (int k = 0; k < 4; k++) {
         u32 v = 0;
 #pragma unroll
         for (int i = 0; i < 4; i++) {
-            u32 j = ph + k * 4 + i;
-            j = j % d;
             v |= get_byte(b, j) << (8 * i);
+            j = (j + 1 == d) ? 0 : j + 1;
         }
         r[k] = v;
     }
@@ -173,6 +173,17 @@ __device__ int lz4_block(const u8* __restrict__ src, u32 csize, u64 src_avail, u
     return ZCG_OK;
 }
 
+// LZ4F keeps going after the output is full when the block that filled it
+// ended exactly at N: the next block header (fed to it together with the
+// block's last bytes by lz4-rs) is read, and a size above blockMax is an
+// error (LZ4F_ERROR_maxBlockSize_invalid).
+__device__ __forceinline__ int lz4_next_header_check(const u8* s, u64 n, u64 pos, u32 bmax) {
+    if (pos + 4 > n) return ZCG_OK;
+    const u32 bs = ld32(s + pos);
+    if (bs != 0 && (bs & 0x7FFFFFFFu) > bmax) return ZCG_ERR_INVALID_DATA;
+    return ZCG_OK;
+}
+
 // Serial decode of a whole frame by one lane, exact output offsets.  Used for
 // linked-block frames and whenever the per-block placement guess failed.
 __device__ int lz4_frame_serial(const u8* s, u64 n, u8* dst, u64 D, u32 vflags) {
@@ -202,6 +213,7 @@ __device__ int lz4_frame_serial(const u8* s, u64 n, u8* dst, u64 D, u32 vflags) 
         }
         out += got;
         pos += need;
+        if (out == D) return lz4_next_header_check(s, n, pos, h.bmax);
     }
     return ZCG_OK;
 }
@@ -343,6 +355,13 @@ __global__ __launch_bounds__(64) void lz4_decode_kernel(const zcg_chunk* __restr
                 const u32 got = slot_dec[j * S + k];
                 total = (u64)k * bmax + got;
                 if (got != bmax && k + 1 < ns) { st = -1; break; }  // short block mid-frame
+            }
+            if (st == ZCG_OK && total == D && ns > 0) {  // last block ended exactly at N
+                const zcg_chunk ch = chunks[c0 + j];
+                const u32 k = ns - 1;
+                const u64 pos = (u64)slot_src[j * S + k] + (slot_cs[j * S + k] & 0x7FFFFFFFu) +
+                                ((c_flags[j] & F_BLOCK_CKSUM) ? 4 : 0);
+                st = lz4_next_header_check((const u8*)ch.src, ch.src_len, pos, bmax);
             }
             if (st == ZCG_OK && total < D) {
                 // frame ended / input ran out before N bytes; a short last
