@@ -71,6 +71,9 @@ enum zcg_status {
 #define ZCG_FLAG_VERIFY_GZIP_CRC 0x1u
 #define ZCG_FLAG_VERIFY_LZ4_CONTENT_CHECKSUM 0x2u
 #define ZCG_FLAG_SKIP_LZ4_BLOCK_CHECKSUM 0x4u
+/* Use the wave-serial inflate kernel instead of the parallel one (the two are
+ * bit-identical; the serial one is kept as a differential reference). */
+#define ZCG_FLAG_SERIAL_INFLATE 0x100u
 
 /* CompressionType + its configuration (camelCase JSON keys in the reference). */
 typedef struct zcg_compression {

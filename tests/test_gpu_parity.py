@@ -353,3 +353,20 @@ def test_lz4_next_header_after_n_bytes():
             bad = bytearray(s)
             struct.pack_into("<I", bad, blocks[k], val)
             check("lz4", bytes(bad), "u1", 65536 * k)
+
+
+@pytest.mark.parametrize("data", list(DATASETS))
+def test_inflate_parallel_vs_serial_kernel(data):
+    """The speculative parallel inflate kernel and the wave-serial one must
+    agree bit for bit (and with the oracle) on every deflate structure."""
+    from zarr_amd._native import FLAG_SERIAL_INFLATE
+    payload = DATASETS[data]()
+    streams = [gzip_wrap(deflate(payload, lvl, strat), payload)
+               for lvl, strat in ((1, 0), (6, 0), (9, 0), (6, zlib.Z_HUFFMAN_ONLY), (6, zlib.Z_RLE))]
+    for s in streams:
+        for D in (len(payload), len(payload) // 3 + 1):
+            meta = meta_for("gzip", "u1", D)
+            a = DefaultChunk.read_chunk(s, meta, [0], np.uint8).get_data()
+            b = DefaultChunk.read_chunk(s, meta, [0], np.uint8, flags=FLAG_SERIAL_INFLATE).get_data()
+            assert np.array_equal(a, b)
+            assert a.tobytes() == payload[:D]

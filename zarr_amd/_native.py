@@ -18,6 +18,7 @@ RUNTIME = 100
 FLAG_VERIFY_GZIP_CRC = 0x1
 FLAG_VERIFY_LZ4_CONTENT_CHECKSUM = 0x2
 FLAG_SKIP_LZ4_BLOCK_CHECKSUM = 0x4
+FLAG_SERIAL_INFLATE = 0x100
 
 STATUS_NAMES = {OK: "Ok", UNEXPECTED_EOF: "UnexpectedEof", INVALID_DATA: "InvalidData",
                 INVALID_INPUT: "InvalidInput", UNSUPPORTED: "Unsupported",

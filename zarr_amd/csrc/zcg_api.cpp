@@ -147,7 +147,11 @@ int zcg_decode_batch(zcg_ctx* ctx, const zcg_array* a, const zcg_chunk* d_chunks
     switch (a->compression.codec) {
     case ZCG_CODEC_RAW: e = launch_raw(a, d_chunks, n, d_status, nullptr, 0, s); break;
     case ZCG_CODEC_LZ4: e = launch_lz4_decode(a, d_chunks, n, d_status, s); break;
-    case ZCG_CODEC_GZIP: e = launch_inflate(a, d_chunks, n, d_status, s); break;
+    case ZCG_CODEC_GZIP:
+        e = (a->compression.flags & ZCG_FLAG_SERIAL_INFLATE)
+                ? launch_inflate(a, d_chunks, n, d_status, s)
+                : launch_inflate_par(a, d_chunks, n, d_status, s);
+        break;
     case ZCG_CODEC_BZIP2:
     case ZCG_CODEC_XZ:
         ctx->err = "codec has no GPU decoder in this build";
