@@ -53,12 +53,13 @@ __device__ __forceinline__ u32 sym_entry(u32 s, u32 len, bool dist) {
 // Build canonical code + primary table from lengths[0..nsym) (wave-cooperative).
 // Returns 0 ok, -1 over-subscribed/incomplete (zlib inflate_table rules).
 __device__ int build_table(const u8* lens, u32 nsym, HuffLds* h, u32* table, int tbits, bool dist) {
-    const int lane = lane_id();
+    // block-cooperative: every thread of the workgroup calls this uniformly
+    const u32 tid = threadIdx.x, nth = blockDim.x;
     __shared__ u16 s_offs[16];
-    if (lane < 16) h->count[lane] = 0;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __syncthreads();
-    if (lane == 0) {
+    if (tid < 16) h->count[tid] = 0;
+    __syncthreads();
+    if (tid == 0) {
         for (u32 s = 0; s < nsym; s++) h->count[lens[s]]++;
     }
     __syncthreads();
@@ -74,7 +75,7 @@ __device__ int build_table(const u8* lens, u32 nsym, HuffLds* h, u32* table, int
         // incomplete codes are only allowed for a single length-1 code
         if (ok && left > 0 && maxlen > 1) ok = 0;
     }
-    if (lane == 0) {
+    if (tid == 0) {
         u32 o = 0;
         s_offs[0] = 0;
         for (int l = 1; l < 16; l++) { s_offs[l] = o; o += h->count[l]; }
@@ -84,7 +85,7 @@ __device__ int build_table(const u8* lens, u32 nsym, HuffLds* h, u32* table, int
     __syncthreads();
     // primary table: slot bits are stream-order (LSB first)
     const u32 nslots = 1u << tbits;
-    for (u32 slot = lane; slot < nslots; slot += 64) {
+    for (u32 slot = tid; slot < nslots; slot += nth) {
         u32 code = 0, first = 0, index = 0, e = mk_entry(0, K_BAD, 0, 0);
         bool found = false;
         for (int l = 1; l <= tbits; l++) {
@@ -106,6 +107,25 @@ __device__ int build_table(const u8* lens, u32 nsym, HuffLds* h, u32* table, int
     }
     __syncthreads();
     return ok ? 0 : -1;
+}
+
+// Canonical decode of a long code from the bits of v (LSB first).
+__device__ __forceinline__ u32 slow_sym(u64 v, const HuffLds* h, bool dist, u32* used) {
+    int code = 0, first = 0, index = 0;
+    for (int len = 1; len <= 15; len++) {
+        code |= (int)((v >> (len - 1)) & 1);
+        const int cnt = h->count[len];
+        if (code - cnt < first) {
+            *used = len;
+            return sym_entry(h->sym[index + (code - first)], len, dist);
+        }
+        index += cnt;
+        first += cnt;
+        first <<= 1;
+        code <<= 1;
+    }
+    *used = 0;
+    return mk_entry(0, K_BAD, 0, 0);
 }
 
 // Wave-uniform bit reader (every lane holds the same state).  Input words
@@ -275,7 +295,7 @@ __device__ __forceinline__ int decode_sym(BitIn& b, const u32* tab, int tbits, c
 
 // Dynamic block header (RFC 1951 3.2.7) -> tables; zlib's validity rules.
 __device__ int read_dynamic(BitIn& b, u8* lens, HuffLds* lh, u32* ltab, HuffLds* dh, u32* dtab) {
-    const int lane = lane_id();
+    const u32 tid = threadIdx.x, nth = blockDim.x;
     if (!bi_has(b, 14)) return R_EXHAUSTED;
     const u32 nlen = bi_bits(b, 5) + 257, ndist = bi_bits(b, 5) + 1, ncode = bi_bits(b, 4) + 4;
     if (nlen > 286 || ndist > 30) return R_INVALID;  // "too many length or distance symbols"
@@ -291,7 +311,7 @@ __device__ int read_dynamic(BitIn& b, u8* lens, HuffLds* lh, u32* ltab, HuffLds*
         if (left != 0) return R_INVALID;
     }
     __syncthreads();
-    for (u32 i = lane; i < 19; i += 64) lens[i] = cl[i];
+    for (u32 i = tid; i < 19; i += nth) lens[i] = cl[i];
     __syncthreads();
     build_table(lens, 19, lh, ltab, 7, false);
     u32 idx = 0;
@@ -302,7 +322,7 @@ __device__ int read_dynamic(BitIn& b, u8* lens, HuffLds* lh, u32* ltab, HuffLds*
         if (r != R_OK) return r;
         const u32 sym = e & 0xFFFF;
         if (sym < 16) {
-            if (lane == 0) lens[idx] = (u8)sym;
+            if (tid == 0) lens[idx] = (u8)sym;
             prev = (u8)sym;
             idx++;
             continue;
@@ -322,17 +342,17 @@ __device__ int read_dynamic(BitIn& b, u8* lens, HuffLds* lh, u32* ltab, HuffLds*
             rep = 11 + bi_bits(b, 7);
         }
         if (idx + rep > nlen + ndist) return R_INVALID;
-        if (lane == 0)
+        if (tid == 0)
             for (u32 k = 0; k < rep; k++) lens[idx + k] = v;
         idx += rep;
         prev = v;
     }
     __syncthreads();
     u8 dl = 0;
-    if ((u32)lane < ndist) dl = lens[nlen + lane];
+    if (tid < ndist) dl = lens[nlen + tid];
     __syncthreads();
-    for (u32 i = nlen + lane; i < 288; i += 64) lens[i] = 0;
-    if ((u32)lane < 32) lens[288 + lane] = (u32)lane < ndist ? dl : 0;
+    for (u32 i = nlen + tid; i < 288; i += nth) lens[i] = 0;
+    if (tid < 32) lens[288 + tid] = tid < ndist ? dl : 0;
     __syncthreads();
     if (lens[256] == 0) return R_INVALID;  // "invalid code -- missing end-of-block"
     if (build_table(lens, 288, lh, ltab, INF_LBITS, false) != 0) return R_INVALID;
@@ -341,9 +361,9 @@ __device__ int read_dynamic(BitIn& b, u8* lens, HuffLds* lh, u32* ltab, HuffLds*
 }
 
 __device__ void fixed_tables(u8* lens, HuffLds* lh, u32* ltab, HuffLds* dh, u32* dtab) {
-    const int lane = lane_id();
+    const u32 tid = threadIdx.x, nth = blockDim.x;
     __syncthreads();
-    for (u32 i = lane; i < 320; i += 64)
+    for (u32 i = tid; i < 320; i += nth)
         lens[i] = i < 144 ? 8 : i < 256 ? 9 : i < 280 ? 7 : i < 288 ? 8 : 5;
     __syncthreads();
     build_table(lens, 288, lh, ltab, INF_LBITS, false);

@@ -2,44 +2,47 @@
 // (GzipCompression decode, src/compression/gzip.rs:49-52 -> flate2 -> zlib).
 //
 // A deflate block is one serial Huffman stream, so a chunk gets lane
-// parallelism by SPECULATIVE, SELF-SYNCHRONISING decoding (one wave/chunk):
+// parallelism by SPECULATIVE, SELF-SYNCHRONISING decoding.  One workgroup of
+// 256 lanes (4 waves, one per SIMD of the CU) owns one chunk:
 //
-//   round: the wave stages the next ~4 KiB of the stream in LDS; lane i
-//     decodes from bit R0 + i*SEG as if a symbol started there, recording
-//     every token (literal, match, EOB/invalid/exhausted marker) and its
-//     start bit, until it is MARGIN bits past lane i+1's start.
-//   sync:  Huffman decoders resynchronise quickly: lane i's path (true from
-//     its own sync point on) meets lane i+1's recorded token starts within a
-//     few symbols; from that common start bit both paths are identical, so
-//     lane i owns the true tokens up to it and lane i+1 from it.  Lane 0 is
-//     true by construction; the valid chain ends at the first lane that
-//     broke it (no sync within MARGIN, token cap, or a marker on its valid
-//     range) — one ballot, no serial walk.
-//   place: a wave prefix sum over the lanes' output lengths positions every
-//     token; the round is cut at STAGE bytes (and at N, with zlib's look-
-//     ahead semantics when N falls on a token boundary).
+//   round: the block stages the next ~8.7 KiB of the stream in LDS; lane i
+//     decodes from bit R0 + i*SEG as if a symbol started there, keeping the
+//     bit buffer in registers, storing every token (literal, match, or an
+//     EOB / invalid-code / input-exhausted marker) and marking its start bit
+//     in lane i's segment bitmap, until it leaves its segment.
+//   sync:  every lane then keeps following its own path past its segment and
+//     stops at the first token start that another lane MARKED (any later
+//     segment): from a common start bit two Huffman paths are identical, so
+//     the lane that marked it is on the true path from there.  Measured on
+//     the bench data (SURVEY §8(d) "quant", zlib-6): median 50-80 bits, p99
+//     ~450 bits to resynchronise.  Lane 0 is true by construction; the valid
+//     chain follows the sync targets (almost always lane i+1; the rare
+//     skips/stops are walked by one thread).
+//   place: a block-wide prefix sum over the chain lanes' output lengths
+//     positions every token; the round is cut at STAGE bytes, and at N with
+//     zlib's look-ahead semantics when N falls on a token boundary.
 //   LZ77:  literals land in an LDS stage; matches resolve in rounds (each
 //     lane walks its own matches in order and copies one as soon as its
 //     source bytes are resolved — the earliest unresolved match is always
-//     resolvable, so this terminates); sources before the round come from a
-//     32 KiB LDS window ring.  Copies read B[src + k mod dist] so the reads of
-//     one match never depend on its own writes.
+//     resolvable, so this terminates); sources before the round come from
+//     the 32 KiB LDS window ring.  Copies read B[src + k mod dist] so a
+//     match's reads never depend on its own writes.
 //   commit: the stage is flushed to HBM with 16 B/lane stores (byte order /
 //     bool transform fused) and appended to the window ring.
 // Block headers, stored blocks and the post-N look-ahead use the wave-uniform
-// reader of zcg_inflate_common.h.  Results are bit-identical to the serial
-// kernel (zcg_inflate.hip), which tests/ compare it against.
+// reader of zcg_inflate_common.h (wave 0).  Results are bit-identical to the
+// serial kernel (zcg_inflate.hip); tests/ compare the two.
 #include "zcg_inflate_common.h"
 
 namespace zcg {
 
-constexpr u32 PI_LANES = 64;
-constexpr u32 PI_SEG = 512;     // bits per lane segment
-constexpr u32 PI_MARGIN = 160;  // bits past the next lane's start searched for sync
-constexpr u32 PI_TMAX = 48;     // tokens recorded per lane per round
-constexpr u32 PI_STAGE = 8192;  // bytes of output per round (power of 2)
-constexpr u32 PI_WIN = 32768;   // LZ77 window ring
-constexpr u32 PI_IN_WORDS = (PI_LANES * PI_SEG + PI_MARGIN + 4 * 64) / 32 + 8;
+constexpr u32 PI_NL = 256;       // lanes per chunk (4 waves)
+constexpr u32 PI_SEG = 256;      // bits per lane segment
+constexpr u32 PI_TMAX = 56;      // tokens stored per lane per round
+constexpr u32 PI_STAGE = 32768;  // output bytes per round (power of 2)
+constexpr u32 PI_WIN = 32768;    // LZ77 window ring
+constexpr u32 PI_SEGW = PI_SEG / 32;
+constexpr u32 PI_IN_WORDS = (PI_NL * PI_SEG + PI_TMAX * 48 + 512) / 32 + 8;
 
 // token word: literal = byte value; match = 1<<31 | (len-3)<<16 | (dist-1);
 // markers (bit 30): EOB, invalid code, input exhausted.
@@ -48,60 +51,39 @@ constexpr u32 T_EOB = 0x40000000u;
 constexpr u32 T_BAD = 0x40000001u;
 constexpr u32 T_EXH = 0x40000002u;
 
+// lane stop codes (next[] >= PI_NL)
+constexpr u32 N_ROUND_END = PI_NL;  // reached the end of the round's range
+constexpr u32 N_MARKER = PI_NL + 1; // last stored token is a marker
+constexpr u32 N_CAP = PI_NL + 2;    // token store full before syncing
+
 __device__ __forceinline__ bool tok_is_marker(u32 t) { return (t & 0xC0000000u) == 0x40000000u; }
 __device__ __forceinline__ u32 tok_len(u32 t) { return (t & T_MATCH) ? ((t >> 16) & 0xFF) + 3 : 1; }
 __device__ __forceinline__ u32 tok_dist(u32 t) { return (t & 0x7FFF) + 1; }
 
 struct ParLds {
-    u8 win[PI_WIN];                         // LZ77 window ring (absolute pos & 32767)
-    u8 stage[PI_STAGE];                     // this round's output (absolute pos & 8191)
-    u32 in[PI_IN_WORDS];                    // staged stream words
-    u32 tok[PI_LANES * PI_TMAX];            // tokens, lane-major
-    u16 tpos[PI_LANES * PI_TMAX];           // token start bit - lane start bit
-    u32 resolved[PI_STAGE / 32];            // MRR bitmap over round offsets
+    u8 win[PI_WIN];                  // LZ77 window ring (absolute pos & 32767)
+    u8 stage[PI_STAGE];              // round output (absolute pos & 32767)
+    u32 in[PI_IN_WORDS];             // staged stream words
+    u32 tok[PI_NL * PI_TMAX];        // tokens, lane-major
+    u32 mark[PI_NL * PI_SEGW];       // token-start bitmap of each lane's own segment
+    u32 resolved[PI_STAGE / 32];     // MRR bitmap over round offsets
     u32 ltab[1u << INF_LBITS];
     u32 dtab[1u << INF_DBITS];
     HuffLds lh, dh;
     u8 lens[320];
-    u32 bcache[BI_CACHE_WORDS];
-    u32 ntok[PI_LANES];
-    u32 endp[PI_LANES];                     // bit after the last decoded token
-    i32 nstart[PI_LANES + 1];               // first valid token of lane i (set by lane i-1)
-    u32 ctl[8];                             // round broadcast words
+    u32 bcache[(PI_NL / 64) * BI_CACHE_WORDS];  // one bit-reader cache per wave
+    u32 next[PI_NL];                 // sync target lane, or a stop code
+    u32 endp[PI_NL];                 // bit where the lane stopped
+    u32 give[PI_NL];                 // index of the sync token in the target's list
+    u32 sidx[PI_NL];                 // first valid token of the lane
+    u32 ntok[PI_NL];
+    u32 base[PI_NL];                 // output offset of the lane's first valid token
+    u32 wsum[8];
+    u32 ctl[16];
 };
 
-// 64 stream bits starting at absolute bit q (staged window starts at bit0).
-__device__ __forceinline__ u64 peek64(const u32* in, u32 q, u32 bit0) {
-    const u32 rel = q - bit0;
-    const u32 w = rel >> 5, sh = rel & 31;
-    const u64 lo = ((u64)in[w + 1] << 32) | in[w];
-    u64 v = lo >> sh;
-    if (sh) v |= (u64)in[w + 2] << (64 - sh);
-    return v;
-}
-
-// Canonical decode of a long code from the bits of v (LSB first).
-__device__ __forceinline__ u32 slow_sym(u64 v, const HuffLds* h, bool dist, u32* used) {
-    int code = 0, first = 0, index = 0;
-    for (int len = 1; len <= 15; len++) {
-        code |= (int)((v >> (len - 1)) & 1);
-        const int cnt = h->count[len];
-        if (code - cnt < first) {
-            *used = len;
-            return sym_entry(h->sym[index + (code - first)], len, dist);
-        }
-        index += cnt;
-        first += cnt;
-        first <<= 1;
-        code <<= 1;
-    }
-    *used = 0;
-    return mk_entry(0, K_BAD, 0, 0);
-}
-
-// Decode one token at bit q.  Returns the token word; *adv = bits consumed.
-__device__ __forceinline__ u32 decode_token(const ParLds& L, u32 q, u32 bit0, u32* adv) {
-    const u64 v = peek64(L.in, q, bit0);
+// Decode one token from a bit buffer holding >= 48 valid bits.
+__device__ __forceinline__ u32 decode_token(const ParLds& L, u64 v, u32* adv) {
     u32 e = L.ltab[(u32)v & ((1u << INF_LBITS) - 1)];
     u32 l = e >> 28;
     if (l == 0) {
@@ -131,32 +113,70 @@ __device__ __forceinline__ u32 decode_token(const ParLds& L, u32 q, u32 bit0, u3
     return T_MATCH | ((len - 3) << 16) | (dist - 1);
 }
 
-// Read the byte at absolute output position q (window ring or stage).
+// Register bit buffer over the staged words: a 96-bit window (lo:hi) holding
+// bits [q, q+nb) of the stream; lb_fill keeps nb >= 48 (one token's worst
+// case: 15+5 bits of length, 15+13 bits of distance), so a token decodes from
+// `lo` alone with no LDS read on its critical path.
+struct LaneBits {
+    u64 lo;
+    u32 hi;
+    u32 nb;
+    u32 w;  // next staged word to append
+};
+
+__device__ __forceinline__ void lb_init(LaneBits& s, const u32* in, u32 q, u32 bit0) {
+    const u32 rel = q - bit0;
+    const u32 w = rel >> 5, sh = rel & 31;
+    const u64 a = ((u64)in[w + 1] << 32) | in[w];
+    const u32 c = in[w + 2];
+    s.lo = sh ? (a >> sh) | ((u64)c << (64 - sh)) : a;
+    s.hi = sh ? c >> sh : c;
+    s.nb = 96 - sh;
+    s.w = w + 3;
+}
+__device__ __forceinline__ void lb_fill(LaneBits& s, const u32* in) {
+    if (s.nb <= 64) {
+        const u32 v = in[s.w++];
+        if (s.nb < 64) {
+            s.lo |= (u64)v << s.nb;
+            if (s.nb > 32) s.hi = v >> (64 - s.nb);
+            else s.hi = 0;  // nb <= 32: v fits in lo entirely
+        } else {
+            s.hi = v;
+        }
+        s.nb += 32;
+    }
+}
+__device__ __forceinline__ void lb_drop(LaneBits& s, u32 k) {  // 0 < k <= 48
+    s.lo = (s.lo >> k) | ((u64)s.hi << (64 - k));
+    s.hi = k >= 32 ? 0u : (s.hi >> k);
+    s.nb -= k;
+}
+
 __device__ __forceinline__ u8 out_byte(const ParLds& L, u64 q, u64 S) {
     return q < S ? L.win[q & (PI_WIN - 1)] : L.stage[q & (PI_STAGE - 1)];
 }
 
 // Flush [from, to) of the stage to dst (transform fused); append to window.
 __device__ void par_commit(ParLds& L, u8* dst, u64 from, u64 to, const DType& t) {
-    const int lane = lane_id();
+    const u32 tid = threadIdx.x;
     __syncthreads();
     const u64 a16 = (from + 15) & ~15ull, b16 = to & ~15ull;
     if (a16 < b16) {
-        for (u64 p = a16 + (u64)lane * 16; p < b16; p += 64 * 16) {
+        for (u64 p = a16 + (u64)tid * 16; p < b16; p += PI_NL * 16) {
             const u32x4 v = *(const u32x4*)(L.stage + (p & (PI_STAGE - 1)));
             st16(dst + p, transform16(v, t));
             *(u32x4*)(L.win + (p & (PI_WIN - 1))) = v;
         }
     }
-    // edges (and everything when the range is shorter than one group)
     const u64 e0 = a16 < b16 ? a16 : to;
-    for (u64 q = from + lane; q < e0; q += 64) {
+    for (u64 q = from + tid; q < e0; q += PI_NL) {
         const u8 v = L.stage[q & (PI_STAGE - 1)];
         dst[swap_pos(q, t)] = norm_byte(v, t);
         L.win[q & (PI_WIN - 1)] = v;
     }
     if (a16 < b16)
-        for (u64 q = b16 + lane; q < to; q += 64) {
+        for (u64 q = b16 + tid; q < to; q += PI_NL) {
             const u8 v = L.stage[q & (PI_STAGE - 1)];
             dst[swap_pos(q, t)] = norm_byte(v, t);
             L.win[q & (PI_WIN - 1)] = v;
@@ -164,60 +184,91 @@ __device__ void par_commit(ParLds& L, u8* dst, u64 from, u64 to, const DType& t)
     __syncthreads();
 }
 
-__device__ __forceinline__ u32 wave_excl_scan(u32 v) {
+// Block-wide exclusive scan over 256 lanes; *total receives the sum.
+__device__ __forceinline__ u32 block_excl_scan(ParLds& L, u32 v, u32* total) {
     const int lane = lane_id();
+    const u32 wv = threadIdx.x >> 6;
     u32 x = v;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
         const u32 y = __shfl_up(x, d, 64);
         if (lane >= d) x += y;
     }
-    return x - v;
+    if (lane == 63) L.wsum[wv] = x;
+    __syncthreads();
+    u32 off = 0, tot = 0;
+    for (u32 k = 0; k < PI_NL / 64; k++) {
+        const u32 s = L.wsum[k];
+        if (k < wv) off += s;
+        tot += s;
+    }
+    __syncthreads();
+    *total = tot;
+    return off + x - v;
 }
 
-__global__ __launch_bounds__(64) void inflate_par_kernel(const zcg_chunk* __restrict__ chunks,
-                                                         u32 n, u64 D, DType t, u32 vflags,
-                                                         i32* __restrict__ status) {
+// Bit position of token `j` of lane `i`: replay its path from the lane start.
+__device__ u32 token_pos(const ParLds& L, u32 R0, u32 bit0, u32 i, u32 j) {
+    u32 q = R0 + i * PI_SEG;
+    LaneBits s;
+    lb_init(s, L.in, q, bit0);
+    for (u32 k = 0; k < j; k++) {
+        lb_fill(s, L.in);
+        u32 adv;
+        decode_token(L, s.lo, &adv);
+        lb_drop(s, adv);
+        q += adv;
+    }
+    return q;
+}
+
+__global__ __launch_bounds__(PI_NL) void inflate_par_kernel(const zcg_chunk* __restrict__ chunks,
+                                                            u32 n, u64 D, DType t, u32 vflags,
+                                                            i32* __restrict__ status) {
     extern __shared__ __attribute__((aligned(16))) u8 smem_raw[];
     ParLds& L = *(ParLds*)smem_raw;
     const u32 c = blockIdx.x;
     if (c >= n) return;
-    const int lane = lane_id();
+    const u32 tid = threadIdx.x;
     const zcg_chunk ch = chunks[c];
-    if (D == 0) { if (lane == 0) status[c] = ZCG_OK; return; }
-    if (ch.dst_cap < D) { if (lane == 0) status[c] = ZCG_ERR_INVALID_INPUT; return; }
+    if (D == 0) { if (tid == 0) status[c] = ZCG_OK; return; }
+    if (ch.dst_cap < D) { if (tid == 0) status[c] = ZCG_ERR_INVALID_INPUT; return; }
     const u8* s = (const u8*)ch.src;
     const u64 n_in = ch.src_len;
     u64 h = 0;
     int st = gzip_header(s, n_in, &h);
     if (st == ZCG_OK && n_in - h >= (1ull << 28)) st = ZCG_ERR_UNSUPPORTED;  // u32 bit positions
-    if (st != ZCG_OK) { if (lane == 0) status[c] = st; return; }
+    if (st != ZCG_OK) { if (tid == 0) status[c] = st; return; }
 
     u8* dst = (u8*)ch.dst;
-    const u8* ds = s + h;                  // deflate stream
+    const u8* ds = s + h;  // deflate stream
     const u64 n_ds = n_in - h;
     const u32 total_bits = (u32)(n_ds * 8);
+    // Every wave runs the wave-uniform header/look-ahead code redundantly on
+    // the same data (block barriers inside), each with its own LDS cache.
     BitIn b;
-    bi_init(b, ds, n_ds, L.bcache);
-    u64 P = 0;                             // output bytes produced (and committed)
+    bi_init(b, ds, n_ds, L.bcache + (tid >> 6) * BI_CACHE_WORDS);
+    u64 P = 0;
     bool last = false, boundary = false, after_stored = false;
     int r = R_OK;
 
     while (r == R_OK && P < D) {
+        // ---- block header (all waves, identical) ------------------------------------
         if (last) { r = R_EXHAUSTED; break; }
         u32 type = 0, slen = 0;
         r = read_block_header(b, &last, &type, &slen, L.lens, &L.lh, L.ltab, &L.dh, L.dtab);
+        const u32 hdr_end = (u32)b.consumed;
         if (r != R_OK) break;
         if (type == 0) {
-            // ---- stored block: byte copies through the stage ----------------
-            u64 in0 = b.consumed >> 3;  // byte aligned after LEN/NLEN
+            // ---- stored block: byte copies through the stage --------------------
+            u64 in0 = hdr_end >> 3;  // byte aligned after LEN/NLEN
             u32 done = 0;
             while (done < slen && P < D) {
                 u32 k = slen - done;
                 if (k > PI_STAGE) k = PI_STAGE;
                 if ((u64)k > D - P) k = (u32)(D - P);
                 if (in0 + k > n_ds) { r = R_EXHAUSTED; break; }
-                for (u32 i = lane; i < k; i += 64) L.stage[(P + i) & (PI_STAGE - 1)] = ds[in0 + i];
+                for (u32 i = tid; i < k; i += PI_NL) L.stage[(P + i) & (PI_STAGE - 1)] = ds[in0 + i];
                 par_commit(L, dst, P, P + k, t);
                 P += k; in0 += k; done += k;
             }
@@ -228,14 +279,13 @@ __global__ __launch_bounds__(64) void inflate_par_kernel(const zcg_chunk* __rest
             continue;
         }
         after_stored = false;
-        // ---- Huffman block body: speculative parallel rounds -----------------
-        u32 R0 = (u32)b.consumed;
+        // ---- Huffman block body: speculative parallel rounds -------------------
+        u32 R0 = hdr_end;
         bool block_end = false;
         while (!block_end && r == R_OK && P < D) {
-            // stage the stream words of this round
             const u32 bit0 = R0 & ~31u;
             const u64 byte0 = bit0 >> 3;
-            for (u32 w = lane; w < PI_IN_WORDS; w += 64) {
+            for (u32 w = tid; w < PI_IN_WORDS; w += PI_NL) {
                 const u64 q = byte0 + 4ull * w;
                 u32 v = 0;
                 if (q + 4 <= n_ds) v = ld32(ds + q);
@@ -244,126 +294,168 @@ __global__ __launch_bounds__(64) void inflate_par_kernel(const zcg_chunk* __rest
                         if (q + i < n_ds) v |= (u32)ds[q + i] << (8 * i);
                 L.in[w] = v;
             }
-            for (u32 i = lane; i <= PI_LANES; i += 64) L.nstart[i] = 0;
+            for (u32 w = tid; w < PI_NL * PI_SEGW; w += PI_NL) L.mark[w] = 0;
             __syncthreads();
 
-            // ---- speculative decode --------------------------------------------
-            const u32 p = R0 + (u32)lane * PI_SEG;
-            const u32 limit = (lane == PI_LANES - 1) ? p + PI_SEG : p + PI_SEG + PI_MARGIN;
+            // ---- pass 1: decode my own segment, mark token starts ----------------
+            const u32 p = R0 + tid * PI_SEG;
+            const u32 pend = p + PI_SEG;
+            u32* mytok = L.tok + tid * PI_TMAX;
+            u32* mymark = L.mark + tid * PI_SEGW;
+            LaneBits bs;
+            lb_init(bs, L.in, p, bit0);
             u32 q = p, nt = 0;
-            u32* mytok = L.tok + lane * PI_TMAX;
-            u16* mypos = L.tpos + lane * PI_TMAX;
-            while (q < limit && nt < PI_TMAX) {
+            u32 nxt = 0xFFFFFFFFu;
+            while (q < pend) {
+                if (nt == PI_TMAX) { nxt = N_CAP; break; }
+                lb_fill(bs, L.in);
                 u32 adv;
-                u32 tk = decode_token(L, q, bit0, &adv);
+                u32 tk = decode_token(L, bs.lo, &adv);
                 if (q + adv > total_bits) tk = T_EXH;
-                mytok[nt] = tk;
-                mypos[nt] = (u16)(q - p);
-                nt++;
-                if (tok_is_marker(tk)) { q += (tk == T_EOB) ? adv : 0; break; }
+                mytok[nt++] = tk;
+                const u32 off = q - p;
+                mymark[off >> 5] |= 1u << (off & 31);
+                if (tok_is_marker(tk)) {
+                    if (tk == T_EOB) q += adv;
+                    nxt = N_MARKER;
+                    break;
+                }
+                lb_drop(bs, adv);
                 q += adv;
             }
-            L.ntok[lane] = nt;
-            L.endp[lane] = q;
+            __syncthreads();
+            // ---- pass 2: follow my path until it meets a marked token start -----
+            const u32 round_hi = R0 + PI_NL * PI_SEG;
+            u32 give = 0;
+            while (nxt == 0xFFFFFFFFu) {
+                if (q >= round_hi) { nxt = N_ROUND_END; break; }
+                const u32 k = (q - R0) / PI_SEG;
+                const u32 off = q - (R0 + k * PI_SEG);
+                const u32 mw = L.mark[k * PI_SEGW + (off >> 5)];
+                if (mw & (1u << (off & 31))) {
+                    // sync: index of that token in lane k's list = marks below it
+                    u32 cnt = __popc(mw & ((1u << (off & 31)) - 1));
+                    for (u32 x = 0; x < (off >> 5); x++) cnt += __popc(L.mark[k * PI_SEGW + x]);
+                    nxt = k;
+                    give = cnt;
+                    break;
+                }
+                if (nt == PI_TMAX) { nxt = N_CAP; break; }
+                lb_fill(bs, L.in);
+                u32 adv;
+                u32 tk = decode_token(L, bs.lo, &adv);
+                if (q + adv > total_bits) tk = T_EXH;
+                mytok[nt++] = tk;
+                if (tok_is_marker(tk)) {
+                    if (tk == T_EOB) q += adv;
+                    nxt = N_MARKER;
+                    break;
+                }
+                lb_drop(bs, adv);
+                q += adv;
+            }
+            L.next[tid] = nxt;
+            L.endp[tid] = q;
+            L.give[tid] = give;
+            L.ntok[tid] = nt;
             __syncthreads();
 
-            // ---- sync with the next lane's path --------------------------------
-            i32 cut = -1;  // index of my first token owned by lane+1
-            if (lane < (int)PI_LANES - 1) {
-                const u32 pn = p + PI_SEG;
-                const u32 nn = L.ntok[lane + 1];
-                const u16* npos = L.tpos + (lane + 1) * PI_TMAX;
-                u32 j = 0;
-                for (u32 a = 0; a < nt; a++) {
-                    const u32 pa = p + mypos[a];
-                    if (pa < pn) continue;
-                    while (j < nn && pn + npos[j] < pa) j++;
-                    if (j >= nn) break;
-                    if (pn + npos[j] == pa) { cut = (i32)a; L.nstart[lane + 1] = (i32)j; break; }
+            // ---- chain: lane 0 is true; follow sync targets --------------------------
+            // Common case next[i] == i+1; one thread walks the exceptions.
+            if (tid == 0) {
+                u32 cur = 0, endl = 0;
+                L.sidx[0] = 0;
+                for (;;) {
+                    u32 a = cur;
+                    while (a + 1 < PI_NL && L.next[a] == a + 1) { L.sidx[a + 1] = L.give[a]; a++; }
+                    // lane a: stop code or a skip
+                    const u32 nx = L.next[a];
+                    if (nx < PI_NL) {  // skip to a later lane
+                        L.sidx[nx] = L.give[a];
+                        for (u32 d2 = a + 1; d2 < nx; d2++) L.sidx[d2] = 0xFFFFFFFFu;  // dead
+                        cur = nx;
+                        continue;
+                    }
+                    endl = a;
+                    break;
                 }
+                for (u32 d2 = endl + 1; d2 < PI_NL; d2++) L.sidx[d2] = 0xFFFFFFFFu;
+                L.ctl[5] = endl;
             }
             __syncthreads();
-            const i32 a0 = L.nstart[lane];
-            // valid range [a0, bnd) and whether this lane ends the chain
-            const bool last_is_marker = nt > 0 && tok_is_marker(mytok[nt - 1]);
-            u32 bnd = (cut >= 0) ? (u32)cut : nt;
-            bool brk = (cut < 0);
+            const u32 E = L.ctl[5];
+            const u32 my_s = L.sidx[tid];
+            const bool on = (tid <= E) && my_s != 0xFFFFFFFFu;
+            u32 vend = nt;
             u32 marker = 0;
-            if (last_is_marker && nt - 1 < bnd) {  // marker lies on my valid range
-                bnd = nt - 1;
-                brk = true;
-                marker = mytok[nt - 1];
-            }
-            const unsigned long long bm = __ballot(brk);
-            const int Lb = (int)__builtin_ctzll(bm);  // lane that ends the chain (lane 63 always breaks)
-            const bool active = lane <= Lb;
-            // ---- output placement -------------------------------------------------
+            if (on && tid == E && nxt == N_MARKER) { vend = nt - 1; marker = mytok[nt - 1]; }
+            // ---- placement ------------------------------------------------------------------
             u32 olen = 0;
-            if (active)
-                for (u32 a = (u32)a0; a < bnd; a++) olen += tok_len(mytok[a]);
-            const u32 base = wave_excl_scan(olen);
-            const u32 total = __shfl(base + olen, Lb, 64);
+            if (on)
+                for (u32 a = my_s; a < vend; a++) olen += tok_len(mytok[a]);
+            u32 total;
+            const u32 base = block_excl_scan(L, olen, &total);
             const u64 room = D - P;
             const u32 cap = room < PI_STAGE ? (u32)room : PI_STAGE;
-            // round end (bit position of the first token not taken) and status
-            u32 round_end = __shfl(L.endp[Lb] , Lb, 64);
-            u32 mk = __shfl(marker, Lb, 64);
-            u32 take_lane = Lb;  // last lane whose tokens are (partly) taken
-            u32 take_end = bnd;  // per-lane: tokens [a0, take_end) are emitted
-            bool final_round = false, fin_boundary = false;
-            if (total > cap || (total == cap && cap == room)) {
-                // cut at `cap` bytes: first lane whose prefix reaches cap
-                const bool over = active && (base + olen >= cap) && olen > 0;
-                const unsigned long long om = __ballot(over && base < cap);
-                const int cl = om ? (int)__builtin_ctzll(om) : Lb;
-                take_lane = cl;
-                mk = 0;
-                if (lane == cl) {
-                    u32 acc = base, a = (u32)a0;
-                    if (cap == room) {
-                        // final round: take tokens until N bytes exist
-                        while (a < bnd && acc < cap) { acc += tok_len(mytok[a]); a++; }
-                        L.ctl[1] = (acc == cap) ? 1u : 0u;  // exact boundary -> look-ahead
-                        L.ctl[2] = a < nt ? p + mypos[a] : L.endp[lane];
-                    } else {
-                        while (a < bnd && acc + tok_len(mytok[a]) <= cap) { acc += tok_len(mytok[a]); a++; }
-                        L.ctl[1] = 0;
-                        L.ctl[2] = a < nt ? p + mypos[a] : L.endp[lane];
-                    }
-                    L.ctl[0] = acc;  // bytes emitted this round
-                    take_end = a;
-                }
-                final_round = (cap == room);
-                __syncthreads();
-                fin_boundary = L.ctl[1] != 0;
-                round_end = L.ctl[2];
-                if (lane > cl) take_end = (u32)a0;  // nothing taken
-            }
-            const bool take = lane <= (int)take_lane;
-            if (!take) take_end = (u32)a0;
-            const u32 emitted = (total > cap || (total == cap && cap == room)) ? L.ctl[0] : total;
+            u32 take_end = on ? vend : my_s;
+            u32 emitted = total;
+            u32 round_end = L.endp[E];
+            if (tid == E) L.ctl[6] = marker;
             __syncthreads();
-            // ---- errors on the taken range -----------------------------------------
+            u32 mk = L.ctl[6];
+            bool final_round = false, fin_boundary = false;
+            const bool cut = total > cap || (total == cap && cap == room);
+            if (cut) {
+                // the lane whose output range holds byte `cap`
+                const bool mine = on && olen > 0 && base < cap && base + olen >= cap;
+                if (mine) {
+                    u32 acc = base, a = my_s;
+                    if (cap == room) {
+                        while (a < vend && acc < cap) { acc += tok_len(mytok[a]); a++; }
+                        L.ctl[7] = (acc == cap) ? 1u : 0u;
+                    } else {
+                        while (a < vend && acc + tok_len(mytok[a]) <= cap) { acc += tok_len(mytok[a]); a++; }
+                        L.ctl[7] = 0;
+                    }
+                    L.ctl[8] = acc;
+                    L.ctl[9] = tid;
+                    L.ctl[10] = a;
+                }
+                __syncthreads();
+                const u32 cl = L.ctl[9];
+                emitted = L.ctl[8];
+                fin_boundary = L.ctl[7] != 0;
+                final_round = (cap == room);
+                mk = 0;
+                if (tid > cl) take_end = my_s;
+                if (tid == cl) take_end = L.ctl[10];
+                if (tid == 0) {  // bit position of the first token not taken
+                    const u32 a = L.ctl[10];
+                    L.ctl[11] = (a < L.ntok[cl]) ? token_pos(L, R0, bit0, cl, a) : L.endp[cl];
+                }
+                __syncthreads();
+                round_end = L.ctl[11];
+            }
+            // ---- errors on the taken range ----------------------------------------------------
             if (mk == T_BAD) { r = R_INVALID; break; }
             if (mk == T_EXH) { r = R_EXHAUSTED; break; }
-            // "invalid distance too far back": dist > bytes before the match
             bool far = false;
             {
                 u32 o = base;
-                for (u32 a = (u32)a0; a < take_end; a++) {
+                for (u32 a = my_s; a < take_end; a++) {
                     const u32 tk = mytok[a];
                     if ((tk & T_MATCH) && tok_dist(tk) > P + o) far = true;
                     o += tok_len(tk);
                 }
             }
-            if (__any(far)) { r = R_INVALID; break; }
-            // ---- literals --------------------------------------------------------------
+            if (__syncthreads_or(far)) { r = R_INVALID; break; }
+            // ---- literals ------------------------------------------------------------------------
             const u64 S = P;
-            for (u32 w = lane; w < PI_STAGE / 32; w += 64) L.resolved[w] = 0;
+            for (u32 w = tid; w < PI_STAGE / 32; w += PI_NL) L.resolved[w] = 0;
             __syncthreads();
             {
                 u32 o = base;
-                for (u32 a = (u32)a0; a < take_end; a++) {
+                for (u32 a = my_s; a < take_end; a++) {
                     const u32 tk = mytok[a];
                     if (!(tk & T_MATCH)) {
                         L.stage[(S + o) & (PI_STAGE - 1)] = (u8)tk;
@@ -373,9 +465,9 @@ __global__ __launch_bounds__(64) void inflate_par_kernel(const zcg_chunk* __rest
                 }
             }
             __syncthreads();
-            // ---- matches: multi-round resolution ---------------------------------------
+            // ---- matches: multi-round resolution -----------------------------------------------
             {
-                u32 a = (u32)a0, o = base;
+                u32 a = my_s, o = base;
                 for (;;) {
                     while (a < take_end) {
                         const u32 tk = mytok[a];
@@ -387,7 +479,7 @@ __global__ __launch_bounds__(64) void inflate_par_kernel(const zcg_chunk* __rest
                         bool ready = true;
                         if (src + (int64_t)span > 0) {
                             const u32 lo = src < 0 ? 0u : (u32)src;
-                            const u32 hi = (u32)(src + span);  // exclusive, <= o
+                            const u32 hi = (u32)(src + span);
                             for (u32 x = lo; x < hi && ready;) {
                                 const u32 wv = L.resolved[x >> 5];
                                 const u32 nb = (hi - x) < (32 - (x & 31)) ? (hi - x) : (32 - (x & 31));
@@ -397,7 +489,6 @@ __global__ __launch_bounds__(64) void inflate_par_kernel(const zcg_chunk* __rest
                             }
                         }
                         if (!ready) break;
-                        // out[o+k] = B[src + k mod d], reads independent of this match's writes
                         u32 ph = 0;
                         for (u32 k = 0; k < len; k += 8) {
                             u8 v[8];
@@ -410,7 +501,6 @@ __global__ __launch_bounds__(64) void inflate_par_kernel(const zcg_chunk* __rest
                             for (int z = 0; z < 8; z++)
                                 if (k + z < len) L.stage[(S + o + k + z) & (PI_STAGE - 1)] = v[z];
                         }
-                        // mark [o, o+len) resolved
                         for (u32 x = o; x < o + len;) {
                             const u32 nb = (o + len - x) < (32 - (x & 31)) ? (o + len - x) : (32 - (x & 31));
                             const u32 m = (nb == 32) ? 0xFFFFFFFFu : (((1u << nb) - 1) << (x & 31));
@@ -420,12 +510,10 @@ __global__ __launch_bounds__(64) void inflate_par_kernel(const zcg_chunk* __rest
                         a++;
                         o += len0;
                     }
-                    __builtin_amdgcn_wave_barrier();
-                    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-                    if (!__any(a < take_end)) break;
+                    if (!__syncthreads_or(a < take_end)) break;
                 }
             }
-            // ---- commit ----------------------------------------------------------------------
+            // ---- commit -------------------------------------------------------------------------------
             par_commit(L, dst, S, S + emitted, t);
             P = S + emitted;
             if (final_round) {
@@ -435,12 +523,12 @@ __global__ __launch_bounds__(64) void inflate_par_kernel(const zcg_chunk* __rest
             }
             if (mk == T_EOB) {
                 block_end = true;
-                bi_seek(b, round_end);  // endp of the EOB lane: bit after EOB
+                bi_seek(b, round_end);  // bit after the EOB code
             }
             R0 = round_end;
-            if (P >= D) { boundary = true; bi_seek(b, R0); }
         }
     }
+    // zlib's post-N look-ahead (all waves, identical); see zcg_inflate_common.h
     if (r == R_OK && P >= D && boundary) {
         const u64 last_byte = h + (b.consumed ? (b.consumed - 1) / 8 : 0);
         u64 wend = (last_byte / 32768 + 1) * 32768;
@@ -453,10 +541,8 @@ __global__ __launch_bounds__(64) void inflate_par_kernel(const zcg_chunk* __rest
     }
     if (r == R_INVALID) st = ZCG_ERR_INVALID_DATA;
     else if (r == R_EXHAUSTED || P < D) st = ZCG_ERR_UNEXPECTED_EOF;
-    if (lane == 0) status[c] = st;
+    if (tid == 0) status[c] = st;
 }
-
-size_t inflate_par_lds_bytes() { return sizeof(ParLds); }
 
 hipError_t launch_inflate_par(const zcg_array* a, const zcg_chunk* d_chunks, uint32_t n,
                               int32_t* d_status, hipStream_t s) {
@@ -471,7 +557,7 @@ hipError_t launch_inflate_par(const zcg_array* a, const zcg_chunk* d_chunks, uin
         if (e != hipSuccess) return e;
         attr_set = true;
     }
-    hipLaunchKernelGGL(inflate_par_kernel, dim3(n), dim3(64), lds, s, d_chunks, n, D, t,
+    hipLaunchKernelGGL(inflate_par_kernel, dim3(n), dim3(PI_NL), lds, s, d_chunks, n, D, t,
                        a->compression.flags, d_status);
     return hipGetLastError();
 }
