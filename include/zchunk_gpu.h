@@ -74,6 +74,8 @@ enum zcg_status {
 /* Use the wave-serial inflate kernel instead of the parallel one (the two are
  * bit-identical; the serial one is kept as a differential reference). */
 #define ZCG_FLAG_SERIAL_INFLATE 0x100u
+/* Accumulate internal kernel statistics (development builds / profiling). */
+#define ZCG_FLAG_DEBUG_COUNTERS 0x200u
 
 /* CompressionType + its configuration (camelCase JSON keys in the reference). */
 typedef struct zcg_compression {

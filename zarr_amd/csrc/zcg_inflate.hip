@@ -27,8 +27,8 @@ __global__ __launch_bounds__(64) void inflate_kernel(const zcg_chunk* __restrict
                                                      u64 D, DType t, u32 vflags,
                                                      i32* __restrict__ status) {
     __shared__ __attribute__((aligned(16))) u8 ring[INF_RING];
-    __shared__ u32 ltab[1u << INF_LBITS];
-    __shared__ u32 dtab[1u << INF_DBITS];
+    __shared__ u32 ltab[INF_LTAB];
+    __shared__ u32 dtab[INF_DTAB];
     __shared__ HuffLds lh, dh;
     __shared__ u8 lens[320];
     __shared__ u32 bcache[BI_CACHE_WORDS];
@@ -94,7 +94,7 @@ __global__ __launch_bounds__(64) void inflate_kernel(const zcg_chunk* __restrict
         for (;;) {
             if (o.P >= D) { boundary = true; break; }
             u32 e;
-            r = decode_sym(b, ltab, INF_LBITS, &lh, false, &e);
+            r = decode_sym(b, ltab, INF_LBITS, &e);
             if (r != R_OK) break;
             const u32 kind = (e >> 24) & 15;
             if (kind == K_LIT) {
@@ -104,7 +104,7 @@ __global__ __launch_bounds__(64) void inflate_kernel(const zcg_chunk* __restrict
                 if (!bi_has(b, ex)) { r = R_EXHAUSTED; break; }
                 u32 len = (e & 0xFFFF) + (ex ? bi_bits(b, ex) : 0);
                 u32 de;
-                r = decode_sym(b, dtab, INF_DBITS, &dh, true, &de);
+                r = decode_sym(b, dtab, INF_DBITS, &de);
                 if (r != R_OK) break;
                 if (((de >> 24) & 15) != K_DIST) { r = R_INVALID; break; }
                 const u32 dex = (de >> 16) & 0xFF;

@@ -8,13 +8,18 @@
 namespace zcg {
 
 
-constexpr int INF_LBITS = 10;
-constexpr int INF_DBITS = 8;
+constexpr int INF_LBITS = 10;  // literal/length root table bits
+constexpr int INF_DBITS = 8;   // distance root table bits
+constexpr u32 INF_LTAB = 1536; // root 1024 + subtables (zlib enough(286,10,15) = 1334)
+constexpr u32 INF_DTAB = 512;  // root 256 + subtables (enough(30,8,15) = 402)
 constexpr u32 INF_RING = 32768;
 constexpr u32 INF_FLUSH = 16384;
 
-// entry: [31:28] codelen (0 => slow path) | [27:24] kind | [23:16] extra | [15:0] value
-enum : u32 { K_LIT = 0, K_LEN = 1, K_EOB = 2, K_BAD = 3, K_DIST = 4 };
+// Two-level tables: every code decodes in <= 2 LDS lookups (no bit-serial
+// path: a rare per-lane slow path would stall whole 64-lane waves).
+// entry: [31:28] code length | [27:24] kind | [23:16] extra bits | [15:0] value
+//        K_SUB: [23:16] subtable bits, [15:0] subtable offset (code length 0)
+enum : u32 { K_LIT = 0, K_LEN = 1, K_EOB = 2, K_BAD = 3, K_DIST = 4, K_SUB = 5 };
 
 __constant__ u16 c_len_base[29] = {3,  4,  5,  6,  7,  8,  9,  10, 11,  13,  15,  17,  19,  23, 27,
                                    31, 35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
@@ -32,9 +37,11 @@ __device__ __forceinline__ u32 mk_entry(u32 len, u32 kind, u32 extra, u32 val) {
     return (len << 28) | (kind << 24) | (extra << 16) | val;
 }
 
-// Canonical Huffman code description in LDS (puff.c style).
+// Canonical Huffman code description in LDS (built per block).
 struct HuffLds {
-    u16 count[16];
+    u32 count[16];
+    u32 first[16];  // first canonical code of each length
+    u32 offs[16];   // index of the first symbol of each length in sym[]
     u16 sym[288];
 };
 
@@ -50,82 +57,123 @@ __device__ __forceinline__ u32 sym_entry(u32 s, u32 len, bool dist) {
     return mk_entry(len, K_BAD, 0, 0);
 }
 
-// Build canonical code + primary table from lengths[0..nsym) (wave-cooperative).
-// Returns 0 ok, -1 over-subscribed/incomplete (zlib inflate_table rules).
-__device__ int build_table(const u8* lens, u32 nsym, HuffLds* h, u32* table, int tbits, bool dist) {
-    // block-cooperative: every thread of the workgroup calls this uniformly
+__device__ __forceinline__ u32 bitrev(u32 v, int n) { return __builtin_bitreverse32(v) >> (32 - n); }
+
+// Canonical decode of stream bits `bits` (LSB = first bit) over at most
+// `maxbits` bits; returns the table entry (K_BAD, length 1, if no code).
+__device__ __forceinline__ u32 canon_decode(const HuffLds* h, u32 bits, int maxbits, bool dist) {
+    u32 code = 0;
+    for (int l = 1; l <= maxbits; l++) {
+        code = (code << 1) | ((bits >> (l - 1)) & 1);
+        const u32 cnt = h->count[l];
+        if (code - h->first[l] < cnt) return sym_entry(h->sym[h->offs[l] + (code - h->first[l])], l, dist);
+    }
+    return mk_entry(1, K_BAD, 0, 0);
+}
+
+// Build the canonical code and the two-level table from lens[0..nsym)
+// (block-cooperative: every thread of the workgroup calls this uniformly).
+// Returns 0 ok, -1 over-subscribed or incomplete (zlib inflate_table rules:
+// an incomplete code is only allowed when it is a single length-1 code).
+__device__ int build_table(const u8* lens, u32 nsym, HuffLds* h, u32* table, int root, bool dist) {
     const u32 tid = threadIdx.x, nth = blockDim.x;
-    __shared__ u16 s_offs[16];
+    __shared__ u32 s_part[256 / 64 + 1];
     __syncthreads();
     if (tid < 16) h->count[tid] = 0;
     __syncthreads();
-    if (tid == 0) {
-        for (u32 s = 0; s < nsym; s++) h->count[lens[s]]++;
-    }
+    for (u32 s = tid; s < nsym; s += nth)
+        if (lens[s]) atomicAdd(&h->count[lens[s]], 1u);
     __syncthreads();
     int ok = 1, maxlen = 0;
     {
         int left = 1;
         for (int l = 1; l <= 15; l++) {
             left <<= 1;
-            left -= h->count[l];
+            left -= (int)h->count[l];
             if (left < 0) ok = 0;  // over-subscribed
             if (h->count[l]) maxlen = l;
         }
-        // incomplete codes are only allowed for a single length-1 code
         if (ok && left > 0 && maxlen > 1) ok = 0;
     }
     if (tid == 0) {
-        u32 o = 0;
-        s_offs[0] = 0;
-        for (int l = 1; l < 16; l++) { s_offs[l] = o; o += h->count[l]; }
-        for (u32 s = 0; s < nsym; s++)
-            if (lens[s]) h->sym[s_offs[lens[s]]++] = (u16)s;
+        u32 o = 0, f = 0;
+        h->count[0] = 0;
+        for (int l = 1; l < 16; l++) {
+            f = (f + h->count[l - 1]) << 1;
+            h->first[l] = f;
+            h->offs[l] = o;
+            o += h->count[l];
+        }
     }
     __syncthreads();
-    // primary table: slot bits are stream-order (LSB first)
-    const u32 nslots = 1u << tbits;
-    for (u32 slot = tid; slot < nslots; slot += nth) {
-        u32 code = 0, first = 0, index = 0, e = mk_entry(0, K_BAD, 0, 0);
-        bool found = false;
-        for (int l = 1; l <= tbits; l++) {
-            code |= (slot >> (l - 1)) & 1;
-            const u32 cnt = h->count[l];
-            if (code - first < cnt) {  // unsigned compare also covers code < first
-                e = sym_entry(h->sym[index + (code - first)], l, dist);
-                found = true;
-                break;
+    // canonical order: a symbol's rank among the symbols of its length
+    for (u32 s = tid; s < nsym; s += nth) {
+        const u32 L = lens[s];
+        if (!L) continue;
+        u32 rank = 0;
+        for (u32 x = 0; x < s; x++) rank += (lens[x] == L);
+        h->sym[h->offs[L] + rank] = (u16)s;
+    }
+    __syncthreads();
+    // root slots: direct entries, or the size of the subtable they head
+    const u32 nroot = 1u << root;
+    const u32 per = (nroot + nth - 1) / nth;  // contiguous slots per thread
+    u32 mysum = 0;
+    for (u32 k = 0; k < per; k++) {
+        const u32 slot = tid * per + k;
+        if (slot >= nroot) break;
+        u32 e = canon_decode(h, slot, root, dist);
+        if (((e >> 24) & 15) == K_BAD && maxlen > root) {
+            // prefix of longer codes: subtable of 2^(maxL - root) entries
+            const u32 pv = bitrev(slot, root);
+            int mx = 0;
+            for (int L = root + 1; L <= maxlen; L++) {
+                const u32 lo = pv << (L - root), hi = (pv + 1) << (L - root);
+                const u32 f = h->first[L], fe = f + h->count[L];
+                if (h->count[L] && lo < fe && f < hi) mx = L;
             }
-            index += cnt;
-            first += cnt;
-            first <<= 1;
-            code <<= 1;
+            if (mx) {
+                e = mk_entry(0, 0xF, 0, (u32)(mx - root));  // temporary: subtable size marker
+                mysum += 1u << (mx - root);
+            }
         }
-        if (!found) e = (maxlen > tbits) ? mk_entry(0, K_LEN, 0, 0) /* slow path */
-                                         : mk_entry(0, K_BAD, 0, 0);
         table[slot] = e;
+    }
+    // exclusive scan of the per-thread subtable sizes
+    u32 x = mysum;
+    const int lane = lane_id();
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const u32 y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
+    }
+    if (lane == 63) s_part[tid >> 6] = x;
+    __syncthreads();
+    u32 off = nroot;
+    for (u32 w = 0; w < (tid >> 6); w++) off += s_part[w];
+    off += x - mysum;
+    for (u32 k = 0; k < per; k++) {
+        const u32 slot = tid * per + k;
+        if (slot >= nroot) break;
+        const u32 e = table[slot];
+        if (((e >> 24) & 15) == 0xF) {
+            const u32 sb = e & 0xFF;
+            table[slot] = mk_entry(0, K_SUB, sb, off);
+            // fill the subtable: stream bits = slot (root bits) then j (sb bits)
+            for (u32 j = 0; j < (1u << sb); j++)
+                table[off + j] = canon_decode(h, slot | (j << root), root + sb, dist);
+            off += 1u << sb;
+        }
     }
     __syncthreads();
     return ok ? 0 : -1;
 }
 
-// Canonical decode of a long code from the bits of v (LSB first).
-__device__ __forceinline__ u32 slow_sym(u64 v, const HuffLds* h, bool dist, u32* used) {
-    int code = 0, first = 0, index = 0;
-    for (int len = 1; len <= 15; len++) {
-        code |= (int)((v >> (len - 1)) & 1);
-        const int cnt = h->count[len];
-        if (code - cnt < first) {
-            *used = len;
-            return sym_entry(h->sym[index + (code - first)], len, dist);
-        }
-        index += cnt;
-        first += cnt;
-        first <<= 1;
-        code <<= 1;
-    }
-    *used = 0;
-    return mk_entry(0, K_BAD, 0, 0);
+// Look up a symbol from >= 15 stream bits `v` (two levels).
+__device__ __forceinline__ u32 table_lookup(const u32* tab, int root, u32 v) {
+    u32 e = tab[v & ((1u << root) - 1)];
+    if (((e >> 24) & 15) == K_SUB) e = tab[(e & 0xFFFF) + ((v >> root) & ((1u << ((e >> 16) & 0xFF)) - 1))];
+    return e;
 }
 
 // Wave-uniform bit reader (every lane holds the same state).  Input words
@@ -258,43 +306,20 @@ __device__ __forceinline__ void put_match(InfOut& o, u32 len, u32 dist) {
 // "zlib waits for input" in the look-ahead), or corrupt.
 enum : int { R_OK = 0, R_EXHAUSTED = 1, R_INVALID = 2 };
 
-// Decode one symbol: primary table, else canonical bit-serial decode.
-__device__ __forceinline__ int decode_sym(BitIn& b, const u32* tab, int tbits, const HuffLds* h,
-                                          bool dist, u32* out) {
+// Decode one symbol (two-level table) with the wave-uniform reader.
+__device__ __forceinline__ int decode_sym(BitIn& b, const u32* tab, int root, u32* out) {
     bi_refill(b);
-    u32 e = __builtin_amdgcn_readfirstlane(tab[bi_peek(b, tbits)]);
-    u32 l = e >> 28;
-    if (l != 0) {
-        if (!bi_has(b, l)) return R_EXHAUSTED;
-        bi_drop(b, l);
-        *out = e;
-        return R_OK;
-    }
-    if (((e >> 24) & 15) == K_BAD) {  // unused slot of an incomplete (1-bit) code
-        if (!bi_has(b, 1)) return R_EXHAUSTED;
-        return R_INVALID;
-    }
-    int code = 0, first = 0, index = 0;
-    for (int len = 1; len <= 15; len++) {
-        if (!bi_has(b, 1)) return R_EXHAUSTED;
-        bi_refill(b);
-        code |= (int)bi_peek(b, 1);
-        bi_drop(b, 1);
-        const int cnt = h->count[len];
-        if (code - cnt < first) {
-            *out = sym_entry(h->sym[index + (code - first)], len, dist);
-            return R_OK;
-        }
-        index += cnt;
-        first += cnt;
-        first <<= 1;
-        code <<= 1;
-    }
-    return R_INVALID;
+    const u32 e = __builtin_amdgcn_readfirstlane(table_lookup(tab, root, bi_peek(b, 15)));
+    const u32 l = e >> 28;
+    if (!bi_has(b, l)) return R_EXHAUSTED;
+    if (((e >> 24) & 15) == K_BAD) return R_INVALID;
+    bi_drop(b, l);
+    *out = e;
+    return R_OK;
 }
 
 // Dynamic block header (RFC 1951 3.2.7) -> tables; zlib's validity rules.
-__device__ int read_dynamic(BitIn& b, u8* lens, HuffLds* lh, u32* ltab, HuffLds* dh, u32* dtab) {
+__device__ __attribute__((always_inline)) int read_dynamic(BitIn& b, u8* lens, HuffLds* lh, u32* ltab, HuffLds* dh, u32* dtab) {
     const u32 tid = threadIdx.x, nth = blockDim.x;
     if (!bi_has(b, 14)) return R_EXHAUSTED;
     const u32 nlen = bi_bits(b, 5) + 257, ndist = bi_bits(b, 5) + 1, ncode = bi_bits(b, 4) + 4;
@@ -318,7 +343,7 @@ __device__ int read_dynamic(BitIn& b, u8* lens, HuffLds* lh, u32* ltab, HuffLds*
     u8 prev = 0;
     while (idx < nlen + ndist) {
         u32 e;
-        int r = decode_sym(b, ltab, 7, lh, false, &e);
+        int r = decode_sym(b, ltab, 7, &e);
         if (r != R_OK) return r;
         const u32 sym = e & 0xFFFF;
         if (sym < 16) {
@@ -372,7 +397,7 @@ __device__ void fixed_tables(u8* lens, HuffLds* lh, u32* ltab, HuffLds* dh, u32*
 
 // Block header: 3 bits, then stored-length check / table construction.
 // *type receives BTYPE; for stored blocks *slen the LEN field.
-__device__ int read_block_header(BitIn& b, bool* last, u32* type, u32* slen, u8* lens, HuffLds* lh,
+__device__ __attribute__((always_inline)) int read_block_header(BitIn& b, bool* last, u32* type, u32* slen, u8* lens, HuffLds* lh,
                                  u32* ltab, HuffLds* dh, u32* dtab) {
     if (!bi_has(b, 3)) return R_EXHAUSTED;
     const u32 hdr = bi_bits(b, 3);
@@ -397,7 +422,7 @@ __device__ int read_block_header(BitIn& b, bool* last, u32* type, u32* slen, u8*
 // next literal/length code, length extra bits, distance code, distance
 // extra bits, and whole block headers are validated.  The input it was
 // given is the rest of flate2's current 32 KiB BufReader window.
-__device__ int inf_lookahead(BitIn& b, bool last, bool at_header, u8* lens, HuffLds* lh,
+__device__ __attribute__((always_inline)) int inf_lookahead(BitIn& b, bool last, bool at_header, u8* lens, HuffLds* lh,
                              u32* ltab, HuffLds* dh, u32* dtab) {
     for (;;) {
         if (at_header) {  // after a stored block: straight to the next header
@@ -413,7 +438,7 @@ __device__ int inf_lookahead(BitIn& b, bool last, bool at_header, u8* lens, Huff
             }
         }
         u32 e;
-        int r = decode_sym(b, ltab, INF_LBITS, lh, false, &e);
+        int r = decode_sym(b, ltab, INF_LBITS, &e);
         if (r != R_OK) return r;
         const u32 kind = (e >> 24) & 15;
         if (kind == K_LIT) return R_OK;
@@ -423,7 +448,7 @@ __device__ int inf_lookahead(BitIn& b, bool last, bool at_header, u8* lens, Huff
             if (!bi_has(b, ex)) return R_EXHAUSTED;
             if (ex) bi_bits(b, ex);
             u32 de;
-            r = decode_sym(b, dtab, INF_DBITS, dh, true, &de);
+            r = decode_sym(b, dtab, INF_DBITS, &de);
             if (r != R_OK) return r;
             if (((de >> 24) & 15) != K_DIST) return R_INVALID;  // "invalid distance code"
             return R_OK;  // DISTEXT then MATCH: zlib leaves there (left == 0)

@@ -38,11 +38,16 @@ namespace zcg {
 
 constexpr u32 PI_NL = 256;       // lanes per chunk (4 waves)
 constexpr u32 PI_SEG = 256;      // bits per lane segment
-constexpr u32 PI_TMAX = 56;      // tokens stored per lane per round
+constexpr u32 PI_BLK = 16;       // tokens per pool block
+constexpr u32 PI_LBLK = 5;       // pool blocks per lane -> up to 80 tokens per lane
+constexpr u32 PI_TMAX = PI_BLK * PI_LBLK;
+constexpr u32 PI_NBLK = 640;     // pool blocks per round (avg need ~1.7 per lane)
 constexpr u32 PI_STAGE = 32768;  // output bytes per round (power of 2)
 constexpr u32 PI_WIN = 32768;    // LZ77 window ring
 constexpr u32 PI_SEGW = PI_SEG / 32;
-constexpr u32 PI_IN_WORDS = (PI_NL * PI_SEG + PI_TMAX * 48 + 512) / 32 + 8;
+constexpr u32 PI_IN_VEC = (PI_NL * PI_SEG + 1024) / 128 + 2;  // staged 16-B vectors
+constexpr u32 PI_IN_WORDS = PI_IN_VEC * 4;
+constexpr u32 PI_MAXSEG = 64;    // chain segments tracked per round
 
 // token word: literal = byte value; match = 1<<31 | (len-3)<<16 | (dist-1);
 // markers (bit 30): EOB, invalid code, input exhausted.
@@ -56,6 +61,23 @@ constexpr u32 N_ROUND_END = PI_NL;  // reached the end of the round's range
 constexpr u32 N_MARKER = PI_NL + 1; // last stored token is a marker
 constexpr u32 N_CAP = PI_NL + 2;    // token store full before syncing
 
+// Debug counters (flag ZCG_FLAG_DEBUG_COUNTERS): summed over all chunks.
+__device__ unsigned long long g_inf_dbg[32];
+enum { DBG_ROUNDS, DBG_CHAIN, DBG_END_CAP, DBG_END_EOB, DBG_END_BAD, DBG_SKIPS, DBG_MRR_IT,
+       DBG_CUTS, DBG_BLOCKS, DBG_BYTES, DBG_TOKENS, DBG_END_ROUND, DBG_PASS2_TOK };
+
+// phase timers (debug): slots 16.. of g_inf_dbg
+enum { TP_HDR = 16, TP_STAGE, TP_PASS1, TP_PASS2, TP_CHAIN, TP_PLACE, TP_LIT, TP_MRR, TP_COMMIT, TP_TOTAL };
+#define TSTAMP(slot)                                                                 \
+    do {                                                                             \
+        if (dbg) {                                                                   \
+            __syncthreads();                                                         \
+            const u64 _t = __builtin_readcyclecounter();                             \
+            if (tid == 0) atomicAdd(&g_inf_dbg[slot], (unsigned long long)(_t - t_last)); \
+            t_last = _t;                                                             \
+        }                                                                            \
+    } while (0)
+
 __device__ __forceinline__ bool tok_is_marker(u32 t) { return (t & 0xC0000000u) == 0x40000000u; }
 __device__ __forceinline__ u32 tok_len(u32 t) { return (t & T_MATCH) ? ((t >> 16) & 0xFF) + 3 : 1; }
 __device__ __forceinline__ u32 tok_dist(u32 t) { return (t & 0x7FFF) + 1; }
@@ -64,11 +86,12 @@ struct ParLds {
     u8 win[PI_WIN];                  // LZ77 window ring (absolute pos & 32767)
     u8 stage[PI_STAGE];              // round output (absolute pos & 32767)
     u32 in[PI_IN_WORDS];             // staged stream words
-    u32 tok[PI_NL * PI_TMAX];        // tokens, lane-major
+    u32 pool[PI_NBLK * PI_BLK];      // token pool: lanes take 16-token blocks
+    u16 blk[PI_NL * PI_LBLK];        // each lane's pool blocks
     u32 mark[PI_NL * PI_SEGW];       // token-start bitmap of each lane's own segment
     u32 resolved[PI_STAGE / 32];     // MRR bitmap over round offsets
-    u32 ltab[1u << INF_LBITS];
-    u32 dtab[1u << INF_DBITS];
+    u32 ltab[INF_LTAB];
+    u32 dtab[INF_DTAB];
     HuffLds lh, dh;
     u8 lens[320];
     u32 bcache[(PI_NL / 64) * BI_CACHE_WORDS];  // one bit-reader cache per wave
@@ -78,39 +101,40 @@ struct ParLds {
     u32 sidx[PI_NL];                 // first valid token of the lane
     u32 ntok[PI_NL];
     u32 base[PI_NL];                 // output offset of the lane's first valid token
+    unsigned long long anom[PI_NL / 64];
+    u32 seg_s[PI_MAXSEG], seg_e[PI_MAXSEG];  // chain segments [s, e] (lane ranges)
+    u32 pool_top;
     u32 wsum[8];
     u32 ctl[16];
 };
 
-// Decode one token from a bit buffer holding >= 48 valid bits.
+static_assert(sizeof(ParLds) <= 160 * 1024, "ParLds exceeds the 160 KiB LDS of a CU");
+
+// Decode one token from a bit buffer holding >= 48 valid bits: <= 2 LDS
+// lookups for the literal/length code, <= 2 for the distance code.
 __device__ __forceinline__ u32 decode_token(const ParLds& L, u64 v, u32* adv) {
-    u32 e = L.ltab[(u32)v & ((1u << INF_LBITS) - 1)];
-    u32 l = e >> 28;
-    if (l == 0) {
-        if (((e >> 24) & 15) == K_BAD) { *adv = 1; return T_BAD; }
-        e = slow_sym(v, &L.lh, false, &l);
-        if (l == 0) { *adv = 1; return T_BAD; }
-    }
+    const u32 e = table_lookup(L.ltab, INF_LBITS, (u32)v);
+    const u32 l = e >> 28;
     const u32 kind = (e >> 24) & 15;
     if (kind == K_LIT) { *adv = l; return e & 0xFF; }
     if (kind == K_EOB) { *adv = l; return T_EOB; }
-    if (kind != K_LEN) { *adv = l; return T_BAD; }
+    if (kind != K_LEN) { *adv = l ? l : 1; return T_BAD; }
     const u32 ex = (e >> 16) & 0xFF;
     const u32 len = (e & 0xFFFF) + ((u32)(v >> l) & ((1u << ex) - 1));
     const u32 t = l + ex;
     const u64 vd = v >> t;
-    u32 de = L.dtab[(u32)vd & ((1u << INF_DBITS) - 1)];
-    u32 dl = de >> 28;
-    if (dl == 0) {
-        if (((de >> 24) & 15) == K_BAD) { *adv = t + 1; return T_BAD; }
-        de = slow_sym(vd, &L.dh, true, &dl);
-        if (dl == 0) { *adv = t + 1; return T_BAD; }
-    }
-    if (((de >> 24) & 15) != K_DIST) { *adv = t + dl; return T_BAD; }
+    const u32 de = table_lookup(L.dtab, INF_DBITS, (u32)vd);
+    const u32 dl = de >> 28;
+    if (((de >> 24) & 15) != K_DIST) { *adv = t + (dl ? dl : 1); return T_BAD; }
     const u32 dex = (de >> 16) & 0xFF;
     const u32 dist = (de & 0xFFFF) + ((u32)(vd >> dl) & ((1u << dex) - 1));
     *adv = t + dl + dex;
     return T_MATCH | ((len - 3) << 16) | (dist - 1);
+}
+
+// Token j of lane i in the pool.
+__device__ __forceinline__ u32& tok_ref(ParLds& L, u32 i, u32 j) {
+    return L.pool[((u32)L.blk[i * PI_LBLK + (j / PI_BLK)] * PI_BLK) + (j % PI_BLK)];
 }
 
 // Register bit buffer over the staged words: a 96-bit window (lo:hi) holding
@@ -230,6 +254,7 @@ __global__ __launch_bounds__(PI_NL) void inflate_par_kernel(const zcg_chunk* __r
     const u32 c = blockIdx.x;
     if (c >= n) return;
     const u32 tid = threadIdx.x;
+    const bool dbg = (vflags & ZCG_FLAG_DEBUG_COUNTERS) != 0;
     const zcg_chunk ch = chunks[c];
     if (D == 0) { if (tid == 0) status[c] = ZCG_OK; return; }
     if (ch.dst_cap < D) { if (tid == 0) status[c] = ZCG_ERR_INVALID_INPUT; return; }
@@ -251,14 +276,19 @@ __global__ __launch_bounds__(PI_NL) void inflate_par_kernel(const zcg_chunk* __r
     u64 P = 0;
     bool last = false, boundary = false, after_stored = false;
     int r = R_OK;
+    u64 t_last = __builtin_readcyclecounter();
+    const u64 t_start = t_last;
 
     while (r == R_OK && P < D) {
+        TSTAMP(TP_COMMIT);
         // ---- block header (all waves, identical) ------------------------------------
         if (last) { r = R_EXHAUSTED; break; }
         u32 type = 0, slen = 0;
         r = read_block_header(b, &last, &type, &slen, L.lens, &L.lh, L.ltab, &L.dh, L.dtab);
         const u32 hdr_end = (u32)b.consumed;
+        TSTAMP(TP_HDR);
         if (r != R_OK) break;
+        if (dbg && tid == 0) atomicAdd(&g_inf_dbg[DBG_BLOCKS], 1ull);
         if (type == 0) {
             // ---- stored block: byte copies through the stage --------------------
             u64 in0 = hdr_end >> 3;  // byte aligned after LEN/NLEN
@@ -283,36 +313,66 @@ __global__ __launch_bounds__(PI_NL) void inflate_par_kernel(const zcg_chunk* __r
         u32 R0 = hdr_end;
         bool block_end = false;
         while (!block_end && r == R_OK && P < D) {
-            const u32 bit0 = R0 & ~31u;
+            const u32 bit0 = R0 & ~127u;  // 16-byte aligned stream offset
             const u64 byte0 = bit0 >> 3;
-            for (u32 w = tid; w < PI_IN_WORDS; w += PI_NL) {
-                const u64 q = byte0 + 4ull * w;
-                u32 v = 0;
-                if (q + 4 <= n_ds) v = ld32(ds + q);
-                else
-                    for (u32 i = 0; i < 4; i++)
-                        if (q + i < n_ds) v |= (u32)ds[q + i] << (8 * i);
-                L.in[w] = v;
+            {
+                u32x4 v[(PI_IN_VEC + PI_NL - 1) / PI_NL];
+#pragma unroll
+                for (u32 k = 0; k < (PI_IN_VEC + PI_NL - 1) / PI_NL; k++) {
+                    const u32 vi = tid + k * PI_NL;
+                    const u64 q = byte0 + 16ull * vi;
+                    u32x4 x = {0u, 0u, 0u, 0u};
+                    if (vi < PI_IN_VEC) {
+                        if (q + 16 <= n_ds) x = ld16(ds + q);
+                        else {
+                            u32 w4[4] = {0u, 0u, 0u, 0u};
+                            for (u32 i = 0; i < 16; i++)
+                                if (q + i < n_ds) w4[i >> 2] |= (u32)ds[q + i] << (8 * (i & 3));
+                            x = u32x4{w4[0], w4[1], w4[2], w4[3]};
+                        }
+                    }
+                    v[k] = x;
+                }
+#pragma unroll
+                for (u32 k = 0; k < (PI_IN_VEC + PI_NL - 1) / PI_NL; k++) {
+                    const u32 vi = tid + k * PI_NL;
+                    if (vi < PI_IN_VEC) *(u32x4*)(L.in + 4 * vi) = v[k];
+                }
             }
             for (u32 w = tid; w < PI_NL * PI_SEGW; w += PI_NL) L.mark[w] = 0;
+            if (tid == 0) L.pool_top = 0;
             __syncthreads();
+            TSTAMP(TP_STAGE);
 
             // ---- pass 1: decode my own segment, mark token starts ----------------
             const u32 p = R0 + tid * PI_SEG;
             const u32 pend = p + PI_SEG;
-            u32* mytok = L.tok + tid * PI_TMAX;
             u32* mymark = L.mark + tid * PI_SEGW;
+            u16* myblk = L.blk + tid * PI_LBLK;
             LaneBits bs;
             lb_init(bs, L.in, p, bit0);
             u32 q = p, nt = 0;
             u32 nxt = 0xFFFFFFFFu;
+            u32* cur = nullptr;  // current pool block of this lane
+            // append a token; false when the lane's token store is full
+            auto push = [&](u32 tk) -> bool {
+                if ((nt % PI_BLK) == 0) {
+                    if (nt == PI_TMAX) return false;
+                    const u32 bi = atomicAdd(&L.pool_top, 1u);
+                    if (bi >= PI_NBLK) return false;
+                    myblk[nt / PI_BLK] = (u16)bi;
+                    cur = L.pool + bi * PI_BLK;
+                }
+                cur[nt % PI_BLK] = tk;
+                nt++;
+                return true;
+            };
             while (q < pend) {
-                if (nt == PI_TMAX) { nxt = N_CAP; break; }
                 lb_fill(bs, L.in);
                 u32 adv;
                 u32 tk = decode_token(L, bs.lo, &adv);
                 if (q + adv > total_bits) tk = T_EXH;
-                mytok[nt++] = tk;
+                if (!push(tk)) { nxt = N_CAP; break; }
                 const u32 off = q - p;
                 mymark[off >> 5] |= 1u << (off & 31);
                 if (tok_is_marker(tk)) {
@@ -324,6 +384,7 @@ __global__ __launch_bounds__(PI_NL) void inflate_par_kernel(const zcg_chunk* __r
                 q += adv;
             }
             __syncthreads();
+            TSTAMP(TP_PASS1);
             // ---- pass 2: follow my path until it meets a marked token start -----
             const u32 round_hi = R0 + PI_NL * PI_SEG;
             u32 give = 0;
@@ -340,12 +401,12 @@ __global__ __launch_bounds__(PI_NL) void inflate_par_kernel(const zcg_chunk* __r
                     give = cnt;
                     break;
                 }
-                if (nt == PI_TMAX) { nxt = N_CAP; break; }
                 lb_fill(bs, L.in);
                 u32 adv;
                 u32 tk = decode_token(L, bs.lo, &adv);
                 if (q + adv > total_bits) tk = T_EXH;
-                mytok[nt++] = tk;
+                if (!push(tk)) { nxt = N_CAP; break; }
+                if (dbg) atomicAdd(&g_inf_dbg[DBG_PASS2_TOK], 1ull);
                 if (tok_is_marker(tk)) {
                     if (tk == T_EOB) q += adv;
                     nxt = N_MARKER;
@@ -359,40 +420,73 @@ __global__ __launch_bounds__(PI_NL) void inflate_par_kernel(const zcg_chunk* __r
             L.give[tid] = give;
             L.ntok[tid] = nt;
             __syncthreads();
+            TSTAMP(TP_PASS2);
 
             // ---- chain: lane 0 is true; follow sync targets --------------------------
-            // Common case next[i] == i+1; one thread walks the exceptions.
+            // Common case next[i] == i+1; one thread walks only the exceptions.
+            {
+                const bool an = nxt != tid + 1;
+                const unsigned long long bm = __ballot(an);
+                if ((tid & 63) == 0) L.anom[tid >> 6] = bm;
+            }
+            __syncthreads();
             if (tid == 0) {
-                u32 cur = 0, endl = 0;
-                L.sidx[0] = 0;
+                u32 curl = 0, ns = 0, endl = 0;
                 for (;;) {
-                    u32 a = cur;
-                    while (a + 1 < PI_NL && L.next[a] == a + 1) { L.sidx[a + 1] = L.give[a]; a++; }
-                    // lane a: stop code or a skip
-                    const u32 nx = L.next[a];
-                    if (nx < PI_NL) {  // skip to a later lane
-                        L.sidx[nx] = L.give[a];
-                        for (u32 d2 = a + 1; d2 < nx; d2++) L.sidx[d2] = 0xFFFFFFFFu;  // dead
-                        cur = nx;
-                        continue;
+                    // first anomaly >= curl
+                    u32 a = PI_NL - 1;
+                    for (u32 w = curl >> 6; w < PI_NL / 64; w++) {
+                        unsigned long long m = L.anom[w];
+                        if (w == (curl >> 6)) m &= ~0ull << (curl & 63);
+                        if (m) { a = w * 64 + __builtin_ctzll(m); break; }
                     }
+                    L.seg_s[ns] = curl;
+                    L.seg_e[ns] = a;
+                    ns++;
+                    const u32 nx = L.next[a];
+                    if (nx < PI_NL && ns < PI_MAXSEG) { curl = nx; continue; }
                     endl = a;
                     break;
                 }
-                for (u32 d2 = endl + 1; d2 < PI_NL; d2++) L.sidx[d2] = 0xFFFFFFFFu;
                 L.ctl[5] = endl;
+                L.ctl[12] = ns;
+            }
+            __syncthreads();
+            {
+                const u32 ns = L.ctl[12];
+                u32 sx = 0xFFFFFFFFu;
+                for (u32 k = 0; k < ns; k++) {
+                    const u32 s0 = L.seg_s[k], e0 = L.seg_e[k];
+                    if (tid >= s0 && tid <= e0) {
+                        if (tid == 0) sx = 0;
+                        else if (tid == s0) sx = L.give[L.seg_e[k - 1]];  // jump target
+                        else sx = L.give[tid - 1];
+                    }
+                }
+                L.sidx[tid] = sx;
             }
             __syncthreads();
             const u32 E = L.ctl[5];
+            TSTAMP(TP_CHAIN);
+            if (dbg && tid == 0) {
+                atomicAdd(&g_inf_dbg[DBG_ROUNDS], 1ull);
+                atomicAdd(&g_inf_dbg[DBG_CHAIN], (unsigned long long)(E + 1));
+                const u32 nx = L.next[E];
+                atomicAdd(&g_inf_dbg[nx == N_CAP ? DBG_END_CAP : nx == N_ROUND_END ? DBG_END_ROUND
+                                    : (tok_ref(L, E, L.ntok[E] - 1) == T_EOB ? DBG_END_EOB : DBG_END_BAD)], 1ull);
+                u32 sk = 0;
+                for (u32 x = 0; x < E; x++) sk += L.next[x] != x + 1;
+                atomicAdd(&g_inf_dbg[DBG_SKIPS], (unsigned long long)sk);
+            }
             const u32 my_s = L.sidx[tid];
             const bool on = (tid <= E) && my_s != 0xFFFFFFFFu;
             u32 vend = nt;
             u32 marker = 0;
-            if (on && tid == E && nxt == N_MARKER) { vend = nt - 1; marker = mytok[nt - 1]; }
+            if (on && tid == E && nxt == N_MARKER) { vend = nt - 1; marker = tok_ref(L, tid, nt - 1); }
             // ---- placement ------------------------------------------------------------------
             u32 olen = 0;
             if (on)
-                for (u32 a = my_s; a < vend; a++) olen += tok_len(mytok[a]);
+                for (u32 a = my_s; a < vend; a++) olen += tok_len(tok_ref(L, tid, a));
             u32 total;
             const u32 base = block_excl_scan(L, olen, &total);
             const u64 room = D - P;
@@ -406,15 +500,16 @@ __global__ __launch_bounds__(PI_NL) void inflate_par_kernel(const zcg_chunk* __r
             bool final_round = false, fin_boundary = false;
             const bool cut = total > cap || (total == cap && cap == room);
             if (cut) {
+                if (dbg && tid == 0) atomicAdd(&g_inf_dbg[DBG_CUTS], 1ull);
                 // the lane whose output range holds byte `cap`
                 const bool mine = on && olen > 0 && base < cap && base + olen >= cap;
                 if (mine) {
                     u32 acc = base, a = my_s;
                     if (cap == room) {
-                        while (a < vend && acc < cap) { acc += tok_len(mytok[a]); a++; }
+                        while (a < vend && acc < cap) { acc += tok_len(tok_ref(L, tid, a)); a++; }
                         L.ctl[7] = (acc == cap) ? 1u : 0u;
                     } else {
-                        while (a < vend && acc + tok_len(mytok[a]) <= cap) { acc += tok_len(mytok[a]); a++; }
+                        while (a < vend && acc + tok_len(tok_ref(L, tid, a)) <= cap) { acc += tok_len(tok_ref(L, tid, a)); a++; }
                         L.ctl[7] = 0;
                     }
                     L.ctl[8] = acc;
@@ -443,12 +538,13 @@ __global__ __launch_bounds__(PI_NL) void inflate_par_kernel(const zcg_chunk* __r
             {
                 u32 o = base;
                 for (u32 a = my_s; a < take_end; a++) {
-                    const u32 tk = mytok[a];
+                    const u32 tk = tok_ref(L, tid, a);
                     if ((tk & T_MATCH) && tok_dist(tk) > P + o) far = true;
                     o += tok_len(tk);
                 }
             }
             if (__syncthreads_or(far)) { r = R_INVALID; break; }
+            TSTAMP(TP_PLACE);
             // ---- literals ------------------------------------------------------------------------
             const u64 S = P;
             for (u32 w = tid; w < PI_STAGE / 32; w += PI_NL) L.resolved[w] = 0;
@@ -456,7 +552,7 @@ __global__ __launch_bounds__(PI_NL) void inflate_par_kernel(const zcg_chunk* __r
             {
                 u32 o = base;
                 for (u32 a = my_s; a < take_end; a++) {
-                    const u32 tk = mytok[a];
+                    const u32 tk = tok_ref(L, tid, a);
                     if (!(tk & T_MATCH)) {
                         L.stage[(S + o) & (PI_STAGE - 1)] = (u8)tk;
                         atomicOr(&L.resolved[o >> 5], 1u << (o & 31));
@@ -465,12 +561,13 @@ __global__ __launch_bounds__(PI_NL) void inflate_par_kernel(const zcg_chunk* __r
                 }
             }
             __syncthreads();
+            TSTAMP(TP_LIT);
             // ---- matches: multi-round resolution -----------------------------------------------
             {
                 u32 a = my_s, o = base;
                 for (;;) {
                     while (a < take_end) {
-                        const u32 tk = mytok[a];
+                        const u32 tk = tok_ref(L, tid, a);
                         if (!(tk & T_MATCH)) { a++; o++; continue; }
                         const u32 len0 = tok_len(tk), d = tok_dist(tk);
                         const u32 len = (o + len0 > emitted) ? emitted - o : len0;  // cut at N
@@ -510,12 +607,18 @@ __global__ __launch_bounds__(PI_NL) void inflate_par_kernel(const zcg_chunk* __r
                         a++;
                         o += len0;
                     }
+                    if (dbg && tid == 0) atomicAdd(&g_inf_dbg[DBG_MRR_IT], 1ull);
                     if (!__syncthreads_or(a < take_end)) break;
                 }
             }
+            TSTAMP(TP_MRR);
             // ---- commit -------------------------------------------------------------------------------
             par_commit(L, dst, S, S + emitted, t);
             P = S + emitted;
+            if (dbg) {
+                if (tid == 0) atomicAdd(&g_inf_dbg[DBG_BYTES], (unsigned long long)emitted);
+                if (take_end > my_s) atomicAdd(&g_inf_dbg[DBG_TOKENS], (unsigned long long)(take_end - my_s));
+            }
             if (final_round) {
                 boundary = fin_boundary;
                 bi_seek(b, round_end);
@@ -541,7 +644,18 @@ __global__ __launch_bounds__(PI_NL) void inflate_par_kernel(const zcg_chunk* __r
     }
     if (r == R_INVALID) st = ZCG_ERR_INVALID_DATA;
     else if (r == R_EXHAUSTED || P < D) st = ZCG_ERR_UNEXPECTED_EOF;
+    if (dbg && tid == 0) atomicAdd(&g_inf_dbg[TP_TOTAL], (unsigned long long)(__builtin_readcyclecounter() - t_start));
     if (tid == 0) status[c] = st;
+}
+
+extern "C" int zcg__debug_inflate_counters(unsigned long long* out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_inf_dbg), sizeof(unsigned long long) * 32) != hipSuccess)
+        return -1;
+    if (reset) {
+        unsigned long long z[32] = {0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_inf_dbg), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return 0;
 }
 
 hipError_t launch_inflate_par(const zcg_array* a, const zcg_chunk* d_chunks, uint32_t n,
