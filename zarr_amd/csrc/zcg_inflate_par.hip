@@ -42,7 +42,7 @@ constexpr u32 PI_BLK = 16;       // tokens per pool block
 constexpr u32 PI_LBLK = 5;       // pool blocks per lane -> up to 80 tokens per lane
 constexpr u32 PI_TMAX = PI_BLK * PI_LBLK;
 constexpr u32 PI_NBLK = 640;     // pool blocks per round (avg need ~1.7 per lane)
-constexpr u32 PI_STAGE = 32768;  // output bytes per round (power of 2)
+constexpr u32 PI_STAGE = 16384;  // output bytes per round (power of 2)
 constexpr u32 PI_WIN = 32768;    // LZ77 window ring
 constexpr u32 PI_SEGW = PI_SEG / 32;
 constexpr u32 PI_IN_VEC = (PI_NL * PI_SEG + 1024) / 128 + 2;  // staged 16-B vectors
@@ -84,12 +84,11 @@ __device__ __forceinline__ u32 tok_dist(u32 t) { return (t & 0x7FFF) + 1; }
 
 struct ParLds {
     u8 win[PI_WIN];                  // LZ77 window ring (absolute pos & 32767)
-    u8 stage[PI_STAGE];              // round output (absolute pos & 32767)
+    u16 ptr[PI_STAGE];               // round bytes: 0x8000|value, or an earlier round offset
     u32 in[PI_IN_WORDS];             // staged stream words
     u32 pool[PI_NBLK * PI_BLK];      // token pool: lanes take 16-token blocks
     u16 blk[PI_NL * PI_LBLK];        // each lane's pool blocks
     u32 mark[PI_NL * PI_SEGW];       // token-start bitmap of each lane's own segment
-    u32 resolved[PI_STAGE / 32];     // MRR bitmap over round offsets
     u32 ltab[INF_LTAB];
     u32 dtab[INF_DTAB];
     HuffLds lh, dh;
@@ -177,31 +176,35 @@ __device__ __forceinline__ void lb_drop(LaneBits& s, u32 k) {  // 0 < k <= 48
     s.nb -= k;
 }
 
-__device__ __forceinline__ u8 out_byte(const ParLds& L, u64 q, u64 S) {
-    return q < S ? L.win[q & (PI_WIN - 1)] : L.stage[q & (PI_STAGE - 1)];
-}
-
-// Flush [from, to) of the stage to dst (transform fused); append to window.
+// Flush the resolved round bytes [from, to) to dst (transform fused) and
+// append them to the window ring.  ptr[] is indexed by absolute pos & mask.
 __device__ void par_commit(ParLds& L, u8* dst, u64 from, u64 to, const DType& t) {
     const u32 tid = threadIdx.x;
     __syncthreads();
     const u64 a16 = (from + 15) & ~15ull, b16 = to & ~15ull;
     if (a16 < b16) {
         for (u64 p = a16 + (u64)tid * 16; p < b16; p += PI_NL * 16) {
-            const u32x4 v = *(const u32x4*)(L.stage + (p & (PI_STAGE - 1)));
+            const u32 i = (u32)(p & (PI_STAGE - 1));
+            const u32x4 lo = *(const u32x4*)(L.ptr + i);
+            const u32x4 hi = *(const u32x4*)(L.ptr + i + 8);
+            // each u32 holds two 16-bit entries; keep their low bytes
+            auto pk = [](u32 a, u32 b) -> u32 {
+                return __builtin_amdgcn_perm(b, a, 0x06040200u);
+            };
+            const u32x4 v = u32x4{pk(lo.x, lo.y), pk(lo.z, lo.w), pk(hi.x, hi.y), pk(hi.z, hi.w)};
             st16(dst + p, transform16(v, t));
             *(u32x4*)(L.win + (p & (PI_WIN - 1))) = v;
         }
     }
     const u64 e0 = a16 < b16 ? a16 : to;
     for (u64 q = from + tid; q < e0; q += PI_NL) {
-        const u8 v = L.stage[q & (PI_STAGE - 1)];
+        const u8 v = (u8)L.ptr[q & (PI_STAGE - 1)];
         dst[swap_pos(q, t)] = norm_byte(v, t);
         L.win[q & (PI_WIN - 1)] = v;
     }
     if (a16 < b16)
         for (u64 q = b16 + tid; q < to; q += PI_NL) {
-            const u8 v = L.stage[q & (PI_STAGE - 1)];
+            const u8 v = (u8)L.ptr[q & (PI_STAGE - 1)];
             dst[swap_pos(q, t)] = norm_byte(v, t);
             L.win[q & (PI_WIN - 1)] = v;
         }
@@ -298,7 +301,8 @@ __global__ __launch_bounds__(PI_NL) void inflate_par_kernel(const zcg_chunk* __r
                 if (k > PI_STAGE) k = PI_STAGE;
                 if ((u64)k > D - P) k = (u32)(D - P);
                 if (in0 + k > n_ds) { r = R_EXHAUSTED; break; }
-                for (u32 i = tid; i < k; i += PI_NL) L.stage[(P + i) & (PI_STAGE - 1)] = ds[in0 + i];
+                for (u32 i = tid; i < k; i += PI_NL)
+                    L.ptr[(P + i) & (PI_STAGE - 1)] = (u16)(0x8000u | ds[in0 + i]);
                 par_commit(L, dst, P, P + k, t);
                 P += k; in0 += k; done += k;
             }
@@ -339,7 +343,6 @@ __global__ __launch_bounds__(PI_NL) void inflate_par_kernel(const zcg_chunk* __r
                     if (vi < PI_IN_VEC) *(u32x4*)(L.in + 4 * vi) = v[k];
                 }
             }
-            for (u32 w = tid; w < PI_NL * PI_SEGW; w += PI_NL) L.mark[w] = 0;
             if (tid == 0) L.pool_top = 0;
             __syncthreads();
             TSTAMP(TP_STAGE);
@@ -347,7 +350,9 @@ __global__ __launch_bounds__(PI_NL) void inflate_par_kernel(const zcg_chunk* __r
             // ---- pass 1: decode my own segment, mark token starts ----------------
             const u32 p = R0 + tid * PI_SEG;
             const u32 pend = p + PI_SEG;
-            u32* mymark = L.mark + tid * PI_SEGW;
+            u32 mkw[PI_SEGW];
+#pragma unroll
+            for (u32 w = 0; w < PI_SEGW; w++) mkw[w] = 0;
             u16* myblk = L.blk + tid * PI_LBLK;
             LaneBits bs;
             lb_init(bs, L.in, p, bit0);
@@ -374,7 +379,8 @@ __global__ __launch_bounds__(PI_NL) void inflate_par_kernel(const zcg_chunk* __r
                 if (q + adv > total_bits) tk = T_EXH;
                 if (!push(tk)) { nxt = N_CAP; break; }
                 const u32 off = q - p;
-                mymark[off >> 5] |= 1u << (off & 31);
+#pragma unroll
+                for (u32 w = 0; w < PI_SEGW; w++) mkw[w] |= ((off >> 5) == w) ? (1u << (off & 31)) : 0u;
                 if (tok_is_marker(tk)) {
                     if (tk == T_EOB) q += adv;
                     nxt = N_MARKER;
@@ -383,6 +389,8 @@ __global__ __launch_bounds__(PI_NL) void inflate_par_kernel(const zcg_chunk* __r
                 lb_drop(bs, adv);
                 q += adv;
             }
+#pragma unroll
+            for (u32 w = 0; w < PI_SEGW; w++) L.mark[tid * PI_SEGW + w] = mkw[w];
             __syncthreads();
             TSTAMP(TP_PASS1);
             // ---- pass 2: follow my path until it meets a marked token start -----
@@ -545,71 +553,49 @@ __global__ __launch_bounds__(PI_NL) void inflate_par_kernel(const zcg_chunk* __r
             }
             if (__syncthreads_or(far)) { r = R_INVALID; break; }
             TSTAMP(TP_PLACE);
-            // ---- literals ------------------------------------------------------------------------
+            // ---- LZ77 resolution by pointer jumping ---------------------------------------
+            // Every round byte gets its value (literal, or a byte of the final
+            // window) or a pointer to an EARLIER round byte: a match byte k
+            // copies B[o - d + (k mod d)], which lies before the match start.
             const u64 S = P;
-            for (u32 w = tid; w < PI_STAGE / 32; w += PI_NL) L.resolved[w] = 0;
-            __syncthreads();
             {
                 u32 o = base;
                 for (u32 a = my_s; a < take_end; a++) {
                     const u32 tk = tok_ref(L, tid, a);
                     if (!(tk & T_MATCH)) {
-                        L.stage[(S + o) & (PI_STAGE - 1)] = (u8)tk;
-                        atomicOr(&L.resolved[o >> 5], 1u << (o & 31));
+                        L.ptr[(S + o) & (PI_STAGE - 1)] = (u16)(0x8000u | (tk & 0xFF));
+                        o++;
+                        continue;
                     }
-                    o += tok_len(tk);
+                    const u32 len0 = tok_len(tk), d = tok_dist(tk);
+                    const u32 len = (o + len0 > emitted) ? emitted - o : len0;  // cut at N
+                    u32 j = 0;  // k mod d
+                    for (u32 k = 0; k < len; k++) {
+                        const int sp = (int)o - (int)d + (int)j;
+                        u16 v;
+                        if (sp < 0) v = (u16)(0x8000u | L.win[(S + (int64_t)sp) & (PI_WIN - 1)]);
+                        else v = (u16)sp;
+                        L.ptr[(S + o + k) & (PI_STAGE - 1)] = v;
+                        j = (j + 1 == d) ? 0 : j + 1;
+                    }
+                    o += len0;
                 }
             }
             __syncthreads();
             TSTAMP(TP_LIT);
-            // ---- matches: multi-round resolution -----------------------------------------------
-            {
-                u32 a = my_s, o = base;
-                for (;;) {
-                    while (a < take_end) {
-                        const u32 tk = tok_ref(L, tid, a);
-                        if (!(tk & T_MATCH)) { a++; o++; continue; }
-                        const u32 len0 = tok_len(tk), d = tok_dist(tk);
-                        const u32 len = (o + len0 > emitted) ? emitted - o : len0;  // cut at N
-                        const int64_t src = (int64_t)o - d;  // round-relative
-                        const u32 span = d < len0 ? d : len0;
-                        bool ready = true;
-                        if (src + (int64_t)span > 0) {
-                            const u32 lo = src < 0 ? 0u : (u32)src;
-                            const u32 hi = (u32)(src + span);
-                            for (u32 x = lo; x < hi && ready;) {
-                                const u32 wv = L.resolved[x >> 5];
-                                const u32 nb = (hi - x) < (32 - (x & 31)) ? (hi - x) : (32 - (x & 31));
-                                const u32 m = (nb == 32) ? 0xFFFFFFFFu : (((1u << nb) - 1) << (x & 31));
-                                if ((wv & m) != m) ready = false;
-                                x += nb;
-                            }
-                        }
-                        if (!ready) break;
-                        u32 ph = 0;
-                        for (u32 k = 0; k < len; k += 8) {
-                            u8 v[8];
-#pragma unroll
-                            for (int z = 0; z < 8; z++) {
-                                v[z] = out_byte(L, (u64)((int64_t)S + src + ph), S);
-                                ph = (ph + 1 == d) ? 0 : ph + 1;
-                            }
-#pragma unroll
-                            for (int z = 0; z < 8; z++)
-                                if (k + z < len) L.stage[(S + o + k + z) & (PI_STAGE - 1)] = v[z];
-                        }
-                        for (u32 x = o; x < o + len;) {
-                            const u32 nb = (o + len - x) < (32 - (x & 31)) ? (o + len - x) : (32 - (x & 31));
-                            const u32 m = (nb == 32) ? 0xFFFFFFFFu : (((1u << nb) - 1) << (x & 31));
-                            atomicOr(&L.resolved[x >> 5], m);
-                            x += nb;
-                        }
-                        a++;
-                        o += len0;
+            for (;;) {
+                bool pending = false;
+                for (u32 x = tid; x < emitted; x += PI_NL) {
+                    const u32 i = (u32)((S + x) & (PI_STAGE - 1));
+                    const u16 v = L.ptr[i];
+                    if (!(v & 0x8000u)) {
+                        const u16 w = L.ptr[(u32)((S + v) & (PI_STAGE - 1))];
+                        L.ptr[i] = w;
+                        pending |= !(w & 0x8000u);
                     }
-                    if (dbg && tid == 0) atomicAdd(&g_inf_dbg[DBG_MRR_IT], 1ull);
-                    if (!__syncthreads_or(a < take_end)) break;
                 }
+                if (dbg && tid == 0) atomicAdd(&g_inf_dbg[DBG_MRR_IT], 1ull);
+                if (!__syncthreads_or(pending)) break;
             }
             TSTAMP(TP_MRR);
             // ---- commit -------------------------------------------------------------------------------
