@@ -370,3 +370,28 @@ def test_inflate_parallel_vs_serial_kernel(data):
             b = DefaultChunk.read_chunk(s, meta, [0], np.uint8, flags=FLAG_SERIAL_INFLATE).get_data()
             assert np.array_equal(a, b)
             assert a.tobytes() == payload[:D]
+
+
+@pytest.mark.parametrize("codec", ["gzip", "lz4", "raw"])
+def test_decode_never_writes_past_n(codec):
+    """read_exact stops at byte N even inside a long match: the bytes after
+    N*elem_size in the caller's buffer stay untouched (chunk.rs:112-113)."""
+    import torch
+    from zarr_amd._native import FLAG_SERIAL_INFLATE
+    from zarr_amd.batch import BatchCodec, PackedStreams
+    payloads = [bytes(300000), (b"abcdefgh" * 40000), rw(150000).tobytes()]
+    streams = [zref.encode(CODEC_IDS[codec], DEFAULT_PARAM[codec], np.frombuffer(p, np.uint8))[1]
+               for p in payloads]
+    guard = 4096
+    for D in (1, 777, 16385, 65537, 99999, 200003):
+        flag_sets = (0, FLAG_SERIAL_INFLATE) if codec == "gzip" else (0,)
+        for flags in flag_sets:
+            dst = torch.full((len(streams) * (D + guard),), 0xAB, dtype=torch.uint8, device="cuda:0")
+            packed = PackedStreams(streams, D + guard, "cuda:0", dst=dst)
+            BatchCodec(0).decode(meta_for(codec, "u1", D), packed, flags=flags)
+            torch.cuda.synchronize()
+            assert (packed.status.cpu().numpy() == 0).all()
+            out = dst.cpu().numpy().reshape(len(streams), D + guard)
+            for i, p in enumerate(payloads):
+                assert out[i, :D].tobytes() == p[:D], (D, i)
+                assert (out[i, D:] == 0xAB).all(), (D, i, flags)

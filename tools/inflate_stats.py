@@ -27,7 +27,7 @@ torch.cuda.synchronize()
 t1 = time.time()
 fn(out.ctypes.data, 1)
 names = ["rounds", "chain_lanes", "end_cap", "end_eob", "end_bad", "skips", "mrr_iters", "cuts",
-         "blocks", "bytes", "tokens", "end_round", "pass2_tokens", "_13", "_14", "_15",
+         "blocks", "bytes", "tokens", "end_round", "pass2_tokens", "cap_p1", "cap_p2", "p2_max",
          "cyc_hdr", "cyc_stage", "cyc_pass1", "cyc_pass2", "cyc_chain", "cyc_place", "cyc_lit",
          "cyc_mrr", "cyc_commit", "cyc_total"]
 d = {k: int(v) for k, v in zip(names, out)}
@@ -37,7 +37,11 @@ d["cycles_per_round"] = {k: round(d[k] / max(1, d["rounds"])) for k in names if 
 d["avg_chain"] = round(d["chain_lanes"] / max(1, d["rounds"]), 2)
 d["mrr_per_round"] = round(d["mrr_iters"] / max(1, d["rounds"]), 2)
 d["bytes_per_round"] = round(d["bytes"] / max(1, d["rounds"]), 1)
-t2 = time.time(); codec.decode(meta, packed); torch.cuda.synchronize(); t3 = time.time()
+best = 1e9
+for _ in range(3):
+    t2 = time.time(); codec.decode(meta, packed); torch.cuda.synchronize(); t3 = time.time()
+    best = min(best, t3 - t2)
+t2, t3 = 0.0, best
 d["ms_debug"] = round((t1 - t0) * 1e3, 2)
 d["ms_nodebug"] = round((t3 - t2) * 1e3, 2)
 d["status_ok"] = bool((packed.status.cpu().numpy() == 0).all())

@@ -40,9 +40,8 @@ __device__ __forceinline__ u32 mk_entry(u32 len, u32 kind, u32 extra, u32 val) {
 // Canonical Huffman code description in LDS (built per block).
 struct HuffLds {
     u32 count[16];
-    u32 first[16];  // first canonical code of each length
-    u32 offs[16];   // index of the first symbol of each length in sym[]
-    u16 sym[288];
+    u32 first[16];     // first canonical code of each length
+    u32 cpre[5 * 16];  // per 64-symbol chunk: codes of each length in earlier chunks
 };
 
 // Entry for symbol `s` of table type `dist`.
@@ -58,31 +57,58 @@ __device__ __forceinline__ u32 sym_entry(u32 s, u32 len, bool dist) {
 }
 
 __device__ __forceinline__ u32 bitrev(u32 v, int n) { return __builtin_bitreverse32(v) >> (32 - n); }
-
-// Canonical decode of stream bits `bits` (LSB = first bit) over at most
-// `maxbits` bits; returns the table entry (K_BAD, length 1, if no code).
-__device__ __forceinline__ u32 canon_decode(const HuffLds* h, u32 bits, int maxbits, bool dist) {
-    u32 code = 0;
-    for (int l = 1; l <= maxbits; l++) {
-        code = (code << 1) | ((bits >> (l - 1)) & 1);
-        const u32 cnt = h->count[l];
-        if (code - h->first[l] < cnt) return sym_entry(h->sym[h->offs[l] + (code - h->first[l])], l, dist);
-    }
-    return mk_entry(1, K_BAD, 0, 0);
+// popcount of the mask bits below this lane
+__device__ __forceinline__ u32 mbcnt64(unsigned long long m) {
+    return __builtin_amdgcn_mbcnt_hi((u32)(m >> 32), __builtin_amdgcn_mbcnt_lo((u32)m, 0u));
 }
 
 // Build the canonical code and the two-level table from lens[0..nsym)
-// (block-cooperative: every thread of the workgroup calls this uniformly).
+// (nsym <= 320; block-cooperative: every thread of the workgroup calls this
+// uniformly).  Symbol-driven, like zlib's inflate_table: a symbol's rank among
+// the codes of its length comes from wave ballots, a short code fills its
+// 2^(root-L) root slots, each long-code prefix gets a subtable sized by its
+// longest code (atomicMax) and placed by a block scan.  `cap` = table entries.
 // Returns 0 ok, -1 over-subscribed or incomplete (zlib inflate_table rules:
 // an incomplete code is only allowed when it is a single length-1 code).
-__device__ int build_table(const u8* lens, u32 nsym, HuffLds* h, u32* table, int root, bool dist) {
+__device__ int build_table(const u8* lens, u32 nsym, HuffLds* h, u32* table, int root, bool dist,
+                           u32 cap) {
     const u32 tid = threadIdx.x, nth = blockDim.x;
+    const u32 lane = tid & 63, wv = tid >> 6, nwv = nth >> 6;
+    const u32 nchunk = (nsym + 63) >> 6;
+    const u32 nroot = 1u << root;
     __shared__ u32 s_part[256 / 64 + 1];
     __syncthreads();
-    if (tid < 16) h->count[tid] = 0;
+    // 1. per-chunk counts of each code length; rank of my symbol in its chunk
+    constexpr u32 MAXC = 5;
+    u32 myL[MAXC], myR[MAXC];
+#pragma unroll
+    for (u32 i = 0; i < MAXC; i++) {
+        const u32 c = wv + i * nwv;
+        myL[i] = 0;
+        myR[i] = 0;
+        if (c < nchunk) {
+            const u32 s = c * 64 + lane;
+            const u32 L = s < nsym ? lens[s] : 0;
+            myL[i] = L;
+            for (u32 l = 1; l < 16; l++) {
+                const unsigned long long m = __ballot(L == l);
+                if (L == l) myR[i] = mbcnt64(m);
+                if (lane == 0) h->cpre[c * 16 + l] = (u32)__popcll(m);
+            }
+        }
+    }
+    for (u32 k = tid; k < nroot; k += nth) table[k] = 0;
     __syncthreads();
-    for (u32 s = tid; s < nsym; s += nth)
-        if (lens[s]) atomicAdd(&h->count[lens[s]], 1u);
+    if (tid < 16) {  // exclusive prefix over chunks, totals
+        u32 acc = 0;
+        if (tid > 0)
+            for (u32 c = 0; c < nchunk; c++) {
+                const u32 v = h->cpre[c * 16 + tid];
+                h->cpre[c * 16 + tid] = acc;
+                acc += v;
+            }
+        h->count[tid] = acc;
+    }
     __syncthreads();
     int ok = 1, maxlen = 0;
     {
@@ -96,77 +122,76 @@ __device__ int build_table(const u8* lens, u32 nsym, HuffLds* h, u32* table, int
         if (ok && left > 0 && maxlen > 1) ok = 0;
     }
     if (tid == 0) {
-        u32 o = 0, f = 0;
-        h->count[0] = 0;
+        u32 f = 0;
         for (int l = 1; l < 16; l++) {
             f = (f + h->count[l - 1]) << 1;
             h->first[l] = f;
-            h->offs[l] = o;
-            o += h->count[l];
         }
     }
     __syncthreads();
-    // canonical order: a symbol's rank among the symbols of its length
-    for (u32 s = tid; s < nsym; s += nth) {
-        const u32 L = lens[s];
-        if (!L) continue;
-        u32 rank = 0;
-        for (u32 x = 0; x < s; x++) rank += (lens[x] == L);
-        h->sym[h->offs[L] + rank] = (u16)s;
+    if (!ok) return -1;
+    u32 rev[MAXC];
+#pragma unroll
+    for (u32 i = 0; i < MAXC; i++) {
+        const u32 c = wv + i * nwv, L = myL[i];
+        rev[i] = 0;
+        if (L) rev[i] = bitrev(h->first[L] + h->cpre[c * 16 + L] + myR[i], (int)L);
     }
-    __syncthreads();
-    // root slots: direct entries, or the size of the subtable they head
-    const u32 nroot = 1u << root;
+    // 2. subtable size of each long-code prefix
+    if (maxlen > root) {
+#pragma unroll
+        for (u32 i = 0; i < MAXC; i++)
+            if (myL[i] > (u32)root) atomicMax(&table[rev[i] & (nroot - 1)], myL[i] - root);
+        __syncthreads();
+    }
+    // 3. root slots: subtable heads (placed by a block scan) or invalid
     const u32 per = (nroot + nth - 1) / nth;  // contiguous slots per thread
     u32 mysum = 0;
     for (u32 k = 0; k < per; k++) {
         const u32 slot = tid * per + k;
-        if (slot >= nroot) break;
-        u32 e = canon_decode(h, slot, root, dist);
-        if (((e >> 24) & 15) == K_BAD && maxlen > root) {
-            // prefix of longer codes: subtable of 2^(maxL - root) entries
-            const u32 pv = bitrev(slot, root);
-            int mx = 0;
-            for (int L = root + 1; L <= maxlen; L++) {
-                const u32 lo = pv << (L - root), hi = (pv + 1) << (L - root);
-                const u32 f = h->first[L], fe = f + h->count[L];
-                if (h->count[L] && lo < fe && f < hi) mx = L;
-            }
-            if (mx) {
-                e = mk_entry(0, 0xF, 0, (u32)(mx - root));  // temporary: subtable size marker
-                mysum += 1u << (mx - root);
-            }
-        }
-        table[slot] = e;
+        if (slot < nroot && table[slot]) mysum += 1u << table[slot];
     }
-    // exclusive scan of the per-thread subtable sizes
     u32 x = mysum;
-    const int lane = lane_id();
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
         const u32 y = __shfl_up(x, d, 64);
-        if (lane >= d) x += y;
+        if ((int)lane >= d) x += y;
     }
-    if (lane == 63) s_part[tid >> 6] = x;
+    if (lane == 63) s_part[wv] = x;
     __syncthreads();
-    u32 off = nroot;
-    for (u32 w = 0; w < (tid >> 6); w++) off += s_part[w];
+    u32 off = nroot, tot = 0;
+    for (u32 w = 0; w < nwv; w++) {
+        const u32 v = s_part[w];
+        if (w < wv) off += v;
+        tot += v;
+    }
     off += x - mysum;
     for (u32 k = 0; k < per; k++) {
         const u32 slot = tid * per + k;
         if (slot >= nroot) break;
-        const u32 e = table[slot];
-        if (((e >> 24) & 15) == 0xF) {
-            const u32 sb = e & 0xFF;
-            table[slot] = mk_entry(0, K_SUB, sb, off);
-            // fill the subtable: stream bits = slot (root bits) then j (sb bits)
-            for (u32 j = 0; j < (1u << sb); j++)
-                table[off + j] = canon_decode(h, slot | (j << root), root + sb, dist);
-            off += 1u << sb;
+        const u32 sb = table[slot];
+        table[slot] = sb ? mk_entry(0, K_SUB, sb, off) : mk_entry(1, K_BAD, 0, 0);
+        off += sb ? (1u << sb) : 0u;
+    }
+    __syncthreads();
+    if (nroot + tot > cap) return -1;  // cannot happen for a complete code (zlib ENOUGH)
+    // 4. fill: short codes into the root, long codes into their subtable
+#pragma unroll
+    for (u32 i = 0; i < MAXC; i++) {
+        const u32 L = myL[i];
+        if (!L) continue;
+        const u32 s = (wv + i * nwv) * 64 + lane;
+        const u32 e = sym_entry(s, L, dist);
+        if (L <= (u32)root) {
+            for (u32 k = rev[i]; k < nroot; k += 1u << L) table[k] = e;
+        } else {
+            const u32 te = table[rev[i] & (nroot - 1)];
+            const u32 base = te & 0xFFFF, sb = (te >> 16) & 0xFF;
+            for (u32 k = rev[i] >> root; k < (1u << sb); k += 1u << (L - root)) table[base + k] = e;
         }
     }
     __syncthreads();
-    return ok ? 0 : -1;
+    return 0;
 }
 
 // Look up a symbol from >= 15 stream bits `v` (two levels).
@@ -338,7 +363,7 @@ __device__ __attribute__((always_inline)) int read_dynamic(BitIn& b, u8* lens, H
     __syncthreads();
     for (u32 i = tid; i < 19; i += nth) lens[i] = cl[i];
     __syncthreads();
-    build_table(lens, 19, lh, ltab, 7, false);
+    build_table(lens, 19, lh, ltab, 7, false, INF_LTAB);
     u32 idx = 0;
     u8 prev = 0;
     while (idx < nlen + ndist) {
@@ -367,8 +392,8 @@ __device__ __attribute__((always_inline)) int read_dynamic(BitIn& b, u8* lens, H
             rep = 11 + bi_bits(b, 7);
         }
         if (idx + rep > nlen + ndist) return R_INVALID;
-        if (tid == 0)
-            for (u32 k = 0; k < rep; k++) lens[idx + k] = v;
+        if (tid < 64)
+            for (u32 k = tid; k < rep; k += 64) lens[idx + k] = v;
         idx += rep;
         prev = v;
     }
@@ -380,8 +405,8 @@ __device__ __attribute__((always_inline)) int read_dynamic(BitIn& b, u8* lens, H
     if (tid < 32) lens[288 + tid] = tid < ndist ? dl : 0;
     __syncthreads();
     if (lens[256] == 0) return R_INVALID;  // "invalid code -- missing end-of-block"
-    if (build_table(lens, 288, lh, ltab, INF_LBITS, false) != 0) return R_INVALID;
-    if (build_table(lens + 288, 30, dh, dtab, INF_DBITS, true) != 0) return R_INVALID;
+    if (build_table(lens, 288, lh, ltab, INF_LBITS, false, INF_LTAB) != 0) return R_INVALID;
+    if (build_table(lens + 288, 30, dh, dtab, INF_DBITS, true, INF_DTAB) != 0) return R_INVALID;
     return R_OK;
 }
 
@@ -391,8 +416,10 @@ __device__ void fixed_tables(u8* lens, HuffLds* lh, u32* ltab, HuffLds* dh, u32*
     for (u32 i = tid; i < 320; i += nth)
         lens[i] = i < 144 ? 8 : i < 256 ? 9 : i < 280 ? 7 : i < 288 ? 8 : 5;
     __syncthreads();
-    build_table(lens, 288, lh, ltab, INF_LBITS, false);
-    build_table(lens + 288, 30, dh, dtab, INF_DBITS, true);
+    build_table(lens, 288, lh, ltab, INF_LBITS, false, INF_LTAB);
+    // all 32 five-bit distance codes (30 and 31 decode as invalid), as zlib
+    // builds the fixed table: the 30-symbol code alone would be incomplete
+    build_table(lens + 288, 32, dh, dtab, INF_DBITS, true, INF_DTAB);
 }
 
 // Block header: 3 bits, then stored-length check / table construction.

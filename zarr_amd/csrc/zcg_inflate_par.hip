@@ -47,6 +47,10 @@ constexpr u32 PI_WIN = 32768;    // LZ77 window ring
 constexpr u32 PI_SEGW = PI_SEG / 32;
 constexpr u32 PI_IN_VEC = (PI_NL * PI_SEG + 1024) / 128 + 2;  // staged 16-B vectors
 constexpr u32 PI_IN_WORDS = PI_IN_VEC * 4;
+// LDS bank-conflict padding: one pad word after every 8 words, so lanes that
+// read at an 8-word stride (segment starts, segment marks) hit distinct banks.
+constexpr u32 PI_IN_PAD = PI_IN_WORDS + PI_IN_WORDS / 8 + 8;
+__device__ __forceinline__ u32 padw(u32 w) { return w + (w >> 3); }
 constexpr u32 PI_MAXSEG = 64;    // chain segments tracked per round
 
 // token word: literal = byte value; match = 1<<31 | (len-3)<<16 | (dist-1);
@@ -64,7 +68,8 @@ constexpr u32 N_CAP = PI_NL + 2;    // token store full before syncing
 // Debug counters (flag ZCG_FLAG_DEBUG_COUNTERS): summed over all chunks.
 __device__ unsigned long long g_inf_dbg[32];
 enum { DBG_ROUNDS, DBG_CHAIN, DBG_END_CAP, DBG_END_EOB, DBG_END_BAD, DBG_SKIPS, DBG_MRR_IT,
-       DBG_CUTS, DBG_BLOCKS, DBG_BYTES, DBG_TOKENS, DBG_END_ROUND, DBG_PASS2_TOK };
+       DBG_CUTS, DBG_BLOCKS, DBG_BYTES, DBG_TOKENS, DBG_END_ROUND, DBG_PASS2_TOK,
+       DBG_CAP_P1, DBG_CAP_P2, DBG_P2_MAX };
 
 // phase timers (debug): slots 16.. of g_inf_dbg
 enum { TP_HDR = 16, TP_STAGE, TP_PASS1, TP_PASS2, TP_CHAIN, TP_PLACE, TP_LIT, TP_MRR, TP_COMMIT, TP_TOTAL };
@@ -73,7 +78,7 @@ enum { TP_HDR = 16, TP_STAGE, TP_PASS1, TP_PASS2, TP_CHAIN, TP_PLACE, TP_LIT, TP
         if (dbg) {                                                                   \
             __syncthreads();                                                         \
             const u64 _t = __builtin_readcyclecounter();                             \
-            if (tid == 0) atomicAdd(&g_inf_dbg[slot], (unsigned long long)(_t - t_last)); \
+            if (tid == 0) L.dbgc[slot] += (u32)(_t - t_last);                     \
             t_last = _t;                                                             \
         }                                                                            \
     } while (0)
@@ -85,10 +90,11 @@ __device__ __forceinline__ u32 tok_dist(u32 t) { return (t & 0x7FFF) + 1; }
 struct ParLds {
     u8 win[PI_WIN];                  // LZ77 window ring (absolute pos & 32767)
     u16 ptr[PI_STAGE];               // round bytes: 0x8000|value, or an earlier round offset
-    u32 in[PI_IN_WORDS];             // staged stream words
+    u32 in[PI_IN_PAD];               // staged stream words (padded: in[padw(w)])
     u32 pool[PI_NBLK * PI_BLK];      // token pool: lanes take 16-token blocks
     u16 blk[PI_NL * PI_LBLK];        // each lane's pool blocks
-    u32 mark[PI_NL * PI_SEGW];       // token-start bitmap of each lane's own segment
+    u32 mark[PI_NL * (PI_SEGW + 1)]; // token-start bitmap of each lane's segment (+1 pad)
+    u32 head[PI_STAGE / 32];         // token-start bitmap over the round's output bytes
     u32 ltab[INF_LTAB];
     u32 dtab[INF_DTAB];
     HuffLds lh, dh;
@@ -105,7 +111,10 @@ struct ParLds {
     u32 pool_top;
     u32 wsum[8];
     u32 ctl[16];
+    u32 dbgc[32];                    // debug counters of this chunk (flushed at the end)
 };
+// debug counter add (LDS atomic; flushed to g_inf_dbg once per chunk)
+#define DBG_ADD(slot, v) atomicAdd(&L.dbgc[slot], (u32)(v))
 
 static_assert(sizeof(ParLds) <= 160 * 1024, "ParLds exceeds the 160 KiB LDS of a CU");
 
@@ -132,8 +141,12 @@ __device__ __forceinline__ u32 decode_token(const ParLds& L, u64 v, u32* adv) {
 }
 
 // Token j of lane i in the pool.
+// Within a block the slots are rotated by the block id so that lanes reading
+// their j-th token at the same time spread over the LDS banks.
+__device__ __forceinline__ u32 pool_slot(u32 b, u32 j) { return b * PI_BLK + ((j + b) % PI_BLK); }
 __device__ __forceinline__ u32& tok_ref(ParLds& L, u32 i, u32 j) {
-    return L.pool[((u32)L.blk[i * PI_LBLK + (j / PI_BLK)] * PI_BLK) + (j % PI_BLK)];
+    const u32 b = L.blk[i * PI_LBLK + (j / PI_BLK)];
+    return L.pool[pool_slot(b, j)];
 }
 
 // Register bit buffer over the staged words: a 96-bit window (lo:hi) holding
@@ -150,8 +163,8 @@ struct LaneBits {
 __device__ __forceinline__ void lb_init(LaneBits& s, const u32* in, u32 q, u32 bit0) {
     const u32 rel = q - bit0;
     const u32 w = rel >> 5, sh = rel & 31;
-    const u64 a = ((u64)in[w + 1] << 32) | in[w];
-    const u32 c = in[w + 2];
+    const u64 a = ((u64)in[padw(w + 1)] << 32) | in[padw(w)];
+    const u32 c = in[padw(w + 2)];
     s.lo = sh ? (a >> sh) | ((u64)c << (64 - sh)) : a;
     s.hi = sh ? c >> sh : c;
     s.nb = 96 - sh;
@@ -159,7 +172,7 @@ __device__ __forceinline__ void lb_init(LaneBits& s, const u32* in, u32 q, u32 b
 }
 __device__ __forceinline__ void lb_fill(LaneBits& s, const u32* in) {
     if (s.nb <= 64) {
-        const u32 v = in[s.w++];
+        const u32 v = in[padw(s.w++)];
         if (s.nb < 64) {
             s.lo |= (u64)v << s.nb;
             if (s.nb > 32) s.hi = v >> (64 - s.nb);
@@ -279,6 +292,11 @@ __global__ __launch_bounds__(PI_NL) void inflate_par_kernel(const zcg_chunk* __r
     u64 P = 0;
     bool last = false, boundary = false, after_stored = false;
     int r = R_OK;
+    if (dbg) {
+        if (tid < 32) L.dbgc[tid] = 0;
+        if (tid == 0) L.ctl[13] = 0;
+        __syncthreads();
+    }
     u64 t_last = __builtin_readcyclecounter();
     const u64 t_start = t_last;
 
@@ -291,7 +309,7 @@ __global__ __launch_bounds__(PI_NL) void inflate_par_kernel(const zcg_chunk* __r
         const u32 hdr_end = (u32)b.consumed;
         TSTAMP(TP_HDR);
         if (r != R_OK) break;
-        if (dbg && tid == 0) atomicAdd(&g_inf_dbg[DBG_BLOCKS], 1ull);
+        if (dbg && tid == 0) DBG_ADD(DBG_BLOCKS, 1);
         if (type == 0) {
             // ---- stored block: byte copies through the stage --------------------
             u64 in0 = hdr_end >> 3;  // byte aligned after LEN/NLEN
@@ -340,10 +358,15 @@ __global__ __launch_bounds__(PI_NL) void inflate_par_kernel(const zcg_chunk* __r
 #pragma unroll
                 for (u32 k = 0; k < (PI_IN_VEC + PI_NL - 1) / PI_NL; k++) {
                     const u32 vi = tid + k * PI_NL;
-                    if (vi < PI_IN_VEC) *(u32x4*)(L.in + 4 * vi) = v[k];
+                    if (vi < PI_IN_VEC) {
+                        const u32 w = 4 * vi;  // 4 words never straddle a pad (pads after 8)
+                        u32* d = L.in + padw(w);
+                        d[0] = v[k].x; d[1] = v[k].y; d[2] = v[k].z; d[3] = v[k].w;
+                    }
                 }
             }
             if (tid == 0) L.pool_top = 0;
+            for (u32 k = tid; k < PI_STAGE / 32; k += PI_NL) L.head[k] = 0;
             __syncthreads();
             TSTAMP(TP_STAGE);
 
@@ -356,9 +379,9 @@ __global__ __launch_bounds__(PI_NL) void inflate_par_kernel(const zcg_chunk* __r
             u16* myblk = L.blk + tid * PI_LBLK;
             LaneBits bs;
             lb_init(bs, L.in, p, bit0);
-            u32 q = p, nt = 0;
+            u32 q = p, nt = 0, olen_all = 0;  // olen_all: output bytes of all stored tokens
             u32 nxt = 0xFFFFFFFFu;
-            u32* cur = nullptr;  // current pool block of this lane
+            u32 curb = 0;  // current pool block of this lane
             // append a token; false when the lane's token store is full
             auto push = [&](u32 tk) -> bool {
                 if ((nt % PI_BLK) == 0) {
@@ -366,10 +389,11 @@ __global__ __launch_bounds__(PI_NL) void inflate_par_kernel(const zcg_chunk* __r
                     const u32 bi = atomicAdd(&L.pool_top, 1u);
                     if (bi >= PI_NBLK) return false;
                     myblk[nt / PI_BLK] = (u16)bi;
-                    cur = L.pool + bi * PI_BLK;
+                    curb = bi;
                 }
-                cur[nt % PI_BLK] = tk;
+                L.pool[pool_slot(curb, nt)] = tk;
                 nt++;
+                olen_all += tok_len(tk);
                 return true;
             };
             while (q < pend) {
@@ -390,21 +414,21 @@ __global__ __launch_bounds__(PI_NL) void inflate_par_kernel(const zcg_chunk* __r
                 q += adv;
             }
 #pragma unroll
-            for (u32 w = 0; w < PI_SEGW; w++) L.mark[tid * PI_SEGW + w] = mkw[w];
+            for (u32 w = 0; w < PI_SEGW; w++) L.mark[tid * (PI_SEGW + 1) + w] = mkw[w];
             __syncthreads();
             TSTAMP(TP_PASS1);
             // ---- pass 2: follow my path until it meets a marked token start -----
             const u32 round_hi = R0 + PI_NL * PI_SEG;
-            u32 give = 0;
+            u32 give = 0, p2tok = 0;
             while (nxt == 0xFFFFFFFFu) {
                 if (q >= round_hi) { nxt = N_ROUND_END; break; }
                 const u32 k = (q - R0) / PI_SEG;
                 const u32 off = q - (R0 + k * PI_SEG);
-                const u32 mw = L.mark[k * PI_SEGW + (off >> 5)];
+                const u32 mw = L.mark[k * (PI_SEGW + 1) + (off >> 5)];
                 if (mw & (1u << (off & 31))) {
                     // sync: index of that token in lane k's list = marks below it
                     u32 cnt = __popc(mw & ((1u << (off & 31)) - 1));
-                    for (u32 x = 0; x < (off >> 5); x++) cnt += __popc(L.mark[k * PI_SEGW + x]);
+                    for (u32 x = 0; x < (off >> 5); x++) cnt += __popc(L.mark[k * (PI_SEGW + 1) + x]);
                     nxt = k;
                     give = cnt;
                     break;
@@ -414,7 +438,7 @@ __global__ __launch_bounds__(PI_NL) void inflate_par_kernel(const zcg_chunk* __r
                 u32 tk = decode_token(L, bs.lo, &adv);
                 if (q + adv > total_bits) tk = T_EXH;
                 if (!push(tk)) { nxt = N_CAP; break; }
-                if (dbg) atomicAdd(&g_inf_dbg[DBG_PASS2_TOK], 1ull);
+                p2tok++;
                 if (tok_is_marker(tk)) {
                     if (tk == T_EOB) q += adv;
                     nxt = N_MARKER;
@@ -427,6 +451,11 @@ __global__ __launch_bounds__(PI_NL) void inflate_par_kernel(const zcg_chunk* __r
             L.endp[tid] = q;
             L.give[tid] = give;
             L.ntok[tid] = nt;
+            if (dbg) {
+                DBG_ADD(DBG_PASS2_TOK, p2tok);
+                atomicMax(&L.ctl[13], p2tok);
+                if (nxt == N_CAP) L.give[tid] = p2tok == 0 ? 1u : 0u;  // capped inside pass 1?
+            }
             __syncthreads();
             TSTAMP(TP_PASS2);
 
@@ -477,14 +506,17 @@ __global__ __launch_bounds__(PI_NL) void inflate_par_kernel(const zcg_chunk* __r
             const u32 E = L.ctl[5];
             TSTAMP(TP_CHAIN);
             if (dbg && tid == 0) {
-                atomicAdd(&g_inf_dbg[DBG_ROUNDS], 1ull);
-                atomicAdd(&g_inf_dbg[DBG_CHAIN], (unsigned long long)(E + 1));
+                DBG_ADD(DBG_ROUNDS, 1);
+                DBG_ADD(DBG_P2_MAX, L.ctl[13]);
+                L.ctl[13] = 0;
+                if (L.next[E] == N_CAP) DBG_ADD(L.give[E] ? DBG_CAP_P1 : DBG_CAP_P2, 1);
+                DBG_ADD(DBG_CHAIN, E + 1);
                 const u32 nx = L.next[E];
-                atomicAdd(&g_inf_dbg[nx == N_CAP ? DBG_END_CAP : nx == N_ROUND_END ? DBG_END_ROUND
-                                    : (tok_ref(L, E, L.ntok[E] - 1) == T_EOB ? DBG_END_EOB : DBG_END_BAD)], 1ull);
+                DBG_ADD(nx == N_CAP ? DBG_END_CAP : nx == N_ROUND_END ? DBG_END_ROUND
+                        : (tok_ref(L, E, L.ntok[E] - 1) == T_EOB ? DBG_END_EOB : DBG_END_BAD), 1);
                 u32 sk = 0;
                 for (u32 x = 0; x < E; x++) sk += L.next[x] != x + 1;
-                atomicAdd(&g_inf_dbg[DBG_SKIPS], (unsigned long long)sk);
+                DBG_ADD(DBG_SKIPS, sk);
             }
             const u32 my_s = L.sidx[tid];
             const bool on = (tid <= E) && my_s != 0xFFFFFFFFu;
@@ -492,9 +524,13 @@ __global__ __launch_bounds__(PI_NL) void inflate_par_kernel(const zcg_chunk* __r
             u32 marker = 0;
             if (on && tid == E && nxt == N_MARKER) { vend = nt - 1; marker = tok_ref(L, tid, nt - 1); }
             // ---- placement ------------------------------------------------------------------
+            // output bytes of my valid tokens [my_s, vend): the running sum minus
+            // the tokens before my sync point (few) and a trailing marker
             u32 olen = 0;
-            if (on)
-                for (u32 a = my_s; a < vend; a++) olen += tok_len(tok_ref(L, tid, a));
+            if (on) {
+                olen = olen_all - (vend < nt ? 1u : 0u);
+                for (u32 a = 0; a < my_s; a++) olen -= tok_len(tok_ref(L, tid, a));
+            }
             u32 total;
             const u32 base = block_excl_scan(L, olen, &total);
             const u64 room = D - P;
@@ -508,7 +544,7 @@ __global__ __launch_bounds__(PI_NL) void inflate_par_kernel(const zcg_chunk* __r
             bool final_round = false, fin_boundary = false;
             const bool cut = total > cap || (total == cap && cap == room);
             if (cut) {
-                if (dbg && tid == 0) atomicAdd(&g_inf_dbg[DBG_CUTS], 1ull);
+                if (dbg && tid == 0) DBG_ADD(DBG_CUTS, 1);
                 // the lane whose output range holds byte `cap`
                 const bool mine = on && olen > 0 && base < cap && base + olen >= cap;
                 if (mine) {
@@ -520,7 +556,7 @@ __global__ __launch_bounds__(PI_NL) void inflate_par_kernel(const zcg_chunk* __r
                         while (a < vend && acc + tok_len(tok_ref(L, tid, a)) <= cap) { acc += tok_len(tok_ref(L, tid, a)); a++; }
                         L.ctl[7] = 0;
                     }
-                    L.ctl[8] = acc;
+                    L.ctl[8] = acc < cap ? acc : cap;  // a token may cross N: clip there
                     L.ctl[9] = tid;
                     L.ctl[10] = a;
                 }
@@ -542,43 +578,78 @@ __global__ __launch_bounds__(PI_NL) void inflate_par_kernel(const zcg_chunk* __r
             // ---- errors on the taken range ----------------------------------------------------
             if (mk == T_BAD) { r = R_INVALID; break; }
             if (mk == T_EXH) { r = R_EXHAUSTED; break; }
+            // ---- token heads: one entry per taken token ----------------------------------
+            // literal -> 0x8000|byte (final); match -> dist-1 at its first byte,
+            // plus a token-start bit in head[] over the round's output bytes.
+            const u64 S = P;
             bool far = false;
             {
                 u32 o = base;
+                u32 hw = 0xFFFFFFFFu, hbits = 0;
                 for (u32 a = my_s; a < take_end; a++) {
                     const u32 tk = tok_ref(L, tid, a);
-                    if ((tk & T_MATCH) && tok_dist(tk) > P + o) far = true;
-                    o += tok_len(tk);
+                    u16 v;
+                    u32 len;
+                    if (tk & T_MATCH) {
+                        const u32 d = tok_dist(tk);
+                        if (d > P + o) far = true;  // before the stream start
+                        v = (u16)(d - 1);
+                        len = tok_len(tk);
+                    } else {
+                        v = (u16)(0x8000u | (tk & 0xFF));
+                        len = 1;
+                    }
+                    L.ptr[(S + o) & (PI_STAGE - 1)] = v;
+                    if ((o >> 5) != hw) {
+                        if (hbits) atomicOr(&L.head[hw], hbits);
+                        hw = o >> 5;
+                        hbits = 0;
+                    }
+                    hbits |= 1u << (o & 31);
+                    o += len;
                 }
+                if (hbits) atomicOr(&L.head[hw], hbits);
             }
             if (__syncthreads_or(far)) { r = R_INVALID; break; }
             TSTAMP(TP_PLACE);
             // ---- LZ77 resolution by pointer jumping ---------------------------------------
             // Every round byte gets its value (literal, or a byte of the final
-            // window) or a pointer to an EARLIER round byte: a match byte k
-            // copies B[o - d + (k mod d)], which lies before the match start.
-            const u64 S = P;
+            // window) or a pointer to an EARLIER round byte: byte k of a match
+            // (start o, distance d) copies B[o - d + (k mod d)], which lies
+            // before the match start.  Thread t expands the contiguous byte
+            // range [x0, x1), carrying in the match that covers x0.
             {
-                u32 o = base;
-                for (u32 a = my_s; a < take_end; a++) {
-                    const u32 tk = tok_ref(L, tid, a);
-                    if (!(tk & T_MATCH)) {
-                        L.ptr[(S + o) & (PI_STAGE - 1)] = (u16)(0x8000u | (tk & 0xFF));
-                        o++;
-                        continue;
+                const u32 ch = (emitted + PI_NL - 1) / PI_NL;
+                const u32 x0 = tid * ch;
+                const u32 x1 = (x0 + ch < emitted) ? x0 + ch : emitted;
+                u32 mo = 0, md = 0, mj = 0;  // current match: start, distance, k mod d
+                if (x0 < x1 && !((L.head[x0 >> 5] >> (x0 & 31)) & 1u)) {
+                    // nearest token start below x0 (a match: <= 258 bytes back)
+                    u32 w = x0 >> 5;
+                    u32 m = L.head[w] & ((1u << (x0 & 31)) - 1u);
+                    while (!m) m = L.head[--w];
+                    mo = w * 32 + 31 - __builtin_clz(m);
+                    md = (u32)L.ptr[(S + mo) & (PI_STAGE - 1)] + 1;
+                    const u32 k0 = x0 - mo - 1;  // the loop steps mj before use
+                    mj = k0 < md ? k0 : k0 % md;
+                }
+                __syncthreads();  // heads are read before any thread rewrites them
+                u32 hb = x0 < x1 ? L.head[x0 >> 5] : 0;
+                bool in_match = md != 0;
+                for (u32 x = x0; x < x1; x++) {
+                    if ((x & 31) == 0) hb = L.head[x >> 5];
+                    const u32 i = (u32)((S + x) & (PI_STAGE - 1));
+                    if ((hb >> (x & 31)) & 1u) {
+                        const u16 v = L.ptr[i];
+                        if (v & 0x8000u) { in_match = false; continue; }  // literal: final
+                        mo = x; md = (u32)v + 1; mj = 0; in_match = true;
+                    } else if (!in_match) {
+                        continue;  // unreachable for a well-formed round
+                    } else {
+                        mj = (mj + 1 == md) ? 0 : mj + 1;
                     }
-                    const u32 len0 = tok_len(tk), d = tok_dist(tk);
-                    const u32 len = (o + len0 > emitted) ? emitted - o : len0;  // cut at N
-                    u32 j = 0;  // k mod d
-                    for (u32 k = 0; k < len; k++) {
-                        const int sp = (int)o - (int)d + (int)j;
-                        u16 v;
-                        if (sp < 0) v = (u16)(0x8000u | L.win[(S + (int64_t)sp) & (PI_WIN - 1)]);
-                        else v = (u16)sp;
-                        L.ptr[(S + o + k) & (PI_STAGE - 1)] = v;
-                        j = (j + 1 == d) ? 0 : j + 1;
-                    }
-                    o += len0;
+                    const int sp = (int)mo - (int)md + (int)mj;
+                    L.ptr[i] = sp < 0 ? (u16)(0x8000u | L.win[(S + (int64_t)sp) & (PI_WIN - 1)]) : (u16)sp;
                 }
             }
             __syncthreads();
@@ -594,7 +665,7 @@ __global__ __launch_bounds__(PI_NL) void inflate_par_kernel(const zcg_chunk* __r
                         pending |= !(w & 0x8000u);
                     }
                 }
-                if (dbg && tid == 0) atomicAdd(&g_inf_dbg[DBG_MRR_IT], 1ull);
+                if (dbg && tid == 0) DBG_ADD(DBG_MRR_IT, 1);
                 if (!__syncthreads_or(pending)) break;
             }
             TSTAMP(TP_MRR);
@@ -602,8 +673,8 @@ __global__ __launch_bounds__(PI_NL) void inflate_par_kernel(const zcg_chunk* __r
             par_commit(L, dst, S, S + emitted, t);
             P = S + emitted;
             if (dbg) {
-                if (tid == 0) atomicAdd(&g_inf_dbg[DBG_BYTES], (unsigned long long)emitted);
-                if (take_end > my_s) atomicAdd(&g_inf_dbg[DBG_TOKENS], (unsigned long long)(take_end - my_s));
+                if (tid == 0) DBG_ADD(DBG_BYTES, emitted);
+                if (take_end > my_s) DBG_ADD(DBG_TOKENS, take_end - my_s);
             }
             if (final_round) {
                 boundary = fin_boundary;
@@ -630,7 +701,11 @@ __global__ __launch_bounds__(PI_NL) void inflate_par_kernel(const zcg_chunk* __r
     }
     if (r == R_INVALID) st = ZCG_ERR_INVALID_DATA;
     else if (r == R_EXHAUSTED || P < D) st = ZCG_ERR_UNEXPECTED_EOF;
-    if (dbg && tid == 0) atomicAdd(&g_inf_dbg[TP_TOTAL], (unsigned long long)(__builtin_readcyclecounter() - t_start));
+    if (dbg) {
+        if (tid == 0) L.dbgc[TP_TOTAL] = (u32)(__builtin_readcyclecounter() - t_start);
+        __syncthreads();
+        if (tid < 32 && L.dbgc[tid]) atomicAdd(&g_inf_dbg[tid], (unsigned long long)L.dbgc[tid]);
+    }
     if (tid == 0) status[c] = st;
 }
 
