@@ -192,7 +192,7 @@ def main():
                    "ratio": round(n * D / comp_bytes, 3), "parallelism": f"chunks round-robin x{world}"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
-                     "kernel": "inflate_kernel", "kernel_ms": round(kern_ms, 4),
+                     "kernel": "zcg::inflate_par_kernel", "kernel_ms": round(kern_ms, 4),
                      "algorithmic_bytes_per_launch": algo_bytes},
     }
 
