@@ -395,3 +395,48 @@ def test_decode_never_writes_past_n(codec):
             for i, p in enumerate(payloads):
                 assert out[i, :D].tobytes() == p[:D], (D, i)
                 assert (out[i, D:] == 0xAB).all(), (D, i, flags)
+
+
+def check_many(codec, streams, dt, n, flags=0):
+    """Batch decode of many streams; each result must classify and decode like
+    the oracle (one launch, so sweeps of corruptions stay fast)."""
+    import torch
+    from zarr_amd.batch import BatchCodec, PackedStreams
+    es, be, isb, _ = dtype_info(dt)
+    st_ref, out_ref = zref.decode_batch(CODEC_IDS[codec], [np.frombuffer(s, np.uint8) for s in streams],
+                                        n * es, elem_size=es, big_endian=be, is_bool=isb)
+    packed = PackedStreams(streams, n * es, "cuda:0")
+    BatchCodec(0).decode(meta_for(codec, dt, n), packed, flags=flags)
+    torch.cuda.synchronize()
+    st = packed.status.cpu().numpy()
+    out = packed.dst.cpu().numpy().reshape(len(streams), n * es)
+    for i in range(len(streams)):
+        assert KIND[int(st[i])] == KIND[int(st_ref[i])], (i, int(st[i]), int(st_ref[i]))
+        if st_ref[i] == zref.OK:
+            assert out[i].tobytes() == out_ref[i].tobytes(), i
+
+
+def test_gzip_dynamic_header_corruption():
+    """Every byte of three dynamic block headers (the first, and two after
+    full flushes) flipped several ways: the block-parallel header decoder must
+    classify and decode exactly like zlib."""
+    from zarr_amd._native import FLAG_SERIAL_INFLATE
+    parts = [rw(20000, seed=s).tobytes() for s in range(3)]
+    c = zlib.compressobj(6, zlib.DEFLATED, -15)
+    raw, offs = b"", []
+    for p in parts:
+        offs.append(len(raw))
+        raw += c.compress(p) + c.flush(zlib.Z_FULL_FLUSH)
+    raw += c.flush()
+    payload = b"".join(parts)
+    s = gzip_wrap(raw, payload)
+    hdr = len(s) - len(raw) - 8
+    variants = [s]
+    for off in offs:
+        for k in range(90):
+            for x in (0x01, 0x08, 0x40, 0xFF):
+                bad = bytearray(s)
+                bad[hdr + off + k] ^= x
+                variants.append(bytes(bad))
+    for flags in (0, FLAG_SERIAL_INFLATE):
+        check_many("gzip", variants, "u1", len(payload), flags)

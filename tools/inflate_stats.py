@@ -29,11 +29,12 @@ fn(out.ctypes.data, 1)
 names = ["rounds", "chain_lanes", "end_cap", "end_eob", "end_bad", "skips", "mrr_iters", "cuts",
          "blocks", "bytes", "tokens", "end_round", "pass2_tokens", "cap_p1", "cap_p2", "p2_max",
          "cyc_hdr", "cyc_stage", "cyc_pass1", "cyc_pass2", "cyc_chain", "cyc_place", "cyc_lit",
-         "cyc_mrr", "cyc_commit", "cyc_total"]
+         "cyc_mrr", "cyc_commit", "cyc_total", "hdr_pre", "hdr_walk", "hdr_post"]
 d = {k: int(v) for k, v in zip(names, out)}
 d["n_chunks"] = packed.n
 d["per_chunk"] = {k: round(v / packed.n, 2) for k, v in d.items() if k != "n_chunks"}
 d["cycles_per_round"] = {k: round(d[k] / max(1, d["rounds"])) for k in names if k.startswith("cyc_")}
+d["hdr_cycles_per_block"] = {k: round(d[k] / max(1, d["blocks"])) for k in ("hdr_pre", "hdr_walk", "hdr_post", "cyc_hdr")}
 d["avg_chain"] = round(d["chain_lanes"] / max(1, d["rounds"]), 2)
 d["mrr_per_round"] = round(d["mrr_iters"] / max(1, d["rounds"]), 2)
 d["bytes_per_round"] = round(d["bytes"] / max(1, d["rounds"]), 1)

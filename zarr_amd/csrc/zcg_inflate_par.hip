@@ -86,6 +86,8 @@ enum { TP_HDR = 16, TP_STAGE, TP_PASS1, TP_PASS2, TP_CHAIN, TP_PLACE, TP_LIT, TP
 __device__ __forceinline__ bool tok_is_marker(u32 t) { return (t & 0xC0000000u) == 0x40000000u; }
 __device__ __forceinline__ u32 tok_len(u32 t) { return (t & T_MATCH) ? ((t >> 16) & 0xFF) + 3 : 1; }
 __device__ __forceinline__ u32 tok_dist(u32 t) { return (t & 0x7FFF) + 1; }
+// stream bits of a literal/match token (bits 24..29; <= 48)
+__device__ __forceinline__ u32 tok_bits(u32 t) { return (t >> 24) & 63; }
 
 struct ParLds {
     u8 win[PI_WIN];                  // LZ77 window ring (absolute pos & 32767)
@@ -124,7 +126,7 @@ __device__ __forceinline__ u32 decode_token(const ParLds& L, u64 v, u32* adv) {
     const u32 e = table_lookup(L.ltab, INF_LBITS, (u32)v);
     const u32 l = e >> 28;
     const u32 kind = (e >> 24) & 15;
-    if (kind == K_LIT) { *adv = l; return e & 0xFF; }
+    if (kind == K_LIT) { *adv = l; return (l << 24) | (e & 0xFF); }
     if (kind == K_EOB) { *adv = l; return T_EOB; }
     if (kind != K_LEN) { *adv = l ? l : 1; return T_BAD; }
     const u32 ex = (e >> 16) & 0xFF;
@@ -137,7 +139,7 @@ __device__ __forceinline__ u32 decode_token(const ParLds& L, u64 v, u32* adv) {
     const u32 dex = (de >> 16) & 0xFF;
     const u32 dist = (de & 0xFFFF) + ((u32)(vd >> dl) & ((1u << dex) - 1));
     *adv = t + dl + dex;
-    return T_MATCH | ((len - 3) << 16) | (dist - 1);
+    return T_MATCH | ((t + dl + dex) << 24) | ((len - 3) << 16) | (dist - 1);
 }
 
 // Token j of lane i in the pool.
@@ -247,19 +249,212 @@ __device__ __forceinline__ u32 block_excl_scan(ParLds& L, u32 v, u32* total) {
     return off + x - v;
 }
 
-// Bit position of token `j` of lane `i`: replay its path from the lane start.
-__device__ u32 token_pos(const ParLds& L, u32 R0, u32 bit0, u32 i, u32 j) {
-    u32 q = R0 + i * PI_SEG;
-    LaneBits s;
-    lb_init(s, L.in, q, bit0);
-    for (u32 k = 0; k < j; k++) {
-        lb_fill(s, L.in);
-        u32 adv;
-        decode_token(L, s.lo, &adv);
-        lb_drop(s, adv);
-        q += adv;
+// ---- dynamic block header, block-parallel --------------------------------------------
+// Same validity rules and result codes as read_dynamic (zcg_inflate_common.h),
+// in the same order.  The code-length symbols (<= 316 of <= 14 bits) are
+// decoded at EVERY bit position of the header region at once; one lane then
+// walks the true chain through those records (one LDS read per symbol) and the
+// block expands the repeat codes in parallel.
+constexpr u32 HD_BITS = 4608;            // >= 316 symbols * 14 bits
+constexpr u32 HD_WORDS = HD_BITS / 32 + 8;
+
+__device__ int read_dynamic_par(ParLds& L, BitIn& b, bool dbg) {
+    const u32 tid = threadIdx.x;
+    u64 hts = __builtin_readcyclecounter();
+    if (!bi_has(b, 14)) return R_EXHAUSTED;
+    const u32 nlen = bi_bits(b, 5) + 257, ndist = bi_bits(b, 5) + 1, ncode = bi_bits(b, 4) + 4;
+    if (nlen > 286 || ndist > 30) return R_INVALID;  // "too many length or distance symbols"
+    if (!bi_has(b, 3 * ncode)) return R_EXHAUSTED;
+    // the 3-bit code-length code lengths: lane i < ncode reads its own field
+    const u64 c0 = b.consumed;
+    u32 mycl = 0;
+    {
+        bi_refill(b);  // >= 33 bits buffered; 3*19 = 57 may need a second word
+        const u32 lane = tid & 63;
+        const u64 w = b.buf;
+        u32 v = 0;
+        if (lane < ncode) {
+            const u32 at = 3 * lane;
+            v = at + 3 <= b.cnt ? (u32)(w >> at) & 7 : 0xFFFFFFFFu;
+        }
+        const bool need = __ballot(v == 0xFFFFFFFFu) != 0;
+        if (need) {  // rare: read the rest through the word reader
+            const u32 lo = b.cnt;
+            bi_drop(b, lo - lo % 3);
+            bi_refill(b);
+            if (v == 0xFFFFFFFFu) v = (u32)(b.buf >> (3 * lane - (lo - lo % 3))) & 7;
+        }
+        mycl = v;
+        bi_seek(b, c0 + 3 * ncode);
     }
-    return q;
+    {  // code-length code must be complete ("invalid code lengths set")
+        u32 cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        const u32 lane = tid & 63;
+        for (u32 i = 0; i < 19; i++) {
+            const u32 li = __shfl(mycl, (int)i, 64);
+            if (i < ncode) cnt[li & 7]++;
+        }
+        int left = 1;
+        for (int l = 1; l <= 7; l++) { left <<= 1; left -= cnt[l]; if (left < 0) break; }
+        if (left != 0) return R_INVALID;
+        __syncthreads();
+        if (tid < 19) L.lens[tid] = 0;
+        __syncthreads();
+        if (tid < ncode) L.lens[c_clen_order[tid]] = (u8)mycl;
+        (void)lane;
+    }
+    // stage the region [H0, H0 + HD_BITS) of the stream
+    const u64 H0 = b.consumed;
+    const u64 B0 = H0 >> 3;
+    const u32 o = (u32)(H0 & 7);
+    u32* hw = L.in;  // free between rounds
+    for (u32 w = tid; w < HD_WORDS; w += PI_NL) {
+        const u64 q = B0 + 4ull * w;
+        u32 v = 0;
+        if (q + 4 <= b.n) v = ld32(b.src + q);
+        else
+            for (u32 k = 0; k < 4; k++)
+                if (q + k < b.n) v |= (u32)b.src[q + k] << (8 * k);
+        hw[w] = v;
+    }
+    build_table(L.lens, 19, &L.lh, L.ltab, 7, false, INF_LTAB);  // barriers inside
+    // one record per bit position: adv | codelen << 4 | sym << 8 | count << 13
+    u32* rec = L.pool;
+    for (u32 r = tid; r < HD_BITS; r += PI_NL) {
+        const u32 bit = o + r, w = bit >> 5, sh = bit & 31;
+        const u64 x = (((u64)hw[w + 1] << 32) | hw[w]) >> sh;
+        const u32 v = (u32)x & 0x3FFF;
+        const u32 e = L.ltab[v & 127];
+        const u32 l = e >> 28, sym = e & 0x1F;
+        u32 adv = l, cnt = 1;
+        if (sym == 16) { adv = l + 2; cnt = 3 + ((v >> l) & 3); }
+        else if (sym == 17) { adv = l + 3; cnt = 3 + ((v >> l) & 7); }
+        else if (sym == 18) { adv = l + 7; cnt = 11 + ((v >> l) & 127); }
+        rec[r] = adv | (l << 4) | (sym << 8) | (cnt << 13);
+    }
+    __syncthreads();
+    // 2- and 4-symbol jumps: pos (13 bits) | summed count << 13
+    u32* rec2 = (u32*)L.ptr;   // free between rounds
+    u32* rec4 = L.pool + HD_BITS;
+    auto rec_at = [&](u32 r) -> u32 { return rec[r < HD_BITS ? r : HD_BITS - 1]; };
+    for (u32 r = tid; r < HD_BITS; r += PI_NL) {
+        const u32 f0 = rec[r];
+        const u32 r1 = r + (f0 & 15);
+        const u32 f1 = rec_at(r1);
+        rec2[r] = (r1 + (f1 & 15)) | (((f0 >> 13) + (f1 >> 13)) << 13);
+    }
+    __syncthreads();
+    for (u32 r = tid; r < HD_BITS; r += PI_NL) {
+        const u32 g0 = rec2[r];
+        const u32 r2 = g0 & 8191;
+        const u32 g1 = rec2[r2 < HD_BITS ? r2 : HD_BITS - 1];
+        rec4[r] = (g1 & 8191) | (((g0 >> 13) + (g1 >> 13)) << 13);
+    }
+    __syncthreads();
+    // the walk over groups of 4 symbols: gpos[g] = start bit | out index << 13
+    u32* gpos = L.mark;
+    const u32 total = nlen + ndist;
+    if (dbg && tid == 0) { const u64 t = __builtin_readcyclecounter(); L.dbgc[26] += (u32)(t - hts); hts = t; }
+    if (tid == 0) {
+        u32 r = 0, idx = 0, g = 0;
+        while (idx < total) {
+            const u32 f = rec4[r < HD_BITS ? r : HD_BITS - 1];
+            gpos[g++] = r | (idx << 13);
+            idx += f >> 13;
+            r = f & 8191;
+        }
+        L.ctl[1] = g;
+        L.ctl[0] = 0xFFFFFFFFu;  // min (symbol << 2 | error code)
+        L.ctl[2] = 0;            // symbols
+        L.ctl[3] = 0;            // end bit
+    }
+    __syncthreads();
+    // expand the groups: symbol i = 4g + k while its out index < total
+    u32* srec = L.mark + 128;  // idx | cnt << 9 | sym << 17
+    {
+        const u64 lim64 = b.limit - H0;
+        const u32 lim = lim64 < HD_BITS ? (u32)lim64 : HD_BITS;
+        const u32 ng = L.ctl[1];
+        for (u32 g = tid; g < ng; g += PI_NL) {
+            u32 r = gpos[g] & 8191, idx = gpos[g] >> 13;
+            for (u32 k = 0; k < 4 && idx < total; k++) {
+                const u32 f = rec_at(r);
+                const u32 adv = f & 15, l = (f >> 4) & 7, sym = (f >> 8) & 31, cnt = f >> 13;
+                const u32 i = 4 * g + k;
+                u32 err = 0;  // zlib's checks in order: code bits, repeat at 0, extra bits, overflow
+                if (r + l > lim) err = 1 + R_EXHAUSTED;
+                else if (sym == 16 && idx == 0) err = 1 + R_INVALID;
+                else if (r + adv > lim) err = 1 + R_EXHAUSTED;
+                else if (idx + cnt > total) err = 1 + R_INVALID;
+                if (err) atomicMin(&L.ctl[0], (i << 2) | (err - 1));
+                srec[i] = idx | (cnt << 9) | (sym << 17);
+                if (idx + cnt >= total) { L.ctl[2] = i + 1; L.ctl[3] = r + adv; }
+                idx += cnt;
+                r += adv;
+            }
+        }
+    }
+    __syncthreads();
+    const u32 em = L.ctl[0];
+    const u32 nsyms = L.ctl[2], rend = L.ctl[3];
+    if (dbg && tid == 0) { const u64 t = __builtin_readcyclecounter(); L.dbgc[27] += (u32)(t - hts); hts = t; }
+    if (em != 0xFFFFFFFFu) return (int)(em & 3);  // (the reader position no longer matters)
+    for (u32 i = tid; i < nsyms; i += PI_NL) {
+        const u32 f = srec[i];
+        const u32 idx = f & 511, cnt = (f >> 9) & 255, sym = f >> 17;
+        u32 val = sym < 16 ? sym : 0u;
+        if (sym == 16) {  // repeat the previous length: nearest earlier non-16 symbol
+            u32 j = i;
+            u32 sj = 16;
+            while (sj == 16 && j > 0) sj = srec[--j] >> 17;
+            val = sj < 16 ? sj : 0u;
+        }
+        for (u32 k = 0; k < cnt; k++) L.lens[idx + k] = (u8)val;
+    }
+    bi_seek(b, H0 + rend);
+    __syncthreads();
+    u8 dl = 0;
+    if (tid < ndist) dl = L.lens[nlen + tid];
+    __syncthreads();
+    for (u32 i = nlen + tid; i < 288; i += PI_NL) L.lens[i] = 0;
+    if (tid < 32) L.lens[288 + tid] = tid < ndist ? dl : 0;
+    __syncthreads();
+    if (L.lens[256] == 0) return R_INVALID;  // "invalid code -- missing end-of-block"
+    if (build_table(L.lens, 288, &L.lh, L.ltab, INF_LBITS, false, INF_LTAB) != 0) return R_INVALID;
+    if (build_table(L.lens + 288, 30, &L.dh, L.dtab, INF_DBITS, true, INF_DTAB) != 0) return R_INVALID;
+    if (dbg && tid == 0) { const u64 t = __builtin_readcyclecounter(); L.dbgc[28] += (u32)(t - hts); hts = t; }
+    return R_OK;
+}
+
+// read_block_header with the block-parallel dynamic header
+__device__ int read_block_header_par(ParLds& L, BitIn& b, bool* last, u32* type, u32* slen, bool dbg) {
+    if (!bi_has(b, 3)) return R_EXHAUSTED;
+    const u32 hdr = bi_bits(b, 3);
+    *last = hdr & 1;
+    *type = hdr >> 1;
+    if (*type == 0) {
+        const u32 pad = (u32)((8 - (b.consumed & 7)) & 7);  // to byte boundary
+        if (!bi_has(b, pad + 32)) return R_EXHAUSTED;
+        bi_bits(b, pad);
+        const u32 len = bi_bits(b, 16), nlen = bi_bits(b, 16);
+        if ((len ^ 0xFFFF) != nlen) return R_INVALID;  // "invalid stored block lengths"
+        *slen = len;
+        return R_OK;
+    }
+    if (*type == 3) return R_INVALID;  // "invalid block type"
+    if (*type == 1) { fixed_tables(L.lens, &L.lh, L.ltab, &L.dh, L.dtab); return R_OK; }
+    return read_dynamic_par(L, b, dbg);
+}
+
+// Bit position of token `j` of lane `i`: its segment start plus the bit
+// lengths stored in tokens 0..j-1 (never markers).  Called by one full wave.
+__device__ u32 token_pos(const ParLds& L, u32 R0, u32 i, u32 j) {
+    const u32 lane = threadIdx.x & 63;
+    u32 sum = 0;
+    for (u32 k = lane; k < j; k += 64) sum += tok_bits(L.pool[pool_slot(L.blk[i * PI_LBLK + k / PI_BLK], k)]);
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) sum += __shfl_xor(sum, d, 64);
+    return R0 + i * PI_SEG + sum;
 }
 
 __global__ __launch_bounds__(PI_NL) void inflate_par_kernel(const zcg_chunk* __restrict__ chunks,
@@ -305,7 +500,7 @@ __global__ __launch_bounds__(PI_NL) void inflate_par_kernel(const zcg_chunk* __r
         // ---- block header (all waves, identical) ------------------------------------
         if (last) { r = R_EXHAUSTED; break; }
         u32 type = 0, slen = 0;
-        r = read_block_header(b, &last, &type, &slen, L.lens, &L.lh, L.ltab, &L.dh, L.dtab);
+        r = read_block_header_par(L, b, &last, &type, &slen, dbg);
         const u32 hdr_end = (u32)b.consumed;
         TSTAMP(TP_HDR);
         if (r != R_OK) break;
@@ -568,9 +763,10 @@ __global__ __launch_bounds__(PI_NL) void inflate_par_kernel(const zcg_chunk* __r
                 mk = 0;
                 if (tid > cl) take_end = my_s;
                 if (tid == cl) take_end = L.ctl[10];
-                if (tid == 0) {  // bit position of the first token not taken
+                if (tid < 64) {  // bit position of the first token not taken
                     const u32 a = L.ctl[10];
-                    L.ctl[11] = (a < L.ntok[cl]) ? token_pos(L, R0, bit0, cl, a) : L.endp[cl];
+                    const u32 pos = (a < L.ntok[cl]) ? token_pos(L, R0, cl, a) : L.endp[cl];
+                    if (tid == 0) L.ctl[11] = pos;
                 }
                 __syncthreads();
                 round_end = L.ctl[11];
@@ -649,21 +845,33 @@ __global__ __launch_bounds__(PI_NL) void inflate_par_kernel(const zcg_chunk* __r
                         mj = (mj + 1 == md) ? 0 : mj + 1;
                     }
                     const int sp = (int)mo - (int)md + (int)mj;
-                    L.ptr[i] = sp < 0 ? (u16)(0x8000u | L.win[(S + (int64_t)sp) & (PI_WIN - 1)]) : (u16)sp;
+                    u16 nv;
+                    if (sp < 0) nv = (u16)(0x8000u | L.win[(S + (int64_t)sp) & (PI_WIN - 1)]);
+                    else if ((u32)sp >= x0) nv = L.ptr[(S + (u32)sp) & (PI_STAGE - 1)];  // mine, final
+                    else nv = (u16)sp;
+                    L.ptr[i] = nv;
                 }
             }
             __syncthreads();
             TSTAMP(TP_LIT);
             for (;;) {
                 bool pending = false;
-                for (u32 x = tid; x < emitted; x += PI_NL) {
-                    const u32 i = (u32)((S + x) & (PI_STAGE - 1));
-                    const u16 v = L.ptr[i];
-                    if (!(v & 0x8000u)) {
-                        const u16 w = L.ptr[(u32)((S + v) & (PI_STAGE - 1))];
-                        L.ptr[i] = w;
-                        pending |= !(w & 0x8000u);
+                for (u32 x = tid; x < emitted; x += 4 * PI_NL) {
+                    u16 v[4], w[4];
+#pragma unroll
+                    for (u32 u = 0; u < 4; u++) {
+                        const u32 xx = x + u * PI_NL;
+                        v[u] = xx < emitted ? L.ptr[(u32)((S + xx) & (PI_STAGE - 1))] : (u16)0x8000u;
                     }
+#pragma unroll
+                    for (u32 u = 0; u < 4; u++)
+                        w[u] = (v[u] & 0x8000u) ? v[u] : L.ptr[(u32)((S + v[u]) & (PI_STAGE - 1))];
+#pragma unroll
+                    for (u32 u = 0; u < 4; u++)
+                        if (!(v[u] & 0x8000u)) {
+                            L.ptr[(u32)((S + x + u * PI_NL) & (PI_STAGE - 1))] = w[u];
+                            pending |= !(w[u] & 0x8000u);
+                        }
                 }
                 if (dbg && tid == 0) DBG_ADD(DBG_MRR_IT, 1);
                 if (!__syncthreads_or(pending)) break;
