@@ -27,9 +27,9 @@ torch.cuda.synchronize()
 t1 = time.time()
 fn(out.ctypes.data, 1)
 names = ["rounds", "chain_lanes", "end_cap", "end_eob", "end_bad", "skips", "mrr_iters", "cuts",
-         "blocks", "bytes", "tokens", "end_round", "pass2_tokens", "cap_p1", "cap_p2", "p2_max",
+         "blocks", "bytes", "tokens", "end_round", "pass2_tokens", "p2h_32_48", "p2h_48up", "p2_max",
          "cyc_hdr", "cyc_stage", "cyc_pass1", "cyc_pass2", "cyc_chain", "cyc_place", "cyc_lit",
-         "cyc_mrr", "cyc_commit", "cyc_total", "hdr_pre", "hdr_walk", "hdr_post"]
+         "cyc_mrr", "cyc_commit", "cyc_total", "hdr_pre", "hdr_walk", "hdr_post", "p2h_0_8", "p2h_8_16", "p2h_16_32"]
 d = {k: int(v) for k, v in zip(names, out)}
 d["n_chunks"] = packed.n
 d["per_chunk"] = {k: round(v / packed.n, 2) for k, v in d.items() if k != "n_chunks"}

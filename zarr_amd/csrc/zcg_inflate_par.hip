@@ -41,7 +41,7 @@ constexpr u32 PI_SEG = 256;      // bits per lane segment
 constexpr u32 PI_BLK = 16;       // tokens per pool block
 constexpr u32 PI_LBLK = 5;       // pool blocks per lane -> up to 80 tokens per lane
 constexpr u32 PI_TMAX = PI_BLK * PI_LBLK;
-constexpr u32 PI_NBLK = 640;     // pool blocks per round (avg need ~1.7 per lane)
+constexpr u32 PI_NBLK = 864;     // pool blocks per round: 2 per lane static + 352 on demand
 constexpr u32 PI_STAGE = 16384;  // output bytes per round (power of 2)
 constexpr u32 PI_WIN = 32768;    // LZ77 window ring
 constexpr u32 PI_SEGW = PI_SEG / 32;
@@ -142,13 +142,48 @@ __device__ __forceinline__ u32 decode_token(const ParLds& L, u64 v, u32* adv) {
     return T_MATCH | ((t + dl + dex) << 24) | ((len - 3) << 16) | (dist - 1);
 }
 
+// decode_token without control flow on the token kind: both table lookups
+// always run (the distance one is ignored for literals), so lanes of a wave
+// holding different kinds do not serialise.
+__device__ __forceinline__ u32 decode_token_fast(const ParLds& L, u64 v, u32* adv) {
+    u32 e = L.ltab[(u32)v & ((1u << INF_LBITS) - 1)];
+    if (((e >> 24) & 15) == K_SUB)
+        e = L.ltab[(e & 0xFFFF) + (((u32)v >> INF_LBITS) & ((1u << ((e >> 16) & 0xFF)) - 1))];
+    const u32 l = e >> 28, kind = (e >> 24) & 15, ex = (e >> 16) & 0xFF;
+    const u32 t = l + ex;
+    const u64 vd = v >> t;
+    u32 de = L.dtab[(u32)vd & ((1u << INF_DBITS) - 1)];
+    if (((de >> 24) & 15) == K_SUB)
+        de = L.dtab[(de & 0xFFFF) + (((u32)vd >> INF_DBITS) & ((1u << ((de >> 16) & 0xFF)) - 1))];
+    const u32 dl = de >> 28, dex = (de >> 16) & 0xFF;
+    const u32 len = (e & 0xFFFF) + ((u32)(v >> l) & ((1u << ex) - 1));
+    const u32 dist = (de & 0xFFFF) + ((u32)(vd >> dl) & ((1u << dex) - 1));
+    const u32 madv = t + dl + dex;
+    const bool dok = ((de >> 24) & 15) == K_DIST;
+    u32 tk = T_BAD, a = l ? l : 1;
+    if (kind == K_LIT) { tk = (l << 24) | (e & 0xFF); a = l; }
+    if (kind == K_EOB) tk = T_EOB;
+    if (kind == K_LEN) {
+        tk = dok ? (T_MATCH | (madv << 24) | ((len - 3) << 16) | (dist - 1)) : T_BAD;
+        a = dok ? madv : t + (dl ? dl : 1);
+    }
+    *adv = a;
+    return tk;
+}
+
 // Token j of lane i in the pool.
 // Within a block the slots are rotated by the block id so that lanes reading
 // their j-th token at the same time spread over the LDS banks.
 __device__ __forceinline__ u32 pool_slot(u32 b, u32 j) { return b * PI_BLK + ((j + b) % PI_BLK); }
+// Lane i owns pool blocks 2i and 2i+1 (its first 32 tokens) outright; blocks
+// from PI_STATIC_BLK up are taken on demand (L.blk records them).
+constexpr u32 PI_STATIC_TOK = 2 * PI_BLK;
+constexpr u32 PI_STATIC_BLK = 2 * PI_NL;
+__device__ __forceinline__ u32 tok_blk(const ParLds& L, u32 i, u32 j) {
+    return j < PI_STATIC_TOK ? 2 * i + j / PI_BLK : (u32)L.blk[i * PI_LBLK + (j / PI_BLK)];
+}
 __device__ __forceinline__ u32& tok_ref(ParLds& L, u32 i, u32 j) {
-    const u32 b = L.blk[i * PI_LBLK + (j / PI_BLK)];
-    return L.pool[pool_slot(b, j)];
+    return L.pool[pool_slot(tok_blk(L, i, j), j)];
 }
 
 // Register bit buffer over the staged words: a 96-bit window (lo:hi) holding
@@ -159,7 +194,8 @@ struct LaneBits {
     u64 lo;
     u32 hi;
     u32 nb;
-    u32 w;  // next staged word to append
+    u32 w;   // staged word after `nw`
+    u32 nw;  // next staged word to append (prefetched one fill ahead)
 };
 
 __device__ __forceinline__ void lb_init(LaneBits& s, const u32* in, u32 q, u32 bit0) {
@@ -170,11 +206,13 @@ __device__ __forceinline__ void lb_init(LaneBits& s, const u32* in, u32 q, u32 b
     s.lo = sh ? (a >> sh) | ((u64)c << (64 - sh)) : a;
     s.hi = sh ? c >> sh : c;
     s.nb = 96 - sh;
-    s.w = w + 3;
+    s.nw = in[padw(w + 3)];
+    s.w = w + 4;
 }
 __device__ __forceinline__ void lb_fill(LaneBits& s, const u32* in) {
     if (s.nb <= 64) {
-        const u32 v = in[padw(s.w++)];
+        const u32 v = s.nw;
+        s.nw = in[padw(s.w++)];
         if (s.nb < 64) {
             s.lo |= (u64)v << s.nb;
             if (s.nb > 32) s.hi = v >> (64 - s.nb);
@@ -451,7 +489,7 @@ __device__ int read_block_header_par(ParLds& L, BitIn& b, bool* last, u32* type,
 __device__ u32 token_pos(const ParLds& L, u32 R0, u32 i, u32 j) {
     const u32 lane = threadIdx.x & 63;
     u32 sum = 0;
-    for (u32 k = lane; k < j; k += 64) sum += tok_bits(L.pool[pool_slot(L.blk[i * PI_LBLK + k / PI_BLK], k)]);
+    for (u32 k = lane; k < j; k += 64) sum += tok_bits(L.pool[pool_slot(tok_blk(L, i, k), k)]);
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) sum += __shfl_xor(sum, d, 64);
     return R0 + i * PI_SEG + sum;
@@ -560,31 +598,34 @@ __global__ __launch_bounds__(PI_NL) void inflate_par_kernel(const zcg_chunk* __r
                     }
                 }
             }
-            if (tid == 0) L.pool_top = 0;
+            if (tid == 0) L.pool_top = PI_STATIC_BLK;
             for (u32 k = tid; k < PI_STAGE / 32; k += PI_NL) L.head[k] = 0;
+            for (u32 k = tid; k < PI_NL * (PI_SEGW + 1); k += PI_NL) L.mark[k] = 0;
             __syncthreads();
             TSTAMP(TP_STAGE);
 
             // ---- pass 1: decode my own segment, mark token starts ----------------
             const u32 p = R0 + tid * PI_SEG;
             const u32 pend = p + PI_SEG;
-            u32 mkw[PI_SEGW];
-#pragma unroll
-            for (u32 w = 0; w < PI_SEGW; w++) mkw[w] = 0;
             u16* myblk = L.blk + tid * PI_LBLK;
+            u32* mymark = L.mark + tid * (PI_SEGW + 1);
             LaneBits bs;
             lb_init(bs, L.in, p, bit0);
             u32 q = p, nt = 0, olen_all = 0;  // olen_all: output bytes of all stored tokens
             u32 nxt = 0xFFFFFFFFu;
-            u32 curb = 0;  // current pool block of this lane
+            u32 curb = 2 * tid;  // current pool block of this lane
             // append a token; false when the lane's token store is full
             auto push = [&](u32 tk) -> bool {
                 if ((nt % PI_BLK) == 0) {
-                    if (nt == PI_TMAX) return false;
-                    const u32 bi = atomicAdd(&L.pool_top, 1u);
-                    if (bi >= PI_NBLK) return false;
-                    myblk[nt / PI_BLK] = (u16)bi;
-                    curb = bi;
+                    if (nt < PI_STATIC_TOK) {
+                        curb = 2 * tid + nt / PI_BLK;
+                    } else {
+                        if (nt == PI_TMAX) return false;
+                        const u32 bi = atomicAdd(&L.pool_top, 1u);
+                        if (bi >= PI_NBLK) return false;
+                        myblk[nt / PI_BLK] = (u16)bi;
+                        curb = bi;
+                    }
                 }
                 L.pool[pool_slot(curb, nt)] = tk;
                 nt++;
@@ -594,12 +635,11 @@ __global__ __launch_bounds__(PI_NL) void inflate_par_kernel(const zcg_chunk* __r
             while (q < pend) {
                 lb_fill(bs, L.in);
                 u32 adv;
-                u32 tk = decode_token(L, bs.lo, &adv);
+                u32 tk = decode_token_fast(L, bs.lo, &adv);
                 if (q + adv > total_bits) tk = T_EXH;
                 if (!push(tk)) { nxt = N_CAP; break; }
                 const u32 off = q - p;
-#pragma unroll
-                for (u32 w = 0; w < PI_SEGW; w++) mkw[w] |= ((off >> 5) == w) ? (1u << (off & 31)) : 0u;
+                atomicOr(&mymark[off >> 5], 1u << (off & 31));
                 if (tok_is_marker(tk)) {
                     if (tk == T_EOB) q += adv;
                     nxt = N_MARKER;
@@ -608,8 +648,6 @@ __global__ __launch_bounds__(PI_NL) void inflate_par_kernel(const zcg_chunk* __r
                 lb_drop(bs, adv);
                 q += adv;
             }
-#pragma unroll
-            for (u32 w = 0; w < PI_SEGW; w++) L.mark[tid * (PI_SEGW + 1) + w] = mkw[w];
             __syncthreads();
             TSTAMP(TP_PASS1);
             // ---- pass 2: follow my path until it meets a marked token start -----
@@ -617,20 +655,21 @@ __global__ __launch_bounds__(PI_NL) void inflate_par_kernel(const zcg_chunk* __r
             u32 give = 0, p2tok = 0;
             while (nxt == 0xFFFFFFFFu) {
                 if (q >= round_hi) { nxt = N_ROUND_END; break; }
-                const u32 k = (q - R0) / PI_SEG;
-                const u32 off = q - (R0 + k * PI_SEG);
-                const u32 mw = L.mark[k * (PI_SEGW + 1) + (off >> 5)];
+                const u32 rel = q - R0;
+                const u32 k = rel / PI_SEG, off = rel % PI_SEG;
+                const u32* km = L.mark + k * (PI_SEGW + 1);
+                const u32 mw = km[off >> 5];
+                lb_fill(bs, L.in);
+                u32 adv;
+                u32 tk = decode_token_fast(L, bs.lo, &adv);  // (discarded on a sync)
                 if (mw & (1u << (off & 31))) {
                     // sync: index of that token in lane k's list = marks below it
                     u32 cnt = __popc(mw & ((1u << (off & 31)) - 1));
-                    for (u32 x = 0; x < (off >> 5); x++) cnt += __popc(L.mark[k * (PI_SEGW + 1) + x]);
+                    for (u32 x = 0; x < (off >> 5); x++) cnt += __popc(km[x]);
                     nxt = k;
                     give = cnt;
                     break;
                 }
-                lb_fill(bs, L.in);
-                u32 adv;
-                u32 tk = decode_token(L, bs.lo, &adv);
                 if (q + adv > total_bits) tk = T_EXH;
                 if (!push(tk)) { nxt = N_CAP; break; }
                 p2tok++;
@@ -647,9 +686,10 @@ __global__ __launch_bounds__(PI_NL) void inflate_par_kernel(const zcg_chunk* __r
             L.give[tid] = give;
             L.ntok[tid] = nt;
             if (dbg) {
+                DBG_ADD(p2tok < 8 ? 29 : p2tok < 16 ? 30 : p2tok < 32 ? 31 : p2tok < 48 ? 13 : 14, 1);
                 DBG_ADD(DBG_PASS2_TOK, p2tok);
                 atomicMax(&L.ctl[13], p2tok);
-                if (nxt == N_CAP) L.give[tid] = p2tok == 0 ? 1u : 0u;  // capped inside pass 1?
+
             }
             __syncthreads();
             TSTAMP(TP_PASS2);
@@ -704,7 +744,7 @@ __global__ __launch_bounds__(PI_NL) void inflate_par_kernel(const zcg_chunk* __r
                 DBG_ADD(DBG_ROUNDS, 1);
                 DBG_ADD(DBG_P2_MAX, L.ctl[13]);
                 L.ctl[13] = 0;
-                if (L.next[E] == N_CAP) DBG_ADD(L.give[E] ? DBG_CAP_P1 : DBG_CAP_P2, 1);
+
                 DBG_ADD(DBG_CHAIN, E + 1);
                 const u32 nx = L.next[E];
                 DBG_ADD(nx == N_CAP ? DBG_END_CAP : nx == N_ROUND_END ? DBG_END_ROUND
