@@ -1,0 +1,130 @@
+#!/usr/bin/env python3
+"""End-to-end (host-resident) decode rate, SURVEY §8(d) 'e2e'.
+
+Compressed chunks start in pinned host memory and decoded chunks end in
+pinned host memory: H2D of each sub-batch's streams, zcg_decode_batch, D2H
+of its decoded elements, software-pipelined over several HIP streams so the
+copy engines and the decode kernel overlap.  Prints one JSON line with the
+e2e GiB/s next to the device-resident rate measured in the same process.
+
+    python tools/e2e_bench.py [--codec gzip] [--chunks 1024] [--sub 128] [--streams 3]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402  (device memory, streams, pinned host buffers)
+
+from bench import gzip_flate2, quant_chunk  # noqa: E402
+from zarr_amd import ArrayMetadata, Gzip  # noqa: E402
+from zarr_amd.batch import BatchCodec  # noqa: E402
+
+GIB = float(1 << 30)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--chunks", type=int, default=1024)
+    ap.add_argument("--sub", type=int, default=128)
+    ap.add_argument("--streams", type=int, default=3)
+    ap.add_argument("--reps", type=int, default=3)
+    args = ap.parse_args()
+    dev = torch.device("cuda:0")
+    D = 1 << 20
+    uniq = [quant_chunk(i).tobytes() for i in range(32)]
+    streams = [gzip_flate2(u, 6) for u in uniq]
+    n, sub = args.chunks, args.sub
+    assert n % sub == 0
+    slot = max(len(s) for s in streams)
+    slot = (slot + 255) // 256 * 256
+    # pinned host: compressed slots (one per chunk) and decoded output
+    h_src = torch.empty(n * slot, dtype=torch.uint8).pin_memory()
+    h_dst = torch.empty(n * D, dtype=torch.uint8).pin_memory()
+    hs = h_src.numpy()
+    lens = np.zeros(n, np.uint64)
+    for i in range(n):
+        s = streams[i % len(streams)]
+        hs[i * slot:i * slot + len(s)] = np.frombuffer(s, np.uint8)
+        lens[i] = len(s)
+    meta = ArrayMetadata.new([256, 256, 4 * n], [256, 256, 4], "<f4", Gzip(6))
+    codec = BatchCodec(0)
+    ns = args.streams
+    strm = [torch.cuda.Stream(device=dev) for _ in range(ns)]
+    # per-stream device buffers for one sub-batch
+    d_src = [torch.empty(sub * slot, dtype=torch.uint8, device=dev) for _ in range(ns)]
+    d_dst = [torch.empty(sub * D, dtype=torch.uint8, device=dev) for _ in range(ns)]
+    d_stat = [torch.empty(sub, dtype=torch.int32, device=dev) for _ in range(ns)]
+    descs = []
+    for k in range(ns):
+        d = np.zeros((sub, 4), np.uint64)
+        for j in range(sub):
+            d[j] = (d_src[k].data_ptr() + j * slot, 0, d_dst[k].data_ptr() + j * D, D)
+        descs.append(d)
+    d_desc = [[None] * (n // sub) for _ in range(ns)]
+    for b in range(n // sub):
+        k = b % ns
+        d = descs[k].copy()
+        d[:, 1] = lens[b * sub:(b + 1) * sub]
+        d_desc[k][b] = torch.from_numpy(d.view(np.int64)).to(dev)
+    stat_host = torch.empty(n, dtype=torch.int32).pin_memory()
+
+    class _P:  # PackedStreams-shaped view for BatchCodec.decode
+        pass
+
+    def run():
+        for b in range(n // sub):
+            k = b % ns
+            s = strm[k]
+            with torch.cuda.stream(s):
+                d_src[k].copy_(h_src[b * sub * slot:(b + 1) * sub * slot], non_blocking=True)
+                p = _P()
+                p.desc, p.n, p.status = d_desc[k][b], sub, d_stat[k]
+                codec.decode(meta, p, stream=s)
+                h_dst[b * sub * D:(b + 1) * sub * D].copy_(d_dst[k], non_blocking=True)
+                stat_host[b * sub:(b + 1) * sub].copy_(d_stat[k], non_blocking=True)
+        torch.cuda.synchronize()
+
+    run()  # warm-up + parity of the pipeline
+    assert (stat_host.numpy() == 0).all()
+    hd = h_dst.numpy()
+    for i in range(0, n, max(1, n // 16)):
+        assert hd[i * D:(i + 1) * D].tobytes() == uniq[i % len(uniq)], i
+    best = 1e9
+    for _ in range(args.reps):
+        t0 = time.perf_counter()
+        run()
+        best = min(best, time.perf_counter() - t0)
+    # device-resident reference point: one sub-batch stream's decode alone, repeated
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s = strm[0]
+    p = _P()
+    p.desc, p.n, p.status = d_desc[0][0], sub, d_stat[0]
+    with torch.cuda.stream(s):
+        codec.decode(meta, p, stream=s)
+        ev0.record(s)
+        for _ in range(4):
+            codec.decode(meta, p, stream=s)
+        ev1.record(s)
+    torch.cuda.synchronize()
+    dev_s = ev0.elapsed_time(ev1) / 4 * 1e-3
+    out = {
+        "what": "e2e gzip decode, pinned host -> H2D -> decode -> D2H -> pinned host",
+        "chunks": n, "sub_batch": sub, "streams": ns, "chunk_bytes": D,
+        "compressed_bytes": int(lens.sum()),
+        "e2e_GiBps": round(n * D / best / GIB, 3),
+        "e2e_ms": round(best * 1e3, 2),
+        "device_only_GiBps_sub_batch": round(sub * D / dev_s / GIB, 3),
+        "h2d_plus_d2h_bytes": int(lens.sum()) + n * D,
+    }
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
