@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Benchmark of the MI355X Zarr chunk-codec path (driver contract).
 
-Default workload (BASELINE.json configs[1], "C2"): gzip level-6 chunks of
+Headline workload (BASELINE.json configs[1], "C2"): gzip level-6 chunks of
 f32 256x256x4 (1 MiB decoded), batch of 4096 device-resident chunks per GPU,
 decoded by one zcg_decode_batch call per step.  A step = one decode of the
 whole batch.  Inputs are synthetic ("quant" distribution of SURVEY §8(d),
@@ -10,10 +10,16 @@ seeded), encoded on the host with the standard-library zlib (same zlib
 A pool of distinct chunks is replicated into distinct HBM slots (compressed
 AND decoded buffers each have their own address) up to the batch size.
 
-N>1: one process per GPU (torch.distributed, RCCL backend only for the
-barrier and the max-over-ranks time).  Chunks are independent, so each rank
-decodes its own batch (round-robin partition, no data-path collective):
-"scaling": "weak".  value = decoded bytes of ALL ranks / max rank time.
+The same JSON line carries "per_codec" legs for the other CompressionTypes
+on the GPU (metric = decoded GiB/s per CompressionType): LZ4 decode on the C4
+shape (i16 random-walk 1 MiB chunks, inputs made by the GPU LZ4 encoder and
+gated bit-exact), Raw decode, and LZ4 encode.  `--codec lz4|raw` makes one of
+them the headline instead.
+
+N>1: one process per GPU (torch.distributed, RCCL only for the barrier and
+the max-over-ranks time).  Chunks are independent, so each rank decodes its
+own batch (round-robin partition, no data-path collective): "scaling":
+"weak".  value = decoded bytes of ALL ranks / max rank time.
 
 roofline: algorithmic bytes per launch = sum(C + D) over the batch (C =
 compressed stream bytes read once, D = decoded bytes written once) / the
@@ -37,6 +43,7 @@ sys.path.insert(0, ROOT)
 METRIC = "decoded chunk GiB/s (device-resident) per CompressionType at 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
 GIB = float(1 << 30)
+KERNEL = {"gzip": "zcg::inflate_par_kernel", "lz4": "zcg::lz4_decode_kernel", "raw": "zcg::raw_kernel"}
 
 
 def quant_chunk(idx: int) -> np.ndarray:
@@ -64,17 +71,178 @@ def gzip_flate2(payload: bytes, level: int = 6) -> bytes:
     return hdr + body + struct.pack("<II", zlib.crc32(payload), len(payload) & 0xFFFFFFFF)
 
 
-def build_pool(codec: str, pool: int, threads: int):
-    from concurrent.futures import ThreadPoolExecutor
+class _Batch:  # PackedStreams-shaped holder for BatchCodec.decode
+    pass
+
+
+def workload(codec: str):
+    """(meta, value generator, description) of each codec's bench shape."""
+    from zarr_amd import ArrayMetadata, Gzip, Lz4, Raw
     if codec == "gzip":
-        gen = quant_chunk
-        enc = lambda a: gzip_flate2(a.tobytes(), 6)  # noqa: E731
-    else:
-        raise SystemExit(f"codec {codec}: host-side input generation not available")
+        meta = ArrayMetadata.new([256 * 64, 256 * 64, 4], [256, 256, 4], "<f4", Gzip(6))
+        return meta, quant_chunk, "C2: gzip f32 256x256x4 (1 MiB) chunks, decode"
+    if codec == "lz4":
+        meta = ArrayMetadata.new([128 * 64, 64 * 64, 64], [128, 64, 64], "<i2", Lz4(65536))
+        return meta, randwalk_chunk, "C4: lz4 i16 128x64x64 (1 MiB) chunks, decode"
+    meta = ArrayMetadata.new([128 * 64, 64 * 64, 64], [128, 64, 64], "<i2", Raw())
+    return meta, randwalk_chunk, "raw i16 128x64x64 (1 MiB) chunks, decode"
+
+
+def gpu_encode_pool(meta, vals, dev):
+    """Pool streams made by the GPU encoder (zcg_encode_batch)."""
+    import torch
+    from zarr_amd.batch import BatchCodec, make_encode_batch
+    bc = BatchCodec(dev.index or 0)
+    D = vals[0].nbytes
+    elems = torch.from_numpy(np.concatenate([v.view(np.uint8) for v in vals])).to(dev)
+    cap = bc.encode_bound(meta, D)
+    desc, dst, out_len, status = make_encode_batch(elems, len(vals), cap, dev)
+    bc.encode(meta, desc, len(vals), out_len, status)
+    torch.cuda.synchronize()
+    assert (status.cpu().numpy() == 0).all(), "GPU encode failed"
+    ol = out_len.cpu().numpy()
+    buf = dst.cpu().numpy().reshape(len(vals), cap)
+    return [buf[i, :ol[i]].tobytes() for i in range(len(vals))]
+
+
+def build_pool(codec, meta, gen, pool, threads, dev):
+    from concurrent.futures import ThreadPoolExecutor
     vals = [gen(i) for i in range(pool)]
-    with ThreadPoolExecutor(threads) as ex:  # zlib releases the GIL
-        streams = list(ex.map(enc, vals))
+    if codec == "gzip":
+        with ThreadPoolExecutor(threads) as ex:  # zlib releases the GIL
+            streams = list(ex.map(lambda a: gzip_flate2(a.tobytes(), 6), vals))
+    elif codec == "lz4":
+        streams = gpu_encode_pool(meta, vals, dev)
+    else:
+        streams = [v.tobytes() for v in vals]
     return vals, streams
+
+
+def sync_max(t_local, world, dev):
+    import torch
+    if world == 1:
+        return t_local
+    t = torch.tensor([t_local], dtype=torch.float64, device=dev)
+    torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    return float(t.item())
+
+
+def barrier(world):
+    import torch
+    if world > 1:
+        torch.distributed.barrier()
+
+
+def decode_leg(codec, n, steps, warmup, pool, rank, world, dev, threads):
+    """Decode `n` device-resident chunks per rank, `steps` timed launches.
+    Returns (result dict, vals, streams)."""
+    import torch
+    from zarr_amd.batch import BatchCodec
+    meta, gen, desc_txt = workload(codec)
+    vals, streams = build_pool(codec, meta, gen, pool, threads, dev)
+    D = vals[0].nbytes
+    ALIGN = 256
+    slot = [(len(s) + ALIGN - 1) // ALIGN * ALIGN for s in streams]
+    order = [(rank * n + i) % pool for i in range(n)]  # round-robin pool mapping
+    offs = np.zeros(n + 1, np.int64)
+    for i, u in enumerate(order):
+        offs[i + 1] = offs[i] + slot[u]
+    src = torch.empty(int(offs[-1]), dtype=torch.uint8, device=dev)
+    pool_dev = [torch.from_numpy(np.frombuffer(s, np.uint8).copy()).to(dev) for s in streams]
+    for i, u in enumerate(order):
+        src[offs[i]:offs[i] + len(streams[u])].copy_(pool_dev[u])
+    dst = torch.empty(n * D, dtype=torch.uint8, device=dev)
+    desc = np.zeros((n, 4), np.uint64)
+    for i, u in enumerate(order):
+        desc[i] = (src.data_ptr() + int(offs[i]), len(streams[u]), dst.data_ptr() + i * D, D)
+    packed = _Batch()
+    packed.n = n
+    packed.desc = torch.from_numpy(desc.view(np.int64)).to(dev)
+    packed.status = torch.full((n,), -1, dtype=torch.int32, device=dev)
+    comp_bytes = int(sum(len(streams[u]) for u in order))
+    algo_bytes = comp_bytes + n * D  # C + D per launch
+    bc = BatchCodec(dev.index or 0)
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        bc.decode(meta, packed, stream=stream)
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    # parity gate on the bench data: every chunk bit-exact
+    st = packed.status.cpu().numpy()
+    assert (st == 0).all(), f"{codec}: decode status != Ok for {int((st != 0).sum())} chunks"
+    ref = torch.stack([torch.from_numpy(v.view(np.uint8).copy()) for v in vals]).to(dev)
+    out = dst.view(n, D)
+    idx = torch.tensor(order, device=dev)
+    bad = int((out != ref[idx]).any(dim=1).sum().item())
+    assert bad == 0, f"{codec}: {bad} chunks differ from their input"
+    del ref, pool_dev
+    # timed region
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(steps):
+        step()
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    barrier(world)
+    wall = time.perf_counter() - t0
+    kern_ms = ev0.elapsed_time(ev1) / steps  # one launch per step
+    t_max = sync_max(wall, world, dev)
+    achieved = algo_bytes / (kern_ms * 1e-3) / 1e9
+    res = {
+        "workload": desc_txt, "value": round(world * n * D * steps / t_max / GIB, 3), "unit": "GiB/s",
+        "ms_per_step": round(t_max / steps * 1e3, 3), "batch_per_gpu": n, "chunk_bytes": D,
+        "compressed_bytes_per_gpu": comp_bytes, "ratio": round(n * D / comp_bytes, 3),
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                     "kernel": KERNEL[codec], "kernel_ms": round(kern_ms, 4),
+                     "algorithmic_bytes_per_launch": algo_bytes},
+    }
+    del src, dst, packed
+    torch.cuda.empty_cache()
+    return res, vals, streams
+
+
+def encode_leg(codec, n, steps, warmup, pool, rank, world, dev):
+    """GPU encode throughput (input GiB/s) of `n` chunks per rank."""
+    import torch
+    from zarr_amd.batch import BatchCodec, make_encode_batch
+    meta, gen, desc_txt = workload(codec)
+    vals = [gen(i) for i in range(pool)]
+    D = vals[0].nbytes
+    host = np.concatenate([vals[(rank * n + i) % pool].view(np.uint8) for i in range(n)])
+    elems = torch.from_numpy(host).to(dev)
+    bc = BatchCodec(dev.index or 0)
+    cap = bc.encode_bound(meta, D)
+    desc, dst, out_len, status = make_encode_batch(elems, n, cap, dev)
+    stream = torch.cuda.current_stream(dev)
+    for _ in range(warmup):
+        bc.encode(meta, desc, n, out_len, status, stream=stream)
+    torch.cuda.synchronize()
+    assert (status.cpu().numpy() == 0).all()
+    out_bytes = int(out_len.sum().item())
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        bc.encode(meta, desc, n, out_len, status, stream=stream)
+    torch.cuda.synchronize()
+    barrier(world)
+    t_max = sync_max(time.perf_counter() - t0, world, dev)
+    achieved = (n * D + out_bytes) / (t_max / steps) / 1e9
+    res = {"workload": desc_txt.replace("decode", "encode"), "direction": "encode",
+           "value": round(world * n * D * steps / t_max / GIB, 3), "unit": "GiB/s (input)",
+           "batch_per_gpu": n, "ratio": round(n * D / out_bytes, 3),
+           "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5)}}
+    del elems, dst
+    torch.cuda.empty_cache()
+    return res
 
 
 def main():
@@ -82,11 +250,12 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--codec", default="gzip", choices=["gzip"])
+    ap.add_argument("--codec", default="gzip", choices=["gzip", "lz4", "raw"])
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--pool", type=int, default=64)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extra", action="store_true", help="skip the per_codec legs")
     args = ap.parse_args()
 
     import torch
@@ -99,121 +268,56 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=dev)
 
-    from zarr_amd import ArrayMetadata, Gzip
-    from zarr_amd.batch import BatchCodec
-
     host_threads = max(1, min(16, os.cpu_count() or 1))
-    vals, streams = build_pool(args.codec, args.pool, host_threads)
+    main_res, vals, streams = decode_leg(args.codec, args.batch, args.steps, args.warmup, args.pool,
+                                         rank, world, dev, host_threads)
     D = vals[0].nbytes
-    n = args.batch
-    meta = ArrayMetadata.new([256 * 64, 256 * 64, 4], [256, 256, 4], "<f4", Gzip(6))
-
-    # ---- device-resident inputs: distinct HBM slots for every chunk ----------
-    ALIGN = 256
-    slot = [(len(s) + ALIGN - 1) // ALIGN * ALIGN for s in streams]
-    order = [(rank * n + i) % args.pool for i in range(n)]  # round-robin pool mapping
-    offs = np.zeros(n + 1, np.int64)
-    for i, u in enumerate(order):
-        offs[i + 1] = offs[i] + slot[u]
-    pool_host = [np.frombuffer(s, np.uint8) for s in streams]
-    src = torch.empty(int(offs[-1]), dtype=torch.uint8, device=dev)
-    pool_dev = [torch.from_numpy(p.copy()).to(dev) for p in pool_host]
-    for i, u in enumerate(order):
-        src[offs[i]:offs[i] + len(streams[u])].copy_(pool_dev[u])
-    dst = torch.empty(n * D, dtype=torch.uint8, device=dev)
-    desc = np.zeros((n, 4), np.uint64)
-    for i, u in enumerate(order):
-        desc[i] = (src.data_ptr() + int(offs[i]), len(streams[u]), dst.data_ptr() + i * D, D)
-
-    class P:  # minimal PackedStreams-compatible holder
-        pass
-    packed = P()
-    packed.n = n
-    packed.desc = torch.from_numpy(desc.view(np.int64)).to(dev)
-    packed.status = torch.full((n,), -1, dtype=torch.int32, device=dev)
-    comp_bytes = int(sum(len(streams[u]) for u in order))
-    algo_bytes = comp_bytes + n * D  # C + D per launch
-
-    codec = BatchCodec(local)
-    stream = torch.cuda.current_stream(dev)
-
-    def step():
-        codec.decode(meta, packed, stream=stream)
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-
-    # ---- parity gate on the bench data: every chunk bit-exact --------------------
-    st = packed.status.cpu().numpy()
-    assert (st == 0).all(), f"decode status != Ok for {int((st != 0).sum())} chunks"
-    ref = torch.stack([torch.from_numpy(v.view(np.uint8).copy()) for v in vals]).to(dev)
-    out = dst.view(n, D)
-    idx = torch.tensor(order, device=dev)
-    bad = (out != ref[idx]).any(dim=1).sum().item()
-    assert bad == 0, f"{bad} chunks differ from their input"
-    del ref
-
-    # ---- timed region --------------------------------------------------------------
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    if world > 1:
-        torch.distributed.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for _ in range(args.steps):
-        step()
-    ev1.record(stream)
-    torch.cuda.synchronize()
-    if world > 1:
-        torch.distributed.barrier()
-    wall = time.perf_counter() - t0
-    kern_ms = ev0.elapsed_time(ev1) / args.steps  # one launch per step
-    t_local = wall
-    if world > 1:
-        t = torch.tensor([t_local], dtype=torch.float64, device=dev)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        t_max = float(t.item())
-    else:
-        t_max = t_local
-    ms_per_step = t_max / args.steps * 1e3
-    total_decoded = world * n * D * args.steps
-    value = total_decoded / t_max / GIB
-
-    achieved = algo_bytes / (kern_ms * 1e-3) / 1e9
     result = {
-        "metric": METRIC, "value": round(value, 3), "unit": "GiB/s", "n_gpus": world,
-        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
+        "metric": METRIC, "value": main_res["value"], "unit": "GiB/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": main_res["ms_per_step"],
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
-        "data": "synthetic (SURVEY §8(d) 'quant' f32, zlib-6, flate2 header; 64-chunk pool "
-                "replicated into distinct HBM slots)",
-        "config": {"workload": "C2: gzip f32 256x256x4 (1 MiB) chunks, decode", "codec": args.codec,
-                   "batch_per_gpu": n, "chunk_bytes": D, "compressed_bytes_per_gpu": comp_bytes,
-                   "ratio": round(n * D / comp_bytes, 3), "parallelism": f"chunks round-robin x{world}"},
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
-                     "kernel": "zcg::inflate_par_kernel", "kernel_ms": round(kern_ms, 4),
-                     "algorithmic_bytes_per_launch": algo_bytes},
+        "data": "synthetic (SURVEY §8(d) distributions, seeded; a pool of distinct chunks "
+                "replicated into distinct HBM slots; every chunk gated bit-exact before timing)",
+        "config": {"workload": main_res["workload"], "codec": args.codec,
+                   "batch_per_gpu": main_res["batch_per_gpu"], "chunk_bytes": D,
+                   "compressed_bytes_per_gpu": main_res["compressed_bytes_per_gpu"],
+                   "ratio": main_res["ratio"], "parallelism": f"chunks round-robin x{world}"},
+        "roofline": main_res["roofline"],
     }
+
+    if not args.no_extra:
+        per = {}
+        for c in ("gzip", "lz4", "raw"):
+            if c == args.codec:
+                continue
+            n_c = 4096 if c == "lz4" else 1024
+            r, _, _ = decode_leg(c, n_c, max(3, args.steps // 2), 1, args.pool, rank, world, dev,
+                                 host_threads)
+            per[c] = r
+        per["lz4_encode"] = encode_leg("lz4", 1024, 3, 1, args.pool, rank, world, dev)
+        result["per_codec"] = per
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import zref  # oracle: CPU baseline leg only
+        cid = {"gzip": zref.GZIP, "lz4": zref.LZ4, "raw": zref.RAW}[args.codec]
+        es = {"gzip": 4, "lz4": 2, "raw": 2}[args.codec]
         srcs = [np.frombuffer(s, np.uint8) for s in streams]
         dsts = [np.empty(D, np.uint8) for _ in srcs]
         t0 = time.perf_counter()
         done = 0
         while time.perf_counter() - t0 < args.cpu_seconds:
-            st, _ = zref.decode_batch(zref.GZIP, srcs, D, elem_size=4, threads=host_threads, dsts=dsts)
+            st, _ = zref.decode_batch(cid, srcs, D, elem_size=es, threads=host_threads, dsts=dsts)
             assert (st == 0).all()
             done += len(srcs)
         el = time.perf_counter() - t0
+        lib = {"gzip": "zlib 1.2.11 inflate + flate2 header rules",
+               "lz4": "liblz4 1.9.3 LZ4F (lz4-rs feeding)", "raw": "memcpy"}[args.codec]
         result["cpu_baseline"] = {
             "value": round(done * D / el / GIB, 4), "unit": "GiB/s", "cores": host_threads,
             "kind": "port",
-            "sample": f"{done} decodes of the {len(srcs)}-chunk pool (1 MiB each) by zlib 1.2.11 "
-                      f"inflate + flate2 header rules (oracle/zref.c), {host_threads} threads, "
-                      f"{el:.1f} s"}
+            "sample": f"{done} decodes of the {len(srcs)}-chunk pool (1 MiB each) by {lib} "
+                      f"(oracle/zref.c), {host_threads} threads, {el:.1f} s"}
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

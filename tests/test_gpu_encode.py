@@ -1,0 +1,180 @@
+"""GPU encoders (write_chunk, chunk.rs:306-323) — parity by round trip.
+
+The reference pins encoded bytes only for the doc-spec vectors
+(tests.rs:147-159); everything larger is "parity unpinned" (SURVEY §8c,
+zarrita_compat.rs:101-102).  So: byte-exact on the doc-spec vector, and for
+every other input the GPU stream must (a) decode with the oracle (the same
+liblz4 LZ4F the reference's lz4-rs wraps) to exactly the serialised input,
+(b) carry the lz4-rs frame conventions (lz.rs:81-92: FLG 0x64, BD from the
+effective block size, header checksum, independent blocks, content checksum
+= XXH32 of the content), and (c) decode with our own GPU decoder.
+"""
+import struct
+
+import numpy as np
+import pytest
+
+from golden_util import doc_spec
+from zarr_amd import ArrayMetadata, DefaultChunk, Lz4, SliceDataChunk, ZarrIOError
+
+pytestmark = pytest.mark.gpu
+
+zref = pytest.importorskip("zref")
+
+
+def xxh32(b: bytes) -> int:
+    import xxhash
+    return xxhash.xxh32_intdigest(b)
+
+
+def serialised(data: np.ndarray, dt: str) -> bytes:
+    """write_data's byte stream (chunk.rs:118-140): array byte order, bool 0/1."""
+    if dt == "bool":
+        return data.astype(np.uint8).tobytes()
+    return data.astype(np.dtype(dt)).tobytes()
+
+
+def encode_batch(meta, arrays, cap_extra=0):
+    """zcg_encode_batch over device buffers; returns (status, [bytes])."""
+    import torch
+    from zarr_amd.batch import BatchCodec, make_encode_batch
+    codec = BatchCodec(0)
+    D = arrays[0].nbytes
+    n = len(arrays)
+    host = np.concatenate([a.view(np.uint8).reshape(-1) for a in arrays]) if D else np.zeros(1, np.uint8)
+    elems = torch.from_numpy(host).to("cuda:0")
+    cap = codec.encode_bound(meta, D) + cap_extra
+    desc, dst, out_len, status = make_encode_batch(elems, n, cap, "cuda:0") if D else (None,) * 4
+    if not D:  # zero-byte chunks: descriptors by hand
+        desc, dst, out_len, status = make_encode_batch(torch.zeros(n, dtype=torch.uint8, device="cuda:0"),
+                                                       n, cap, "cuda:0")
+        d = desc.cpu().numpy().view(np.uint64).reshape(n, 4).copy()
+        d[:, 1] = 0
+        desc = torch.from_numpy(d.view(np.int64)).to("cuda:0")
+    codec.encode(meta, desc, n, out_len, status)
+    torch.cuda.synchronize()
+    st = status.cpu().numpy()
+    ol = out_len.cpu().numpy()
+    buf = dst.cpu().numpy().reshape(n, cap)
+    return st, [buf[i, : ol[i]].tobytes() for i in range(n)]
+
+
+def check_lz4_frame(stream: bytes, content: bytes, block_size: int):
+    assert stream[:4] == b"\x04\x22\x4d\x18"
+    flg, bd = stream[4], stream[5]
+    assert flg == 0x64  # version 01 | independent blocks | content checksum
+    eff = 65536 if block_size <= 65536 else 262144 if block_size <= 262144 else \
+        1048576 if block_size <= 1048576 else 4194304
+    assert bd == {65536: 0x40, 262144: 0x50, 1048576: 0x60, 4194304: 0x70}[eff]
+    assert stream[6] == (xxh32(bytes([flg, bd])) >> 8) & 0xFF
+    pos, total = 7, 0
+    while True:
+        (w,) = struct.unpack_from("<I", stream, pos)
+        pos += 4
+        if w == 0:
+            break
+        size = w & 0x7FFFFFFF
+        raw = w >> 31
+        blk = min(eff, len(content) - total)
+        assert size <= (blk if raw else blk - 1)
+        if raw:
+            assert stream[pos:pos + size] == content[total:total + size]
+        total += blk
+        pos += size
+    assert total == len(content)
+    assert struct.unpack_from("<I", stream, pos)[0] == xxh32(content)
+    assert pos + 4 == len(stream)
+
+
+def test_lz4_encode_doc_spec_exact():
+    """tests.rs:147-159 + lz.rs:101-115: byte-identical to the reference vector."""
+    d = doc_spec()
+    meta = ArrayMetadata.new([5, 6, 7], [1, 2, 3], ">i2", Lz4(65536))
+    out = DefaultChunk.write_chunk(meta, SliceDataChunk([0, 0, 0], np.array(d["expected_values"], np.int16)))
+    assert out.hex() == d["encode_expected"]["lz4"]
+
+
+def _data(kind, nbytes, seed=0):
+    rng = np.random.default_rng(seed)
+    if kind == "zeros":
+        return np.zeros(nbytes, np.uint8)
+    if kind == "uniform":
+        return rng.integers(0, 256, nbytes, dtype=np.uint8)
+    if kind == "randwalk":
+        return np.cumsum(rng.integers(-3, 4, nbytes // 2 + 1)).astype("<i2").view(np.uint8)[:nbytes]
+    if kind == "text":
+        return np.frombuffer((b"the quick brown fox jumps over the lazy dog %d\n" * (nbytes // 40 + 2)
+                              )[:nbytes], np.uint8).copy()
+    if kind == "ramp":
+        return (np.arange(nbytes // 2 + 1) % 4096).astype("<i2").view(np.uint8)[:nbytes]
+    if kind == "mixed":  # compressible and incompressible blocks alternate
+        a = rng.integers(0, 256, nbytes, dtype=np.uint8)
+        for s in range(0, nbytes, 131072):
+            a[s:s + 65536] = 7
+        return a
+    raise ValueError(kind)
+
+
+@pytest.mark.parametrize("block", [65536, 262144, 1048576, 4194304])
+@pytest.mark.parametrize("kind", ["zeros", "uniform", "randwalk", "text", "ramp", "mixed"])
+def test_lz4_encode_roundtrip(kind, block):
+    D = 1 << 20
+    arrays = [_data(kind, D, seed=s) for s in range(3)]
+    meta = ArrayMetadata.new([D * 3], [D], "u1", Lz4(block))
+    st, outs = encode_batch(meta, arrays)
+    assert (st == 0).all()
+    for a, s in zip(arrays, outs):
+        content = a.tobytes()
+        check_lz4_frame(s, content, block)
+        rst, dec = zref.decode(zref.LZ4, s, D, 1, False, False)
+        assert rst == zref.OK and dec == content
+        back = DefaultChunk.read_chunk(s, meta, [0], np.uint8).get_data()
+        assert back.tobytes() == content
+    if kind in ("zeros", "text", "ramp"):
+        assert max(len(s) for s in outs) < D // 4  # it does compress
+
+
+@pytest.mark.parametrize("nbytes", [1, 5, 12, 13, 14, 100, 4095, 65535, 65536, 65537, 65536 + 13,
+                                    131072 + 100, 300001])
+def test_lz4_encode_edge_sizes(nbytes):
+    arrays = [_data("text", nbytes, 1), _data("uniform", nbytes, 2), _data("zeros", nbytes)]
+    meta = ArrayMetadata.new([nbytes * 3], [nbytes], "u1", Lz4(65536))
+    st, outs = encode_batch(meta, arrays)
+    assert (st == 0).all()
+    for a, s in zip(arrays, outs):
+        content = a.tobytes()
+        check_lz4_frame(s, content, 65536)
+        rst, dec = zref.decode(zref.LZ4, s, nbytes, 1, False, False)
+        assert rst == zref.OK and dec == content
+
+
+@pytest.mark.parametrize("dt", ["<i2", ">i2", ">f4", "<f8", ">u8", "bool", "i1"])
+def test_lz4_encode_dtypes(dt):
+    """write_data serialises in the array's byte order, bool as 0/1
+    (chunk.rs:118-140,192-206); the GPU encoder applies that transform."""
+    rng = np.random.default_rng(4)
+    n = 200003
+    if dt == "bool":
+        data = rng.integers(0, 2, n).astype(bool)
+    else:
+        data = (np.cumsum(rng.integers(-3, 4, n)) % 100).astype(np.dtype(dt).newbyteorder("="))
+    meta = ArrayMetadata.new([n], [n], dt, Lz4(65536))
+    out = DefaultChunk.write_chunk(meta, SliceDataChunk([0], data))
+    content = serialised(data, dt)
+    check_lz4_frame(out, content, 65536)
+    rst, dec = zref.decode(zref.LZ4, out, len(content), 1, False, False)
+    assert rst == zref.OK and dec == content
+    back = DefaultChunk.read_chunk(out, meta, [0], data.dtype).get_data()
+    assert np.array_equal(back, data)
+
+
+def test_lz4_encode_errors():
+    meta = ArrayMetadata.new([100], [50], "<i4", Lz4(65536))
+    with pytest.raises(ZarrIOError) as e:  # chunk.rs:309-318
+        DefaultChunk.write_chunk(meta, SliceDataChunk([0], np.arange(49, dtype=np.int32)))
+    assert e.value.kind == "InvalidData"
+    # a destination below zcg_encode_bound is refused per chunk
+    D = 65536
+    meta = ArrayMetadata.new([D], [D], "u1", Lz4(65536))
+    st, _ = encode_batch(meta, [_data("uniform", D)], cap_extra=-64)
+    assert st[0] == 5  # ZCG_ERR_OUTPUT_TOO_SMALL

@@ -112,7 +112,7 @@ int32_t zcg_effective_lz4_block_size(int32_t bs) {
 int zcg_codec_on_gpu(int32_t codec, int encode) {
     switch (codec) {
     case ZCG_CODEC_RAW: return 1;
-    case ZCG_CODEC_LZ4: return encode ? 0 : 1;
+    case ZCG_CODEC_LZ4: return 1;
     case ZCG_CODEC_GZIP: return encode ? 0 : 1;
     default: return 0;
     }
@@ -172,6 +172,9 @@ int zcg_encode_batch(zcg_ctx* ctx, const zcg_array* a, const zcg_chunk* d_chunks
     hipError_t e;
     switch (a->compression.codec) {
     case ZCG_CODEC_RAW: e = launch_raw(a, d_chunks, n, d_status, d_out_len, 1, s); break;
+    case ZCG_CODEC_LZ4:
+        e = launch_lz4_encode(a, d_chunks, n, d_out_len, d_status, nullptr, 0, s);
+        break;
     default:
         ctx->err = "codec has no GPU encoder in this build";
         return ZCG_ERR_UNSUPPORTED;
