@@ -9,6 +9,7 @@ liblz4 LZ4F the reference's lz4-rs wraps) to exactly the serialised input,
 effective block size, header checksum, independent blocks, content checksum
 = XXH32 of the content), and (c) decode with our own GPU decoder.
 """
+import os
 import struct
 
 import numpy as np
@@ -178,3 +179,91 @@ def test_lz4_encode_errors():
     meta = ArrayMetadata.new([D], [D], "u1", Lz4(65536))
     st, _ = encode_batch(meta, [_data("uniform", D)], cap_extra=-64)
     assert st[0] == 5  # ZCG_ERR_OUTPUT_TOO_SMALL
+
+
+# ---- gzip (gzip.rs:50-56 -> flate2 GzEncoder, zlib raw deflate) ----------------------
+import zlib  # noqa: E402
+
+from zarr_amd import Gzip  # noqa: E402
+
+
+def check_gzip_member(stream: bytes, content: bytes, level: int):
+    eff = 6 if (level < 0 or level > 9) else level
+    xfl = 2 if eff >= 9 else (4 if eff <= 1 else 0)
+    assert stream[:10] == bytes([0x1F, 0x8B, 8, 0, 0, 0, 0, 0, xfl, 255])
+    crc, isize = struct.unpack_from("<II", stream, len(stream) - 8)
+    assert crc == zlib.crc32(content) and isize == len(content) & 0xFFFFFFFF
+    d = zlib.decompressobj(-15)
+    assert d.decompress(stream[10:-8]) == content and d.eof and not d.unused_data
+
+
+def test_gzip_encode_doc_spec_exact():
+    """tests.rs:147-159 + gzip.rs:66-80: byte-identical to the reference vector."""
+    d = doc_spec()
+    meta = ArrayMetadata.new([5, 6, 7], [1, 2, 3], ">i2", Gzip(-1))
+    out = DefaultChunk.write_chunk(meta, SliceDataChunk([0, 0, 0], np.array(d["expected_values"], np.int16)))
+    assert out.hex() == d["encode_expected"]["gzip"]
+
+
+@pytest.mark.parametrize("level", [0, 1, 4, 6, 9, -1])
+@pytest.mark.parametrize("kind", ["zeros", "uniform", "randwalk", "text", "ramp", "mixed"])
+def test_gzip_encode_roundtrip(kind, level):
+    D = 1 << 20
+    arrays = [_data(kind, D, seed=s) for s in range(2)]
+    meta = ArrayMetadata.new([D * 2], [D], "u1", Gzip(level))
+    st, outs = encode_batch(meta, arrays)
+    assert (st == 0).all()
+    for a, s in zip(arrays, outs):
+        content = a.tobytes()
+        check_gzip_member(s, content, level)
+        rst, dec = zref.decode(zref.GZIP, s, D, 1, False, False)
+        assert rst == zref.OK and dec == content
+        back = DefaultChunk.read_chunk(s, meta, [0], np.uint8).get_data()
+        assert back.tobytes() == content
+        if level != 0 and kind in ("zeros", "text", "ramp", "randwalk"):
+            # compresses within a bounded factor of zlib at the same level
+            ref_len = len(zlib.compress(content, 6 if level < 0 else level))
+            bound = 2.5 if kind == "ramp" else 1.5  # ramp: exact 8 KiB period; zlib hash chains vs our 1-slot buckets
+            assert len(s) <= bound * ref_len + 48 * (D // 16384), (len(s), ref_len)  # + per-block header/sync
+
+
+@pytest.mark.parametrize("nbytes", [1, 2, 3, 4, 5, 100, 16383, 16384, 16385, 32768 + 5, 300001])
+def test_gzip_encode_edge_sizes(nbytes):
+    arrays = [_data("text", nbytes, 1), _data("uniform", nbytes, 2), _data("zeros", nbytes)]
+    meta = ArrayMetadata.new([nbytes * 3], [nbytes], "u1", Gzip(6))
+    st, outs = encode_batch(meta, arrays)
+    assert (st == 0).all()
+    for a, s in zip(arrays, outs):
+        check_gzip_member(s, a.tobytes(), 6)
+
+
+@pytest.mark.parametrize("dt", ["<i2", ">i2", ">f4", "<f8", ">u8", "bool", "i1"])
+def test_gzip_encode_dtypes(dt):
+    rng = np.random.default_rng(5)
+    n = 150001
+    if dt == "bool":
+        data = rng.integers(0, 2, n).astype(bool)
+    else:
+        data = (np.cumsum(rng.integers(-3, 4, n)) % 100).astype(np.dtype(dt).newbyteorder("="))
+    meta = ArrayMetadata.new([n], [n], dt, Gzip(6))
+    out = DefaultChunk.write_chunk(meta, SliceDataChunk([0], data))
+    content = serialised(data, dt)
+    check_gzip_member(out, content, 6)
+    back = DefaultChunk.read_chunk(out, meta, [0], data.dtype).get_data()
+    assert np.array_equal(back, data)
+
+
+def test_gzip_encode_quant_ratio():
+    """C5 data ('quant' f32): report and bound the ratio against zlib-6."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from bench import quant_chunk
+    arrays = [quant_chunk(i).view(np.uint8) for i in range(4)]
+    meta = ArrayMetadata.new([1 << 22], [1 << 20], "u1", Gzip(6))
+    st, outs = encode_batch(meta, arrays)
+    assert (st == 0).all()
+    ours = sum(len(s) for s in outs)
+    ref = sum(len(zlib.compress(a.tobytes(), 6)) for a in arrays)
+    for a, s in zip(arrays, outs):
+        check_gzip_member(s, a.tobytes(), 6)
+    assert ours <= 1.4 * ref, (ours, ref)

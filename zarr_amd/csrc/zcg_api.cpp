@@ -113,7 +113,7 @@ int zcg_codec_on_gpu(int32_t codec, int encode) {
     switch (codec) {
     case ZCG_CODEC_RAW: return 1;
     case ZCG_CODEC_LZ4: return 1;
-    case ZCG_CODEC_GZIP: return encode ? 0 : 1;
+    case ZCG_CODEC_GZIP: return 1;
     default: return 0;
     }
 }
@@ -121,8 +121,8 @@ int zcg_codec_on_gpu(int32_t codec, int encode) {
 uint64_t zcg_encode_bound(const zcg_compression* c, uint64_t n) {
     switch (c->codec) {
     case ZCG_CODEC_RAW: return n;
-    case ZCG_CODEC_GZIP:  // stored-block worst case + header/trailer
-        return n + 5 * (n / 16383 + 1) + 18 + 64;
+    case ZCG_CODEC_GZIP:  // 16 KiB segment slots (stored worst case + sync) + header/trailer
+        return 18 + ((n + 16383) / 16384) * (16384 + 128) + 64;
     case ZCG_CODEC_LZ4: {
         const uint64_t b = (uint64_t)zcg_effective_lz4_block_size(c->lz4_block_size);
         return 15 + (n / b + 1) * (b + 8) + 8;
@@ -174,6 +174,9 @@ int zcg_encode_batch(zcg_ctx* ctx, const zcg_array* a, const zcg_chunk* d_chunks
     case ZCG_CODEC_RAW: e = launch_raw(a, d_chunks, n, d_status, d_out_len, 1, s); break;
     case ZCG_CODEC_LZ4:
         e = launch_lz4_encode(a, d_chunks, n, d_out_len, d_status, nullptr, 0, s);
+        break;
+    case ZCG_CODEC_GZIP:
+        e = launch_deflate(a, d_chunks, n, d_out_len, d_status, nullptr, 0, s);
         break;
     default:
         ctx->err = "codec has no GPU encoder in this build";

@@ -35,7 +35,8 @@ constexpr u32 LE_HDR = 7;           // frame header bytes
 
 struct LzEncLds {
     u8 win[LE_WIN + 64];            // window bytes (+ slack for 4-byte reads)
-    u32 tab[1u << LE_HBITS];        // position + 1 of the latest position per hash, 0 = empty
+    u16 tab[1u << LE_HBITS];        // position + 1 of the latest position per hash, 0 = empty
+                                    // (match starts are < 65536 - 12, so p + 1 fits)
 };
 
 // 4 bytes at LDS window offset p (any alignment).
@@ -106,7 +107,7 @@ __global__ __launch_bounds__(64) void lz4_block_compress(const zcg_chunk* __rest
             }
         }
         for (u32 q = wl + lane; q < wl + 64; q += 64) L.win[q] = 0;
-        for (u32 q = lane; q < (1u << LE_HBITS); q += 64) L.tab[q] = 0;
+        for (u32 q = lane; q < (1u << LE_HBITS) / 2; q += 64) ((u32*)L.tab)[q] = 0;
         __syncthreads();
         // match starts < S - MFLIMIT (block-relative), match ends <= S - LASTLIT
         const u32 mfl = (S - LE_MFLIMIT > wb) ? (S - LE_MFLIMIT - wb) : 0;
@@ -119,13 +120,18 @@ __global__ __launch_bounds__(64) void lz4_block_compress(const zcg_chunk* __rest
             const bool valid = p < mflim && p + 4 <= wl;
             const u32 v = valid ? win_rd32(L.win, p) : 0u;
             const u32 h = (v * 2654435761u) >> (32 - LE_HBITS);
-            const u32 e = valid ? L.tab[h] : 0u;
-            if (valid) atomicMax(&L.tab[h], p + 1);
+            const u32 e = valid ? (u32)L.tab[h] : 0u;
             const u32 ref = e - 1;
             const bool cand = valid && e != 0 && ref < p && win_rd32(L.win, ref) == v;
             const unsigned long long m = __ballot(cand);
+            // insert the positions scanned up to (and including) the chosen
+            // match start, like LZ4's sequential loop; positions after it are
+            // scanned again after the match and must not find themselves.
+            // Same-hash lanes: the store of the highest lane lands; any entry
+            // is only a candidate (verified above), so the stream stays valid.
+            const u32 f = m ? (u32)__builtin_ctzll(m) : 63u;
+            if (valid && lane <= f) L.tab[h] = (u16)(p + 1);
             if (!m) { ip += 64; continue; }
-            const u32 f = (u32)__builtin_ctzll(m);
             u32 mpos = ip + f;
             u32 mref = (u32)__shfl((int)ref, (int)f, 64);
             // backward extension (bounded by the pending literals and the window)
