@@ -235,7 +235,11 @@ def encode_leg(codec, n, steps, warmup, pool, rank, world, dev):
     barrier(world)
     t_max = sync_max(time.perf_counter() - t0, world, dev)
     achieved = (n * D + out_bytes) / (t_max / steps) / 1e9
+    ref_ratio = None
+    if codec == "gzip":  # C5: ratio of the CPU reference library (zlib level 6) on the same pool
+        ref_ratio = round(len(vals) * D / sum(len(gzip_flate2(v.tobytes(), 6)) for v in vals), 3)
     res = {"workload": desc_txt.replace("decode", "encode"), "direction": "encode",
+           "ref_ratio": ref_ratio,
            "value": round(world * n * D * steps / t_max / GIB, 3), "unit": "GiB/s (input)",
            "batch_per_gpu": n, "ratio": round(n * D / out_bytes, 3),
            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
@@ -295,6 +299,7 @@ def main():
                                  host_threads)
             per[c] = r
         per["lz4_encode"] = encode_leg("lz4", 1024, 3, 1, args.pool, rank, world, dev)
+        per["gzip_encode"] = encode_leg("gzip", 512, 2, 1, args.pool, rank, world, dev)  # C5 shape
         result["per_codec"] = per
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -1,19 +1,22 @@
 #!/usr/bin/env python3
-"""Time the GPU LZ4 encoder per data distribution (kernel time via HIP events)."""
-import os, sys, json
+"""Time the GPU encoders per data distribution (kernel time via HIP events),
+with the CPU reference library's ratio on the same data for comparison.
+    python tools/enc_stats.py [n_chunks] [lz4|gzip]"""
+import os, sys, json, zlib
 import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import torch
 from bench import randwalk_chunk, quant_chunk
-from zarr_amd import ArrayMetadata, Lz4
+from zarr_amd import ArrayMetadata, Lz4, Gzip
 from zarr_amd.batch import BatchCodec, make_encode_batch
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 512
+codec = sys.argv[2] if len(sys.argv) > 2 else "lz4"
 D = 1 << 20
 gens = {"zeros": lambda i: np.zeros(D, np.uint8), "uniform": lambda i: np.random.default_rng(i).integers(0, 256, D, dtype=np.uint8),
         "randwalk": lambda i: randwalk_chunk(i).view(np.uint8), "quant": lambda i: quant_chunk(i).view(np.uint8)}
 bc = BatchCodec(0)
-meta = ArrayMetadata.new([D * n], [D], "u1", Lz4(65536))
+meta = ArrayMetadata.new([D * n], [D], "u1", Lz4(65536) if codec == "lz4" else Gzip(6))
 for name, g in gens.items():
     pool = [g(i) for i in range(16)]
     elems = torch.from_numpy(np.concatenate([pool[i % 16] for i in range(n)])).cuda()
@@ -25,5 +28,9 @@ for name, g in gens.items():
     for _ in range(3): bc.encode(meta, desc, n, ol, st)
     e1.record(); torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / 3
-    print(json.dumps({"data": name, "ms": round(ms, 2), "GiBps": round(n * D / ms / 1e-3 / 2**30, 2),
-                      "ratio": round(n * D / float(ol.sum().item()), 3), "ok": bool((st == 0).all().item())}))
+    ref = None
+    if codec == "gzip":
+        ref = round(4 * D / sum(len(zlib.compress(pool[i].tobytes(), 6)) for i in range(4)), 3)
+    print(json.dumps({"codec": codec, "data": name, "ms": round(ms, 2), "GiBps": round(n * D / ms / 1e-3 / 2**30, 2),
+                      "ratio": round(n * D / float(ol.sum().item()), 3), "ref_ratio_zlib6": ref,
+                      "ok": bool((st == 0).all().item())}), flush=True)

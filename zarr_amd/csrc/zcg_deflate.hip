@@ -67,7 +67,8 @@ __device__ __forceinline__ u32 rev_bits(u32 v, u32 n) { return n ? __builtin_bit
 
 struct DefLds {
     u8 win[DF_WIN + 64];
-    u32 tab[1u << DF_HBITS];   // position + 1 of the latest position per hash (0 = empty)
+    u16 t0[1u << DF_HBITS];    // per 3-byte hash: latest position + 1 (0 = empty)
+    u16 t1[1u << DF_HBITS];    // ... and the one before it
     u32 lfreq[288], dfreq[32], cfreq[20];
     u32 lcode[288], dcode[32], ccode[20];  // (length << 16) | bit-reversed code
     u32 ring[DF_RING];
@@ -92,13 +93,20 @@ __device__ __forceinline__ void ring_put(DefLds& L, u32 bp, u32 v, u32 n) {
 }
 
 // Flush complete ring words [*fw, upto) to out (wave-cooperative).
+constexpr u32 DF_OUTCAP = DF_SLOT - 4;   // bytes a segment may write after its length word
+constexpr u32 CTL_ERR = 8;               // L.ctl slot: pass B inconsistency / overrun
+
 __device__ void ring_flush(DefLds& L, u8* out, u32* fw, u32 upto) {
     const u32 lane = lane_id();
     __syncthreads();
     for (u32 w = *fw + lane; w < upto; w += 64) {
         const u32 v = L.ring[w & (DF_RING - 1)];
-        u8* o = out + 4ull * w;
-        o[0] = (u8)v; o[1] = (u8)(v >> 8); o[2] = (u8)(v >> 16); o[3] = (u8)(v >> 24);
+        if (4 * w + 4 <= DF_OUTCAP) {
+            u8* o = out + 4ull * w;
+            o[0] = (u8)v; o[1] = (u8)(v >> 8); o[2] = (u8)(v >> 16); o[3] = (u8)(v >> 24);
+        } else {
+            L.ctl[CTL_ERR] = 1;  // would overrun the slot: the segment falls back to stored
+        }
         L.ring[w & (DF_RING - 1)] = 0;
     }
     *fw = upto;
@@ -211,26 +219,39 @@ struct ParseCfg {
 
 // One pass of the segment parse over window positions [h0, wend).
 // EMIT=false: symbol frequencies.  EMIT=true: bits into the ring (bp, fw).
+__device__ __forceinline__ u32 hash3(u32 v) { return ((v & 0xFFFFFFu) * 2654435761u) >> (32 - DF_HBITS); }
+
+// Insert position p (hash h) at the head of its 2-slot bucket.  Lanes of one
+// instruction that share a bucket resolve in hardware order; every candidate
+// is verified before use, and pass B checks that it only emits coded symbols
+// (else the segment is stored), so the stream never depends on that order.
+__device__ __forceinline__ void ins2(DefLds& L, u32 h, u32 p) {
+    const u16 old = L.t0[h];
+    L.t1[h] = old;
+    L.t0[h] = (u16)(p + 1);
+}
+
+// One pass of the segment parse over window positions [h0, wend).
+// EMIT=false: symbol frequencies.  EMIT=true: bits into the ring (bp, fw).
 template <bool EMIT>
 __device__ void parse_pass(DefLds& L, u32 h0, u32 wend, ParseCfg cfg, u32* bp, u32* fw, u8* out) {
     const u32 lane = lane_id();
-    // fresh table; insert the history positions (no matching)
-    for (u32 q = lane; q < (1u << DF_HBITS); q += 64) L.tab[q] = 0;
-    __syncthreads();
-    for (u32 g = 0; g < h0; g += 64) {
-        const u32 p = g + lane;
-        if (p < h0 && p + 4 <= wend) {
-            const u32* w = (const u32*)L.win;
-            const u32 v = __builtin_amdgcn_alignbit(w[(p >> 2) + 1], w[p >> 2], (p & 3) * 8);
-            atomicMax(&L.tab[(v * 2654435761u) >> (32 - DF_HBITS)], p + 1);
-        }
-    }
-    __syncthreads();
-    u32 ip = h0;
     auto rd32 = [&](u32 p) -> u32 {
         const u32* w = (const u32*)L.win;
         return __builtin_amdgcn_alignbit(w[(p >> 2) + 1], w[p >> 2], (p & 3) * 8);
     };
+    // fresh buckets; insert the history positions (no matching)
+    for (u32 q = lane; q < (1u << DF_HBITS) / 2; q += 64) { ((u32*)L.t0)[q] = 0; ((u32*)L.t1)[q] = 0; }
+    __syncthreads();
+    for (u32 g = 0; g < h0; g += 64) {
+        const u32 p = g + lane;
+        const bool on = p < h0 && p + 3 <= wend;
+        const u32 h = on ? hash3(rd32(p)) : 0u;
+        if (on) ins2(L, h, p);
+        __builtin_amdgcn_wave_barrier();
+    }
+    __syncthreads();
+    u32 ip = h0;
     // literal emission for positions [a, b) (b - a <= 64)
     auto literals = [&](u32 a, u32 b) {
         const u32 p = a + lane;
@@ -242,8 +263,8 @@ __device__ void parse_pass(DefLds& L, u32 h0, u32 wend, ParseCfg cfg, u32* bp, u
         }
         const u32 cw = on ? L.lcode[byte] : 0u;
         const u32 nb = cw >> 16;
-        // wave exclusive scan of code lengths
-        u32 x = nb;
+        if (on && nb == 0) L.ctl[CTL_ERR] = 1;
+        u32 x = nb;  // wave exclusive scan of code lengths
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1) {
             const u32 y = __shfl_up(x, d, 64);
@@ -253,8 +274,8 @@ __device__ void parse_pass(DefLds& L, u32 h0, u32 wend, ParseCfg cfg, u32* bp, u
         if (on) ring_put(L, *bp + x - nb, cw & 0xFFFF, nb);
         *bp += tot;
     };
-    auto match_len = [&](u32 p, u32 r) -> u32 {  // verified 4 bytes; extend to <= 258, < wend
-        u32 e = p + 4;
+    auto match_len = [&](u32 p, u32 r) -> u32 {  // 3 bytes verified; extend to <= 258, < wend
+        u32 e = p + 3;
         const u32 lim = (p + 258 < wend) ? p + 258 : wend;
         for (;;) {
             const u32 x = e + lane;
@@ -266,62 +287,125 @@ __device__ void parse_pass(DefLds& L, u32 h0, u32 wend, ParseCfg cfg, u32* bp, u
         }
         return e - p;
     };
+    // best (length, ref) of lane `l`'s two candidates (wave-uniform call)
+    auto best_of = [&](u32 l, u32 r0, u32 r1, u32 ok0, u32 ok1, u32* blen, u32* bref) {
+        const u32 p = ip + l;
+        const u32 a0 = (u32)__shfl((int)r0, (int)l, 64), a1 = (u32)__shfl((int)r1, (int)l, 64);
+        const u32 k0 = (u32)__shfl((int)ok0, (int)l, 64), k1 = (u32)__shfl((int)ok1, (int)l, 64);
+        u32 bl = 0, br = 0;
+        if (k0) { const u32 ln = match_len(p, a0); bl = ln; br = a0; }
+        if (k1) {
+            const u32 ln = match_len(p, a1);
+            if (ln > bl) { bl = ln; br = a1; }
+        }
+        if (bl == 3 && p - br > 4096) bl = 0;  // zlib TOO_FAR: a far 3-byte match does not pay
+        *blen = bl;
+        *bref = br;
+    };
+    constexpr u32 LCAP = 32;  // per-lane match measurement cap
+    // lane-local match length from 3 verified bytes, capped at min(LCAP, wend - p)
+    auto ext = [&](u32 p, u32 r) -> u32 {
+        const u32 lim = (wend - p) < LCAP ? (wend - p) : LCAP;
+        u32 k = 3;
+        while (k < lim) {
+            const u32 x = rd32(p + k) ^ rd32(r + k);
+            if (x) { k += (u32)__builtin_ctz(x) >> 3; break; }
+            k += 4;
+        }
+        return k < lim ? k : lim;
+    };
     while (ip < wend) {
-        // keep the ring from wrapping: every iteration adds < 2 Kbit
+        // keep the ring from wrapping: a group adds < 2 Kbit
         if (EMIT && (*bp >> 5) >= *fw + DF_FLUSH) ring_flush(L, out, fw, *bp >> 5);
+        const u32 gend = (wend - ip) < 64 ? (wend - ip) : 64u;  // positions of this group
         const u32 p = ip + lane;
-        const bool valid = p + 4 <= wend;
+        const bool valid = lane < gend && p + 3 <= wend;
         const u32 v = valid ? rd32(p) : 0u;
-        const u32 h = (v * 2654435761u) >> (32 - DF_HBITS);
-        const u32 e = valid ? L.tab[h] : 0u;
-        const u32 ref = e - 1;
-        const bool cand = valid && e != 0 && ref < p && p - ref <= DF_HIST && rd32(ref) == v;
-        const unsigned long long m = __ballot(cand);
-        u32 f = m ? (u32)__builtin_ctzll(m) : 64u;
-        // lazy: a longer match at the next position wins (the first becomes a literal)
-        u32 mlen = 0, mref = 0;
-        if (m) {
-            mref = (u32)__shfl((int)ref, (int)f, 64);
-            mlen = match_len(ip + f, mref);
-            if (cfg.lazy && f + 1 < 64 && ((m >> (f + 1)) & 1ull) && mlen < 258) {
-                const u32 r2 = (u32)__shfl((int)ref, (int)(f + 1), 64);
-                const u32 l2 = match_len(ip + f + 1, r2);
-                if (l2 > mlen) { f = f + 1; mref = r2; mlen = l2; }
+        const u32 h = hash3(v);
+        const u32 e0 = valid ? (u32)L.t0[h] : 0u, e1 = valid ? (u32)L.t1[h] : 0u;
+        const u32 r0 = e0 - 1, r1 = e1 - 1;
+        auto cand_len = [&](u32 e, u32 r) -> u32 {
+            if (!valid || e == 0 || r >= p || p - r > DF_HIST) return 0u;
+            if (((rd32(r) ^ v) & 0xFFFFFFu) != 0) return 0u;
+            const u32 ln = ext(p, r);
+            return (ln == 3 && p - r > 4096) ? 0u : ln;  // zlib TOO_FAR
+        };
+        const u32 l0 = cand_len(e0, r0), l1 = cand_len(e1, r1);
+        u32 bl = l1 > l0 ? l1 : l0;                  // ties: the nearer (t0)
+        u32 br = l1 > l0 ? r1 : r0;
+        // positions of this group are not in the buckets yet: try the nearest
+        // of a few short distances inside the group (periodic element data)
+        {
+            u32 dn = 0;
+#pragma unroll
+            for (u32 dd = 1; dd <= 32; dd <<= 1) {
+                const u32 vd = (u32)__shfl_up((int)v, dd, 64);
+                if (!dn && lane >= dd && ((vd ^ v) & 0xFFFFFFu) == 0) dn = dd;
+            }
+            if (valid && dn) {
+                const u32 ln = ext(p, p - dn);
+                if (ln > bl) { bl = ln; br = p - dn; }
             }
         }
-        const u32 last = m ? f : 63u;  // insert scanned positions up to the match start
-        if (valid && lane <= last) atomicMax(&L.tab[h], p + 1);
-        const u32 lit_end = m ? ip + f : ((ip + 64 < wend) ? ip + 64 : wend);
-        literals(ip, lit_end);
-        if (!m) { ip = lit_end; continue; }
-        const u32 mpos = ip + f;
-        const u32 d = mpos - mref;
-        const u32 lc = len_code(mlen), dc = dist_code(d);
-        if (!EMIT) {
-            if (lane == 0) { atomicAdd(&L.lfreq[257 + lc], 1u); atomicAdd(&L.dfreq[dc], 1u); }
-        } else {
-            if (lane == 0) {
-                u32 b = *bp;
-                const u32 lcw = L.lcode[257 + lc];
-                ring_put(L, b, lcw & 0xFFFF, lcw >> 16); b += lcw >> 16;
-                ring_put(L, b, mlen - d_len_base[lc], d_len_extra[lc]); b += d_len_extra[lc];
-                const u32 dcw = L.dcode[dc];
-                ring_put(L, b, dcw & 0xFFFF, dcw >> 16); b += dcw >> 16;
-                ring_put(L, b, d - d_dist_base[dc], d_dist_extra[dc]); b += d_dist_extra[dc];
-                L.ctl[0] = b;
+        const unsigned long long mask = __ballot(bl >= 3);
+        if (valid) ins2(L, h, p);  // all lookups of the group are done
+        __builtin_amdgcn_wave_barrier();
+        // walk the group: successive greedy (lazy) matches from the lane lengths
+        u32 pos = 0;
+        while (pos < gend) {
+            const unsigned long long mm = mask & (~0ull << pos);
+            if (!mm) { literals(ip + pos, ip + gend); pos = gend; break; }
+            u32 f = (u32)__builtin_ctzll(mm);
+            u32 mlen = (u32)__shfl((int)bl, (int)f, 64), mref = (u32)__shfl((int)br, (int)f, 64);
+            if (cfg.lazy && mlen < 32 && f + 1 < gend && ((mask >> (f + 1)) & 1ull)) {
+                const u32 l2 = (u32)__shfl((int)bl, (int)(f + 1), 64);
+                if (l2 > mlen) { f = f + 1; mlen = l2; mref = (u32)__shfl((int)br, (int)f, 64); }
             }
-            __syncthreads();
-            *bp = L.ctl[0];
+            const u32 mpos = ip + f;
+            if (mlen == LCAP) {  // measured to the cap: extend wave-parallel up to 258
+                u32 e = mpos + LCAP;
+                const u32 lim = (mpos + 258 < wend) ? mpos + 258 : wend;
+                const u32 d = mpos - mref;
+                for (;;) {
+                    const u32 x = e + lane;
+                    const bool okb = x < lim && L.win[x] == L.win[x - d];
+                    const unsigned long long bm = __ballot(!okb);
+                    const u32 run = bm ? (u32)__builtin_ctzll(bm) : 64u;
+                    e += run;
+                    if (run < 64) break;
+                }
+                mlen = e - mpos;
+            }
+            if (f > pos) literals(ip + pos, ip + f);
+            const u32 d = mpos - mref;
+            const u32 lc = len_code(mlen), dc = dist_code(d);
+            if (!EMIT) {
+                if (lane == 0) { atomicAdd(&L.lfreq[257 + lc], 1u); atomicAdd(&L.dfreq[dc], 1u); }
+            } else {
+                const u32 lcw = L.lcode[257 + lc], dcw = L.dcode[dc];  // uniform reads
+                const u32 nl = lcw >> 16, nd = dcw >> 16;
+                const u32 el = d_len_extra[lc], ed = d_dist_extra[dc];
+                if (lane == 0) {
+                    if (nl == 0 || nd == 0) L.ctl[CTL_ERR] = 1;
+                    u32 b = *bp;
+                    ring_put(L, b, lcw & 0xFFFF, nl); b += nl;
+                    ring_put(L, b, mlen - d_len_base[lc], el); b += el;
+                    ring_put(L, b, dcw & 0xFFFF, nd); b += nd;
+                    ring_put(L, b, d - d_dist_base[dc], ed);
+                }
+                *bp += nl + el + nd + ed;
+            }
+            pos = f + mlen;
+            if (pos > gend) {  // the match runs past the group: insert its last two positions
+                const u32 endp = ip + pos;
+                if (lane < 2) {
+                    const u32 q = endp - 2 + lane;
+                    if (q + 3 <= wend && q >= ip + gend) ins2(L, hash3(rd32(q)), q);
+                }
+                __builtin_amdgcn_wave_barrier();
+            }
         }
-        {   // insert positions inside the match: all of them for short matches at
-            // level >= 4 (zlib max_insert_length), else only the last two (like
-            // LZ4's ip-2): one slot per hash bucket, so inserting every position
-            // of long matches would evict the older candidates periodic data needs
-            const u32 from = (cfg.insert && mlen <= 16) ? mpos + 1 : (mlen > 2 ? mpos + mlen - 2 : mpos + 1);
-            for (u32 q = from + lane; q < mpos + mlen; q += 64)
-                if (q + 4 <= wend) atomicMax(&L.tab[(rd32(q) * 2654435761u) >> (32 - DF_HBITS)], q + 1);
-        }
-        ip = mpos + mlen;
+        ip += pos;
     }
     if (EMIT && (*bp >> 5) >= *fw + DF_FLUSH) ring_flush(L, out, fw, *bp >> 5);
 }
@@ -483,6 +567,8 @@ __global__ __launch_bounds__(64) void deflate_segment(const zcg_chunk* __restric
     bp = L.ctl[0];
     // the header may exceed a flush unit only in theory (< 400 bytes); flush if needed
     if ((bp >> 5) >= fw + DF_FLUSH) ring_flush(L, out, &fw, bp >> 5);
+    if (lane == 0) L.ctl[CTL_ERR] = 0;
+    __syncthreads();
     const ParseCfg cfg{level >= 4, level >= 4};
     parse_pass<true>(L, hist, wend, cfg, &bp, &fw, out);
     if (lane == 0) {
@@ -499,6 +585,16 @@ __global__ __launch_bounds__(64) void deflate_segment(const zcg_chunk* __restric
     if (!final_seg && lane == 0) ring_put(L, bp - 16, 0xFFFFu, 16);
     __syncthreads();
     ring_flush(L, out, &fw, (bp + 31) >> 5);
+    if (L.ctl[CTL_ERR]) {  // inconsistent or oversized: store the segment instead
+        if (lane == 0) {
+            out[0] = final_seg ? 1 : 0;
+            out[1] = (u8)S; out[2] = (u8)(S >> 8);
+            out[3] = (u8)~S; out[4] = (u8)(~S >> 8);
+        }
+        for (u32 q = lane; q < S; q += 64) out[5 + q] = L.win[hist + q];
+        if (lane == 0) { const u32 len = 5 + S; slot[0] = (u8)len; slot[1] = (u8)(len >> 8); slot[2] = (u8)(len >> 16); slot[3] = (u8)(len >> 24); }
+        return;
+    }
     if (lane == 0) { slot[0] = (u8)nbytes; slot[1] = (u8)(nbytes >> 8); slot[2] = (u8)(nbytes >> 16); slot[3] = (u8)(nbytes >> 24); }
 }
 
