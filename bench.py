@@ -43,7 +43,8 @@ sys.path.insert(0, ROOT)
 METRIC = "decoded chunk GiB/s (device-resident) per CompressionType at 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
 GIB = float(1 << 30)
-KERNEL = {"gzip": "zcg::inflate_par_kernel", "lz4": "zcg::lz4_decode_kernel", "raw": "zcg::raw_kernel"}
+KERNEL = {"gzip": "zcg::inflate_par_kernel", "lz4": "zcg::lz4_decode_kernel", "raw": "zcg::raw_kernel",
+          "xz": "zcg::xz_decode_kernel<7990u>"}
 
 
 def quant_chunk(idx: int) -> np.ndarray:
@@ -78,6 +79,10 @@ class _Batch:  # PackedStreams-shaped holder for BatchCodec.decode
 def workload(codec: str):
     """(meta, value generator, description) of each codec's bench shape."""
     from zarr_amd import ArrayMetadata, Gzip, Lz4, Raw
+    from zarr_amd.compression import Xz
+    if codec == "xz":  # xz2 default preset 6 on the C2 data shape
+        meta = ArrayMetadata.new([256 * 64, 256 * 64, 4], [256, 256, 4], "<f4", Xz(6))
+        return meta, quant_chunk, "xz preset 6 f32 256x256x4 (1 MiB) chunks, decode"
     if codec == "gzip":
         meta = ArrayMetadata.new([256 * 64, 256 * 64, 4], [256, 256, 4], "<f4", Gzip(6))
         return meta, quant_chunk, "C2: gzip f32 256x256x4 (1 MiB) chunks, decode"
@@ -113,6 +118,11 @@ def build_pool(codec, meta, gen, pool, threads, dev):
             streams = list(ex.map(lambda a: gzip_flate2(a.tobytes(), 6), vals))
     elif codec == "lz4":
         streams = gpu_encode_pool(meta, vals, dev)
+    elif codec == "xz":
+        import lzma
+        with ThreadPoolExecutor(threads) as ex:  # xz2 XzEncoder = easy encoder, preset 6, CRC64
+            streams = list(ex.map(lambda a: lzma.compress(a.tobytes(), format=lzma.FORMAT_XZ,
+                                                          check=lzma.CHECK_CRC64, preset=6), vals))
     else:
         streams = [v.tobytes() for v in vals]
     return vals, streams
@@ -249,12 +259,39 @@ def encode_leg(codec, n, steps, warmup, pool, rank, world, dev):
     return res
 
 
+CPU_LIB = {"gzip": "zlib 1.2.11 inflate + flate2 header rules",
+           "lz4": "liblz4 1.9.3 LZ4F (lz4-rs feeding)", "raw": "memcpy",
+           "xz": "liblzma 5.2.5 stream decoder (xz2 feeding)",
+           "bzip2": "libbz2 1.0.8 (bzip2-rs feeding)"}
+
+
+def cpu_leg(codec, streams, D, seconds, threads):
+    """The oracle (reference C codec libraries, oracle/zref.c) decoding the
+    same pool on host threads for about `seconds` — cpu_baseline only."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import zref  # oracle: CPU baseline leg only
+    cid = {"gzip": zref.GZIP, "lz4": zref.LZ4, "raw": zref.RAW, "xz": zref.XZ, "bzip2": zref.BZIP2}[codec]
+    es = {"gzip": 4, "lz4": 2, "raw": 2, "xz": 4, "bzip2": 4}[codec]
+    srcs = [np.frombuffer(s, np.uint8) for s in streams]
+    dsts = [np.empty(D, np.uint8) for _ in srcs]
+    t0 = time.perf_counter()
+    done = 0
+    while time.perf_counter() - t0 < seconds:
+        st, _ = zref.decode_batch(cid, srcs, D, elem_size=es, threads=threads, dsts=dsts)
+        assert (st == 0).all()
+        done += len(srcs)
+    el = time.perf_counter() - t0
+    return {"value": round(done * D / el / GIB, 4), "unit": "GiB/s", "cores": threads, "kind": "port",
+            "sample": f"{done} decodes of the {len(srcs)}-chunk pool (1 MiB each) by {CPU_LIB[codec]} "
+                      f"(oracle/zref.c), {threads} threads, {el:.1f} s"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--codec", default="gzip", choices=["gzip", "lz4", "raw"])
+    ap.add_argument("--codec", default="gzip", choices=["gzip", "lz4", "raw", "xz"])
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--pool", type=int, default=64)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -291,38 +328,21 @@ def main():
 
     if not args.no_extra:
         per = {}
-        for c in ("gzip", "lz4", "raw"):
+        for c in ("gzip", "lz4", "raw", "xz"):
             if c == args.codec:
                 continue
-            n_c = 4096 if c == "lz4" else 1024
-            r, _, _ = decode_leg(c, n_c, max(3, args.steps // 2), 1, args.pool, rank, world, dev,
-                                 host_threads)
+            n_c = {"lz4": 4096, "xz": 2048}.get(c, 1024)
+            r, _, s_c = decode_leg(c, n_c, 2 if c == "xz" else max(3, args.steps // 2), 1,
+                                   args.pool, rank, world, dev, host_threads)
+            if rank == 0 and world == 1 and not args.no_cpu_baseline and c != "raw":
+                r["cpu_baseline"] = cpu_leg(c, s_c, r["chunk_bytes"], 3.0, host_threads)
             per[c] = r
         per["lz4_encode"] = encode_leg("lz4", 1024, 3, 1, args.pool, rank, world, dev)
         per["gzip_encode"] = encode_leg("gzip", 512, 2, 1, args.pool, rank, world, dev)  # C5 shape
         result["per_codec"] = per
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        import zref  # oracle: CPU baseline leg only
-        cid = {"gzip": zref.GZIP, "lz4": zref.LZ4, "raw": zref.RAW}[args.codec]
-        es = {"gzip": 4, "lz4": 2, "raw": 2}[args.codec]
-        srcs = [np.frombuffer(s, np.uint8) for s in streams]
-        dsts = [np.empty(D, np.uint8) for _ in srcs]
-        t0 = time.perf_counter()
-        done = 0
-        while time.perf_counter() - t0 < args.cpu_seconds:
-            st, _ = zref.decode_batch(cid, srcs, D, elem_size=es, threads=host_threads, dsts=dsts)
-            assert (st == 0).all()
-            done += len(srcs)
-        el = time.perf_counter() - t0
-        lib = {"gzip": "zlib 1.2.11 inflate + flate2 header rules",
-               "lz4": "liblz4 1.9.3 LZ4F (lz4-rs feeding)", "raw": "memcpy"}[args.codec]
-        result["cpu_baseline"] = {
-            "value": round(done * D / el / GIB, 4), "unit": "GiB/s", "cores": host_threads,
-            "kind": "port",
-            "sample": f"{done} decodes of the {len(srcs)}-chunk pool (1 MiB each) by {lib} "
-                      f"(oracle/zref.c), {host_threads} threads, {el:.1f} s"}
+        result["cpu_baseline"] = cpu_leg(args.codec, streams, D, args.cpu_seconds, host_threads)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

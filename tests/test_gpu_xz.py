@@ -1,0 +1,94 @@
+"""GPU parity of the Xz decoder (zcg_xz.hip) against the oracle.
+
+The reference decodes Xz with xz2's read::XzDecoder (src/compression/xz.rs:
+34-43) = liblzma 5.2's stream decoder; the oracle runs that same liblzma
+with the same 32 KiB input windows.  Streams come from the oracle encoder
+(xz2 XzEncoder = lzma_easy_encoder(preset, CRC64), xz.rs:34-43) and from
+Python's lzma (the same liblzma) for structures xz2 never writes but
+liblzma decodes: other checks, lc/lp/pb, multiple LZMA2 chunks, stored
+(uncompressed) chunks.  The same decode core is fuzzed on the CPU in
+tests/test_hostcore.py; here the GPU kernel runs the corruption sweeps in
+batches.
+"""
+import lzma
+
+import numpy as np
+import pytest
+
+import zref
+from test_gpu_parity import DATASETS, check, check_many, rw
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("data", list(DATASETS))
+@pytest.mark.parametrize("preset", [0, 6, 9])
+def test_xz_large(data, preset):
+    payload = DATASETS[data]()
+    st, s = zref.encode(zref.XZ, preset, np.frombuffer(payload, np.uint8))
+    assert st == zref.OK
+    for D in (len(payload), len(payload) // 3 + 7):
+        check("xz", s, "u1", D, param=preset)
+
+
+@pytest.mark.parametrize("dt", ["<i2", ">i2", ">f4", ">u8", "bool", "i1"])
+def test_xz_transform(dt):
+    from golden_util import dtype_info
+    es = dtype_info(dt)[0]
+    n = 70001
+    raw = rw(n * es // 2 + 1).tobytes()[: n * es]
+    st, s = zref.encode(zref.XZ, 6, np.frombuffer(raw, np.uint8))
+    check("xz", s, dt, n)
+
+
+@pytest.mark.parametrize("check_id", [lzma.CHECK_NONE, lzma.CHECK_CRC32, lzma.CHECK_CRC64])
+@pytest.mark.parametrize("lclppb", [(3, 0, 2), (0, 4, 0), (4, 0, 4), (1, 3, 1), (2, 2, 3)])
+def test_xz_liblzma_variants(check_id, lclppb):
+    lc, lp, pb = lclppb
+    payload = rw(200000, seed=lc * 7 + lp).tobytes()
+    filt = [{"id": lzma.FILTER_LZMA2, "preset": 6, "lc": lc, "lp": lp, "pb": pb}]
+    s = lzma.compress(payload, format=lzma.FORMAT_XZ, check=check_id, filters=filt)
+    for D in (len(payload), 123457):
+        check("xz", s, "u1", D)
+
+
+def test_xz_uncompressed_chunks_and_many_lzma_chunks():
+    rng = np.random.default_rng(3)
+    noise = rng.integers(0, 256, 300000, dtype=np.uint8).tobytes()   # stored LZMA2 chunks
+    mixed = noise[:100000] + bytes(200000) + noise[100000:200000]
+    for payload in (noise, mixed):
+        s = lzma.compress(payload, format=lzma.FORMAT_XZ, check=lzma.CHECK_CRC64, preset=6)
+        for D in (len(payload), 65536, 65537, 250001):
+            check("xz", s, "u1", D)
+
+
+def test_xz_corruption_sweep():
+    """Truncations and byte corruptions everywhere, including after byte N
+    (liblzma validates what its current input window holds)."""
+    rng = np.random.default_rng(17)
+    for k, payload in enumerate([rw(30000, seed=1).tobytes(), bytes(50000),
+                                 rng.integers(0, 256, 40000, dtype=np.uint8).tobytes()]):
+        s = lzma.compress(payload, format=lzma.FORMAT_XZ, check=(lzma.CHECK_CRC64, lzma.CHECK_CRC32)[k % 2],
+                          preset=6)
+        for D in (len(payload), len(payload) // 2):
+            streams = [s[:int(t)] for t in rng.integers(0, len(s), 64)]
+            for _ in range(448):
+                b = bytearray(s)
+                if rng.random() < 0.3:
+                    p = len(b) - 1 - int(rng.integers(0, min(len(b), 64)))
+                else:
+                    p = int(rng.integers(0, len(b)))
+                b[p] ^= int(rng.integers(1, 256))
+                streams.append(bytes(b))
+            check_many("xz", streams, "u1", D)
+
+
+def test_xz_unsupported_filter_chain_fails_loudly():
+    from zarr_amd import ArrayMetadata, DefaultChunk, NativeUnavailable
+    from zarr_amd.compression import Xz
+    payload = rw(5000).tobytes()
+    s = lzma.compress(payload, format=lzma.FORMAT_XZ,
+                      filters=[{"id": lzma.FILTER_DELTA, "dist": 2}, {"id": lzma.FILTER_LZMA2}])
+    meta = ArrayMetadata.new([len(payload)], [len(payload)], "u1", Xz(6))
+    with pytest.raises(NativeUnavailable):
+        DefaultChunk.read_chunk(s, meta, [0], np.uint8)

@@ -1,0 +1,94 @@
+"""CPU fuzzing of the device decode cores (zarr_amd/csrc/*_core.h, compiled
+for the host by tests/hostcore) against the oracle.  The GPU kernels run the
+same core source; this is where the long corruption sweeps run, because a
+host decode costs microseconds.  TEST INFRASTRUCTURE ONLY."""
+import ctypes
+import lzma
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import zref
+
+HERE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "hostcore")
+_H = None
+
+
+def host():
+    global _H
+    if _H is None:
+        subprocess.run(["make", "-s", "-C", HERE], check=True)
+        _H = ctypes.CDLL(os.path.join(HERE, "libzcg_host.so"))
+        _H.zh_xz_decode.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64]
+        _H.zh_xz_decode.restype = ctypes.c_int
+    return _H
+
+
+def host_xz(s: bytes, D: int):
+    out = np.zeros(max(D, 1), np.uint8)
+    a = np.frombuffer(s, np.uint8) if s else np.zeros(1, np.uint8)
+    st = host().zh_xz_decode(a.ctypes.data, len(s), out.ctypes.data, D)
+    return st, out[:D].tobytes()
+
+
+def same(s, D):
+    r1 = zref.decode(zref.XZ, s, D)
+    r2 = host_xz(s, D)
+    assert r1[0] == r2[0], (r1[0], r2[0], D, len(s))
+    if r1[0] == zref.OK:
+        assert r1[1] == r2[1]
+
+
+def _data(rng, k, n):
+    if k == 0:
+        return rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+    if k == 1:
+        return np.cumsum(rng.integers(-3, 4, n // 2 + 1)).astype("<i2").tobytes()[:n]
+    if k == 2:
+        return bytes(n)
+    return (np.arange(n) % 251).astype(np.uint8).tobytes()
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_xz_core_fuzz_vs_liblzma(seed):
+    rng = np.random.default_rng(seed)
+    checks = [lzma.CHECK_CRC64, lzma.CHECK_CRC32, lzma.CHECK_NONE]
+    for _ in range(120):
+        k = int(rng.integers(0, 4))
+        n = int(rng.choice([1, 7, 300, 4000, 40000, 120000]))
+        raw = _data(rng, k, n)
+        lc = int(rng.integers(0, 5))
+        lp = int(rng.integers(0, 5 - lc))
+        filt = [{"id": lzma.FILTER_LZMA2, "preset": int(rng.integers(0, 10)), "lc": lc, "lp": lp,
+                 "pb": int(rng.integers(0, 5))}]
+        s = lzma.compress(raw, format=lzma.FORMAT_XZ, check=checks[int(rng.integers(0, 3))], filters=filt)
+        Ds = [len(raw), max(1, len(raw) // 3), len(raw) + 1]
+        for D in Ds:
+            same(s, D)
+        for t in rng.integers(0, len(s), 4):
+            same(s[:int(t)], len(raw))
+        for _ in range(20):
+            b = bytearray(s)
+            if rng.random() < 0.3:
+                p = len(b) - 1 - int(rng.integers(0, min(len(b), 48)))
+            else:
+                p = int(rng.integers(0, len(b)))
+            b[p] ^= 1 << int(rng.integers(0, 8)) if rng.random() < 0.5 else int(rng.integers(1, 256))
+            same(bytes(b), Ds[int(rng.integers(0, 3))])
+
+
+def test_xz_core_reference_vectors():
+    """doc-spec vector (xz.rs:52-75) and the oracle's xz2-style encodes."""
+    from golden_util import doc_spec
+    d = doc_spec()
+    s = bytes.fromhex(d["chunks"]["xz"]["hex"])
+    st, out = host_xz(s, 12)
+    assert st == 0
+    assert np.frombuffer(out, ">i2").tolist() == d["expected_values"]
+    for preset in range(10):
+        v = np.cumsum(np.random.default_rng(preset).integers(-3, 4, 50000)).astype("<i2")
+        st, enc = zref.encode(zref.XZ, preset, v)
+        assert st == 0
+        same(enc, v.nbytes)

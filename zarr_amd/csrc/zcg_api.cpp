@@ -114,6 +114,7 @@ int zcg_codec_on_gpu(int32_t codec, int encode) {
     case ZCG_CODEC_RAW: return 1;
     case ZCG_CODEC_LZ4: return 1;
     case ZCG_CODEC_GZIP: return 1;
+    case ZCG_CODEC_XZ: return encode ? 0 : 1;
     default: return 0;
     }
 }
@@ -152,8 +153,8 @@ int zcg_decode_batch(zcg_ctx* ctx, const zcg_array* a, const zcg_chunk* d_chunks
                 ? launch_inflate(a, d_chunks, n, d_status, s)
                 : launch_inflate_par(a, d_chunks, n, d_status, s);
         break;
+    case ZCG_CODEC_XZ: e = launch_xz_decode(a, d_chunks, n, d_status, nullptr, 0, s); break;
     case ZCG_CODEC_BZIP2:
-    case ZCG_CODEC_XZ:
         ctx->err = "codec has no GPU decoder in this build";
         return ZCG_ERR_UNSUPPORTED;
     default: return ZCG_ERR_INVALID_INPUT;

@@ -94,6 +94,24 @@ __device__ __forceinline__ u32 ld16le(const u8* p) { return *(const u16_ua*)p; }
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
+// In-place element transform of a decoded chunk by the whole wave.
+__device__ inline void wave_transform(u8* dst, u64 D, const DType& t) {
+    const int lane = lane_id();
+    const bool al = (((uintptr_t)dst) & 15) == 0;
+    for (u64 p = (u64)lane * 16; p < D; p += 64 * 16) {
+        if (p + 16 <= D) {
+            u32x4 v = al ? *(u32x4*)(dst + p) : ld16(dst + p);
+            v = transform16(v, t);
+            if (al) *(u32x4*)(dst + p) = v; else st16(dst + p, v);
+        } else {
+            // tail shorter than 16 bytes: whole elements only (D % es == 0)
+            u8 tmp[16];
+            for (u64 q = p; q < D; q++) tmp[q - p] = dst[q];
+            for (u64 q = p; q < D; q++) dst[swap_pos(q, t)] = norm_byte(tmp[q - p], t);
+        }
+    }
+}
+
 // ---- XXH32 (LZ4 frame header / block / content checksums) --------------
 constexpr u32 XXH_P1 = 2654435761u;
 constexpr u32 XXH_P2 = 2246822519u;

@@ -218,24 +218,6 @@ __device__ int lz4_frame_serial(const u8* s, u64 n, u8* dst, u64 D, u32 vflags) 
     return ZCG_OK;
 }
 
-// In-place element transform of a decoded chunk by the whole wave.
-__device__ void wave_transform(u8* dst, u64 D, const DType& t) {
-    const int lane = lane_id();
-    const bool al = (((uintptr_t)dst) & 15) == 0;
-    for (u64 p = (u64)lane * 16; p < D; p += 64 * 16) {
-        if (p + 16 <= D) {
-            u32x4 v = al ? *(u32x4*)(dst + p) : ld16(dst + p);
-            v = transform16(v, t);
-            if (al) *(u32x4*)(dst + p) = v; else st16(dst + p, v);
-        } else {
-            // tail shorter than 16 bytes: whole elements only (D % es == 0)
-            u8 tmp[16];
-            for (u64 q = p; q < D; q++) tmp[q - p] = dst[q];
-            for (u64 q = p; q < D; q++) dst[swap_pos(q, t)] = norm_byte(tmp[q - p], t);
-        }
-    }
-}
-
 __global__ __launch_bounds__(64) void lz4_decode_kernel(const zcg_chunk* __restrict__ chunks,
                                                         u32 n, u64 D, DType t, u32 vflags, u32 G,
                                                         u32 S, i32* __restrict__ status) {

@@ -1,0 +1,293 @@
+// zcg_xz.hip — XzCompression decode (src/compression/xz.rs:34-43, xz2
+// read::XzDecoder = liblzma 5.2 stream decoder) on gfx950.
+//
+// LZMA is one serial range-coded bit stream per chunk, so the parallelism is
+// across chunks: one wave (one 64-lane workgroup) per chunk.  The decoder
+// itself (zcg_xz_core.h) runs wave-uniformly — every lane computes the same
+// state, which keeps control flow convergent — and the lanes fan out where
+// the work is data-parallel:
+//   * the probability model (7 990 u16 for lc+lp<=3; 14 134 for lc+lp=4,
+//     via a second launch with the larger LDS carve) lives in LDS; every
+//     lane reads/writes the same entry (LDS broadcast, no bank conflicts);
+//   * decoded bytes go to a 4 KiB LDS history ring; a match copies all its
+//     bytes in one wave-parallel step (byte k of a match at distance d is
+//     byte k mod d of the d bytes before it, all already decoded), reading
+//     the ring for recent history and the chunk's HBM output for far
+//     distances (older than the ring, already flushed and fenced);
+//   * the ring drains to HBM in 16-B-per-lane coalesced stores;
+//   * the block check (CRC32/CRC64) is 64 per-lane segment CRCs over HBM,
+//     combined with GF(2) x^(8n) shifts (zlib's crc32_combine, 64-bit);
+//   * '>'-types / bool are transformed in place at the end (the ring keeps
+//     raw bytes because far matches re-read the output).
+// Algorithmic bytes per chunk: C + D.  The kernel is latency-bound on the
+// serial range decoder (one dependent LDS round trip per coded bit), not HBM.
+#include "zcg_common.h"
+#include "zcg_xz_core.h"
+
+namespace zcg {
+
+constexpr u32 XZ_RING = 4096;
+constexpr u32 XZ_PROBS_SMALL = 1846 + (0x300u << 3);  // lc+lp <= 3
+constexpr u32 XZ_PROBS_BIG = 1846 + (0x300u << 4);    // lc+lp == 4
+
+constexpr u64 CRC64_POLY = 0xC96C5795D7870F42ull;  // ECMA-182, reflected (xz CRC64)
+constexpr u32 CRC32_POLY = 0xEDB88320u;
+
+struct Crc64Table {
+    u64 t[256];
+    constexpr Crc64Table() : t() {
+        for (u32 i = 0; i < 256; i++) {
+            u64 c = i;
+            for (int k = 0; k < 8; k++) c = (c >> 1) ^ (CRC64_POLY & (0ull - (c & 1)));
+            t[i] = c;
+        }
+    }
+};
+__constant__ Crc64Table g_crc64 = Crc64Table();
+
+// a*b mod P in the reflected bit order (bit 63 = x^0), zlib's multmodp.
+template <typename T, T POLY>
+__device__ inline T gf2_mulmod(T a, T b) {
+    const int W = sizeof(T) * 8;
+    T m = (T)1 << (W - 1), p = 0;
+    if (a == 0) return 0;
+    for (;;) {
+        if (a & m) {
+            p ^= b;
+            if ((a & (m - 1)) == 0) break;
+        }
+        m >>= 1;
+        b = (b & 1) ? (T)((b >> 1) ^ POLY) : (T)(b >> 1);
+    }
+    return p;
+}
+
+// x^(8*nbytes) mod P
+template <typename T, T POLY>
+__device__ inline T gf2_xpow8n(u64 nbytes) {
+    const int W = sizeof(T) * 8;
+    T r = (T)1 << (W - 1);          // x^0
+    T p = (T)1 << (W - 1 - 8);      // x^8
+    while (nbytes) {
+        if (nbytes & 1) r = gf2_mulmod<T, POLY>(p, r);
+        p = gf2_mulmod<T, POLY>(p, p);
+        nbytes >>= 1;
+    }
+    return r;
+}
+
+// CRC of dst[a, b) by the whole wave (all lanes return the same value).
+template <typename T, T POLY>
+__device__ __forceinline__ T wave_crc(const u8* dst, u64 a, u64 b) {
+    const int lane = lane_id();
+    const u64 len = b - a;
+    const u64 seg = ((len + 63) / 64 + 15) & ~15ull;
+    const u64 s0 = a + (u64)lane * seg;
+    const u64 s1 = (s0 + seg < b) ? s0 + seg : b;
+    T c = (T)~(T)0;
+    for (u64 p = s0; p < s1; p += 16) {
+        if (p + 16 <= s1) {
+            u32x4 v = ld16(dst + p);
+            u32 w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const u32 byte = (w[q] >> (8 * k)) & 0xFF;
+                    if (sizeof(T) == 8) c = (T)(g_crc64.t[(c ^ byte) & 0xFF] ^ ((u64)c >> 8));
+                    else c = (T)(g_crc32_table[(c ^ byte) & 0xFF] ^ ((u32)c >> 8));
+                }
+            }
+        } else {
+            for (u64 q = p; q < s1; q++) {
+                const u32 byte = dst[q];
+                if (sizeof(T) == 8) c = (T)(g_crc64.t[(c ^ byte) & 0xFF] ^ ((u64)c >> 8));
+                else c = (T)(g_crc32_table[(c ^ byte) & 0xFF] ^ ((u32)c >> 8));
+            }
+        }
+    }
+    c = ~c;
+    const u64 my_len = s1 > s0 ? s1 - s0 : 0;
+    // combine lane CRCs in order: crc(A||B) = crc(A)*x^(8|B|) ^ crc(B)
+    const T xs = gf2_xpow8n<T, POLY>(seg);
+    T total = 0;  // CRC of the empty message
+    for (int l = 0; l < 64; l++) {
+        const T cl = (T)__shfl((u64)c, l);
+        const u64 ll = __shfl(my_len, l);
+        if (ll == 0) continue;
+        const T sh = (ll == seg) ? xs : gf2_xpow8n<T, POLY>(ll);
+        total = gf2_mulmod<T, POLY>(sh, total) ^ cl;
+    }
+    return total;
+}
+
+typedef __attribute__((address_space(1))) u8 gu8;  // global (HBM) bytes: no flat ops
+typedef __attribute__((address_space(3))) u8 lu8;   // LDS
+typedef __attribute__((address_space(3))) u16 lu16;
+__device__ __forceinline__ u64 ru64(u64 x) {
+    return ((u64)__builtin_amdgcn_readfirstlane((u32)(x >> 32)) << 32) |
+           (u32)__builtin_amdgcn_readfirstlane((u32)x);
+}
+typedef __attribute__((address_space(1))) u32x4 gu32x4_ua __attribute__((aligned(1)));
+
+// Device IO of zx::xz_decode: LDS model + LDS ring + HBM output.
+struct XzDevIO {
+    u64 n, D, pos;
+    const gu8* __restrict__ src;
+    gu8* dst;
+    lu16* probs;
+    lu8* ring;
+    u32 nprob_cap;
+    u64 gfl;  // output bytes already stored to HBM (and fenced)
+    u64 wb;   // input window base
+    u32x4 w;
+    int lane;
+
+    __device__ __forceinline__ void make_uniform() {
+        n = ru64(n); D = ru64(D); pos = ru64(pos); gfl = ru64(gfl); wb = ru64(wb);
+        src = (const gu8*)ru64((u64)src); dst = (gu8*)ru64((u64)dst);
+        probs = (lu16*)(uintptr_t)__builtin_amdgcn_readfirstlane((u32)(uintptr_t)probs);
+        ring = (lu8*)(uintptr_t)__builtin_amdgcn_readfirstlane((u32)(uintptr_t)ring);
+        w.x = __builtin_amdgcn_readfirstlane(w.x); w.y = __builtin_amdgcn_readfirstlane(w.y);
+        w.z = __builtin_amdgcn_readfirstlane(w.z); w.w = __builtin_amdgcn_readfirstlane(w.w);
+        nprob_cap = __builtin_amdgcn_readfirstlane(nprob_cap);
+    }
+    __device__ __forceinline__ void refill(u64 i) {
+        wb = i;
+        if (i + 16 <= n) {
+            w = *(const gu32x4_ua*)(src + i);
+        } else {
+            u32 t[4] = {0, 0, 0, 0};
+            for (u64 q = i; q < n && q < i + 16; q++) t[(q - i) >> 2] |= (u32)src[q] << (8 * ((q - i) & 3));
+            w = u32x4{t[0], t[1], t[2], t[3]};
+        }
+        w.x = __builtin_amdgcn_readfirstlane(w.x);
+        w.y = __builtin_amdgcn_readfirstlane(w.y);
+        w.z = __builtin_amdgcn_readfirstlane(w.z);
+        w.w = __builtin_amdgcn_readfirstlane(w.w);
+    }
+    __device__ __forceinline__ u32 in(u64 i) {
+        u64 d = i - wb;
+        if (d >= 16) { refill(i); d = 0; }
+        const u32 word = d < 8 ? (d < 4 ? w.x : w.y) : (d < 12 ? w.z : w.w);
+        return __builtin_amdgcn_readfirstlane((word >> ((d & 3) * 8)) & 0xFF);
+    }
+    // wave-uniform values are moved to SGPRs so the decoder runs on the SALU
+    __device__ __forceinline__ u32 pget(u32 i) { return __builtin_amdgcn_readfirstlane(probs[i]); }
+    __device__ __forceinline__ void pset(u32 i, u32 v) { probs[i] = (u16)v; }
+    __device__ __forceinline__ void init_probs(u32 count) {
+        for (u32 i = lane; i < count; i += 64) probs[i] = 1024;
+    }
+    __device__ __forceinline__ bool lclp_ok(u32 lclp) { return zx::probs_count(lclp) <= nprob_cap; }
+
+    // store ring bytes [gfl, e) to HBM, then fence
+    __device__ __forceinline__ void flush(u64 e) {
+        const u64 a = gfl;
+        u64 a16 = (a + 15) & ~15ull;
+        if (a16 > e) a16 = e;
+        if ((u64)lane < a16 - a) dst[a + lane] = ring[(a + lane) & (XZ_RING - 1)];
+        const u64 e16 = e & ~15ull;
+        if (e16 >= a16) {
+            for (u64 p = a16 + (u64)lane * 16; p < e16; p += 64 * 16)
+                *(gu32x4_ua*)(dst + p) = *(const __attribute__((address_space(3))) u32x4*)(ring + (p & (XZ_RING - 1)));
+            if ((u64)lane < e - e16) dst[e16 + lane] = ring[(e16 + lane) & (XZ_RING - 1)];
+        }
+        gfl = e;
+        __threadfence_block();
+    }
+    __device__ __forceinline__ void put(u32 b) {
+        ring[pos & (XZ_RING - 1)] = (u8)b;
+        pos++;
+        if (pos - gfl > XZ_RING - 320) flush(pos & ~15ull);
+    }
+    __device__ __forceinline__ u32 back(u64 dist) {
+        const u64 s = pos - 1 - dist;
+        return __builtin_amdgcn_readfirstlane(s >= gfl ? (u32)ring[s & (XZ_RING - 1)] : (u32)dst[s]);
+    }
+    __device__ __forceinline__ void copy(u64 d, u32 len) {
+        if (pos + len - gfl > XZ_RING - 16) flush(pos & ~15ull);
+        for (u32 base = 0; base < len; base += 64) {
+            const u32 k = base + lane;
+            if (k < len) {
+                const u64 s = pos - d + ((u64)k < d ? (u64)k : (u64)k % d);
+                const u8 v = s >= gfl ? ring[s & (XZ_RING - 1)] : dst[s];
+                ring[(pos + k) & (XZ_RING - 1)] = v;
+            }
+        }
+        pos += len;
+    }
+    __device__ __forceinline__ void copy_in(u64 ip, u32 len) {
+        while (len > 0) {
+            const u32 k = len < 256 ? len : 256;
+            if (pos + k - gfl > XZ_RING - 16) flush(pos & ~15ull);
+            for (u32 q = lane; q < k; q += 64) ring[(pos + q) & (XZ_RING - 1)] = src[ip + q];
+            pos += k;
+            ip += k;
+            len -= k;
+        }
+    }
+    __device__ __forceinline__ void finish() {
+        if (gfl != pos) flush(pos);
+    }
+    __device__ __forceinline__ u64 check(u32 id, u64 a, u64 b) {
+        if (id == 4) return wave_crc<u64, CRC64_POLY>((const u8*)dst, a, b);
+        return (u64)wave_crc<u32, CRC32_POLY>((const u8*)dst, a, b);
+    }
+};
+
+template <u32 NPROB>
+__global__ __launch_bounds__(64) void xz_decode_kernel(const zcg_chunk* __restrict__ chunks, u32 n,
+                                                       u64 D, DType t, int retry,
+                                                       i32* __restrict__ status) {
+    __shared__ u16 probs[NPROB];
+    __shared__ __attribute__((aligned(16))) u8 ring[XZ_RING];
+    const u32 c = blockIdx.x;
+    if (c >= n) return;
+    const int lane = lane_id();
+    if (retry && __builtin_amdgcn_readfirstlane(status[c]) != zx::ST_NEED_BIG) return;
+    const zcg_chunk ch = chunks[c];
+    if (D > 0 && ch.dst_cap < D) {
+        if (lane == 0) status[c] = ZCG_ERR_INVALID_INPUT;
+        return;
+    }
+    XzDevIO io;
+    io.n = ch.src_len;
+    io.D = D;
+    io.pos = 0;
+    io.src = (const gu8*)ch.src;
+    io.dst = (gu8*)ch.dst;
+    io.probs = (lu16*)probs;
+    io.ring = (lu8*)ring;
+    io.nprob_cap = NPROB;
+    io.gfl = 0;
+    io.wb = ~0ull >> 1;
+    io.w = u32x4{0, 0, 0, 0};
+    io.lane = lane;
+    int st = zx::xz_decode(io);
+    io.finish();
+    if (st == ZCG_OK && (t.swap || t.isbool)) wave_transform((u8*)ch.dst, D, t);
+    if (lane == 0) status[c] = st;
+}
+
+hipError_t launch_xz_decode(const zcg_array* a, const zcg_chunk* d_chunks, uint32_t n,
+                            int32_t* d_status, void* ws, uint64_t ws_bytes, hipStream_t s) {
+    (void)ws; (void)ws_bytes;
+    if (n == 0) return hipSuccess;
+    const DType t = make_dtype(a->dtype);
+    const u64 D = a->chunk_num_elements * (u64)t.es;
+    hipLaunchKernelGGL(xz_decode_kernel<XZ_PROBS_SMALL>, dim3(n), dim3(64), 0, s, d_chunks, n, D, t,
+                       0, d_status);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    // chunks that switched to lc+lp = 4 re-run with the larger model
+    hipLaunchKernelGGL(xz_decode_kernel<XZ_PROBS_BIG>, dim3(n), dim3(64), 0, s, d_chunks, n, D, t,
+                       1, d_status);
+    return hipGetLastError();
+}
+
+uint64_t xz_decode_ws_bytes(const zcg_array* a, uint32_t n) {
+    (void)a; (void)n;
+    return 0;
+}
+
+}  // namespace zcg

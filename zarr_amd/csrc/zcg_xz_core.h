@@ -1,0 +1,799 @@
+// zcg_xz_core.h — XzCompression decode core (src/compression/xz.rs:34-43:
+// xz2 read::XzDecoder = liblzma 5.2 lzma_stream_decoder, memlimit u64::MAX,
+// no flags), written once and instantiated twice:
+//   * on gfx950 by zcg_xz.hip (IO = LDS probability model + LDS history ring
+//     + wave-parallel match copies into the chunk's HBM output);
+//   * on the host by tests/hostcore (IO = plain arrays), where the same code
+//     is fuzzed against liblzma (the oracle) on corrupted streams.
+// The product path only ever runs the device instantiation.
+//
+// What is restated (the .xz container of xz-file-format-1.0.4 and LZMA2 as
+// liblzma 5.2 decodes them), including the acceptance rules that decide
+// INVALID_DATA vs UNEXPECTED_EOF:
+//   stream header (magic, flags CRC32, reserved bits) -> blocks (header CRC32,
+//   reserved flag bits, compressed/uncompressed size VLIs, filter flags,
+//   header padding; LZMA2 chunks with their dictionary/state/property reset
+//   rules; lc+lp<=4; distances checked against the decoded dictionary; the
+//   final range-coder normalisation and code==0 at every chunk end; exact
+//   compressed chunk sizes; block padding; CRC32/CRC64 check) -> index
+//   (record count, unpadded/uncompressed sizes against the decoded blocks,
+//   padding, CRC32) -> stream footer (magic, CRC32, backward size, flags).
+//
+// read_exact semantics (chunk.rs:112-113): decoding stops once D = N*size
+// bytes exist.  liblzma keeps going inside the lzma_code() call that filled
+// the output, over the input window the BufReader handed it (32 KiB windows,
+// see oracle/zref.c zr_decode_xz): after the output is full, this core keeps
+// validating headers/sizes/checks up to that window's end and stops there
+// with OK.  Truncation before D bytes is UNEXPECTED_EOF.
+//
+// Not restated: filter chains other than a single LZMA2 filter (delta/BCJ;
+// liblzma accepts them, the kernel reports UNSUPPORTED), and the SHA-256
+// check (the block check is skipped for check ID 10, as for the IDs liblzma
+// does not know).  xz2's XzEncoder writes a single LZMA2 filter with CRC64.
+#pragma once
+
+#include <stdint.h>
+
+#if defined(__HIP__)
+#define ZX_INL __host__ __device__ __forceinline__
+#else
+#define ZX_INL inline __attribute__((always_inline))
+#endif
+#if defined(__HIP__)
+#define ZX_HOT __host__ __device__ __attribute__((noinline))
+#else
+#define ZX_HOT inline
+#endif
+
+namespace zx {
+
+// Wave-uniform hint: the device decoder's state is identical in every lane;
+// readfirstlane tells the compiler so (SGPRs, scalar branches).
+#if defined(__HIP_DEVICE_COMPILE__)
+#define ZX_U32(x) ((x) = __builtin_amdgcn_readfirstlane(x))
+#define ZX_UB(c) (__builtin_amdgcn_readfirstlane((uint32_t)(c)) != 0)
+#define ZX_UPH(x) __builtin_amdgcn_readfirstlane(x)
+#define ZX_U64(x) ((x) = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)((x) >> 32)) << 32) | \
+                          (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(x)))
+#else
+#define ZX_U32(x) ((void)0)
+#define ZX_UB(c) (c)
+#define ZX_UPH(x) (x)
+#define ZX_U64(x) ((void)0)
+#endif
+
+typedef uint8_t u8;
+typedef uint16_t u16;
+typedef uint32_t u32;
+typedef uint64_t u64;
+
+// status codes (values of enum zcg_status; NEED_BIG = internal retry code)
+enum : int { ST_OK = 0, ST_EOF = 1, ST_INVALID = 2, ST_UNSUPPORTED = 4, ST_NEED_BIG = 101 };
+
+constexpr u64 BUFREADER = 32768;  // xz2 bufread window (oracle zr_decode_xz)
+constexpr u64 VLI_MAX = 0x7FFFFFFFFFFFFFFFull;
+constexpr u64 VLI_UNKNOWN = ~0ull;
+constexpr u64 UNPADDED_MIN = 5;
+constexpr u64 UNPADDED_MAX = VLI_MAX & ~3ull;
+
+// LZMA probability model layout (u16 entries)
+enum : u32 {
+    P_IS_MATCH = 0,      // [12][16]
+    P_IS_REP = 192,      // [12]
+    P_IS_REP_G0 = 204,   // [12]
+    P_IS_REP_G1 = 216,   // [12]
+    P_IS_REP_G2 = 228,   // [12]
+    P_IS_REP0_LONG = 240,  // [12][16]
+    P_POS_SLOT = 432,    // [4][64]
+    P_SPEC_POS = 688,    // [114]
+    P_ALIGN = 802,       // [16]
+    P_LEN = 818,         // length coder (514)
+    P_REP_LEN = 1332,    // rep length coder (514)
+    P_LITERAL = 1846     // [0x300 << (lc+lp)]
+};
+enum : u32 { L_CHOICE = 0, L_CHOICE2 = 1, L_LOW = 2, L_MID = 130, L_HIGH = 258 };
+
+ZX_INL u32 probs_count(u32 lclp) { return P_LITERAL + (0x300u << lclp); }
+
+ZX_INL u32 check_size(u32 id) {
+    // lzma_check_size(): 0,4,4,4,8,8,8,16,16,16,32,32,32,64,64,64
+    return id == 0 ? 0u : (4u << ((id - 1) / 3));
+}
+
+ZX_INL u32 vli_size(u64 v) {
+    u32 k = 0;
+    do { v >>= 7; ++k; } while (v != 0);
+    return k;
+}
+
+// CRC32 (IEEE, reflected) bit-serial update, for headers/index (a few bytes).
+ZX_INL u32 crc32_byte(u32 c, u32 b) {
+    c ^= b;
+    for (int k = 0; k < 8; k++) c = (c >> 1) ^ (0xEDB88320u & (0u - (c & 1u)));
+    return c;
+}
+
+// 64-bit mixing hash of the (unpadded, uncompressed) size pairs; stands in
+// for liblzma's index hash (best available check over the same pairs, in
+// order): equal lists <=> equal hashes up to collisions.
+ZX_INL u64 pair_hash(u64 h, u64 a, u64 b) {
+    u64 x = h ^ (a * 0x9E3779B97F4A7C15ull);
+    x = (x ^ (x >> 29)) * 0xBF58476D1CE4E5B9ull;
+    x ^= b * 0x94D049BB133111EBull;
+    x = (x ^ (x >> 32)) * 0xD6E8FEB86659FD93ull;
+    return x ^ (x >> 31);
+}
+
+struct IndexSums {
+    u64 count, blocks_size, uncompressed, list_size, hash;
+};
+
+ZX_INL void sums_add(IndexSums& s, u64 unpadded, u64 usize) {
+    s.count++;
+    s.blocks_size += (unpadded + 3) & ~3ull;
+    s.uncompressed += usize;
+    s.list_size += vli_size(unpadded) + vli_size(usize);
+    s.hash = pair_hash(s.hash, unpadded, usize);
+}
+
+// The LZMA symbol loop of one LZMA2 chunk: a separate (non-inlined on the
+// device) function so its ~50 live values get their own register allocation,
+// all 32-bit (the kernel restricts streams and chunks to < 4 GiB).  Returns
+// ST_CONT when the chunk ended cleanly, otherwise the final status.
+struct LzJob {
+    u32 ip, lim, rlim, n, D, chunk_end, dict_start, dsz, u_end, kstart, csz, full;
+    u32 rc_range, rc_code, lc, lp, pb, state, rep0, rep1, rep2, rep3;
+};
+constexpr int ST_CONT = -1;
+
+template <class IO>
+ZX_HOT int lzma_symbols(IO& io_r, LzJob& j) {
+    IO io = io_r;
+    io.make_uniform();  // device: function arguments arrive as per-lane values
+    u32 ip = j.ip, lim = j.lim;
+    u32 rlim = j.rlim, n = j.n, D = j.D, chunk_end = j.chunk_end, dict_start = j.dict_start;
+    u32 dsz = j.dsz, u_end = j.u_end, kstart = j.kstart, csz = j.csz;
+    u32 fullw = j.full;
+    u32 rc_range = j.rc_range, rc_code = j.rc_code;
+    u32 lc = j.lc, lp = j.lp, pb = j.pb;
+    u32 state = j.state, rep0 = j.rep0, rep1 = j.rep1, rep2 = j.rep2, rep3 = j.rep3;
+    ZX_U32(ip); ZX_U32(lim); ZX_U32(rlim); ZX_U32(n); ZX_U32(D); ZX_U32(chunk_end);
+    ZX_U32(dict_start); ZX_U32(dsz); ZX_U32(u_end); ZX_U32(kstart); ZX_U32(csz); ZX_U32(fullw);
+    ZX_U32(rc_range); ZX_U32(rc_code); ZX_U32(lc); ZX_U32(lp); ZX_U32(pb);
+    ZX_U32(state); ZX_U32(rep0); ZX_U32(rep1); ZX_U32(rep2); ZX_U32(rep3);
+    bool full = fullw != 0;
+    const u32 pb_mask = (1u << pb) - 1, lp_mask = (1u << lp) - 1;
+    int rv = ST_CONT;
+#define ZX_RET(v) do { rv = (v); goto out; } while (0)
+#define ZX_STOP() ZX_RET(full ? ST_OK : ST_EOF)
+#define ZX_SET_FULL() do { full = true; u32 ve = (u32)((((u64)ip - 1) / BUFREADER + 1) * BUFREADER); \
+                           lim = ve < n ? ve : n; } while (0)
+
+#define ZX_NORM()                                                \
+    do {                                                         \
+        if (ZX_UB(rc_range < (1u << 24))) {                      \
+            if (ZX_UB(ip >= lim)) ZX_STOP();                     \
+            if (ZX_UB(ip >= rlim)) ZX_RET(ST_INVALID);           \
+            rc_range <<= 8;                                      \
+            rc_code = (rc_code << 8) | io.in(ip++);              \
+            ZX_U32(rc_range); ZX_U32(rc_code); ZX_U32(ip);       \
+        }                                                        \
+    } while (0)
+// branch-free binary decision (the hot instruction sequence)
+#define ZX_BIT(pidx, bitvar)                                     \
+    do {                                                         \
+        ZX_NORM();                                               \
+        const u32 pi_ = (pidx);                                  \
+        const u32 p_ = io.pget(pi_);                             \
+        const u32 bound_ = (rc_range >> 11) * p_;                \
+        const u32 one_ = ZX_UB(rc_code >= bound_) ? 1u : 0u;     \
+        rc_range = one_ ? rc_range - bound_ : bound_;            \
+        rc_code = one_ ? rc_code - bound_ : rc_code;             \
+        io.pset(pi_, one_ ? p_ - (p_ >> 5) : p_ + ((2048 - p_) >> 5)); \
+        bitvar = one_;                                           \
+        ZX_U32(rc_range); ZX_U32(rc_code); ZX_U32(bitvar);       \
+    } while (0)
+
+        // The symbol decoder is a bit-level state machine with one
+        // probability-decode site (and one direct-bit site): every
+        // binary decision of LZMA goes through the same few
+        // instructions, which keeps the device code small and its
+        // state in scalar registers.
+        enum : u32 { M_SYM, M_ISMATCH, M_LIT, M_MLIT, M_ISREP, M_G0, M_R0LONG, M_G1, M_G2,
+                     M_CHOICE, M_CHOICE2, M_TREE, M_REV, M_DIRECT };
+        enum : u32 { C_LEN, C_SLOT };
+        u32 ph = M_SYM, pi = 0, tb = 0, m = 0, tend = 0, tadd = 0, cont = 0;
+        u32 lbase = 0, len = 0, dist = 0, rk = 0, rn = 0, mb = 0, off = 0, mbit = 0;
+        u32 pos_state = 0;
+        u32 dpos = 0;
+        for (;;) {
+            ZX_U32(rc_range); ZX_U32(rc_code); ZX_U32(ph); ZX_U32(pi); ZX_U32(m);
+            ZX_U32(state); ZX_U32(ip); ZX_U64(io.pos);
+            if (ph == M_SYM) {
+                if ((u32)io.pos > u_end) ZX_RET(ST_INVALID);  // more than the declared size
+                if ((u32)io.pos == D && !full) ZX_SET_FULL();
+                const u32 dlim = chunk_end < D ? chunk_end : D;
+                if ((u32)io.pos == dlim) {
+                    // the main loop ends at the dictionary limit; one more
+                    // normalisation, then (chunk end) code must be 0
+                    ZX_NORM();
+                    if ((u32)io.pos != chunk_end) ZX_RET(ST_OK);  // output full mid-chunk
+                    if (rc_code != 0) ZX_RET(ST_INVALID);
+                    if (ip - kstart != csz) ZX_RET(ST_INVALID);
+                    ZX_RET(ST_CONT);
+                }
+                dpos = (u32)io.pos - dict_start;
+                pos_state = (u32)dpos & pb_mask;
+                pi = P_IS_MATCH + (state << 4) + pos_state;
+                ph = M_ISMATCH;
+            }
+            u32 bit;
+            if (ph == M_DIRECT) {
+                ZX_NORM();
+                rc_range >>= 1;
+                rc_code -= rc_range;
+                const u32 t = 0u - (rc_code >> 31);
+                rc_code += rc_range & t;
+                bit = t + 1;
+                ZX_U32(rc_range); ZX_U32(rc_code); ZX_U32(bit);
+            } else {
+                ZX_BIT(pi, bit);
+            }
+            bool dist_done = false, do_copy = false;
+            switch (ZX_UPH(ph)) {
+            case M_ISMATCH:
+                if (bit == 0) {  // literal
+                    const u32 prev = dpos ? io.back(0) : 0u;
+                    tb = P_LITERAL + 0x300u * ((((u32)dpos & lp_mask) << lc) + (prev >> (8 - lc)));
+                    m = 1;
+                    if (state < 7) {
+                        ph = M_LIT;
+                        pi = tb + 1;
+                    } else {
+                        mb = io.back(rep0) << 1;
+                        off = 0x100;
+                        mbit = mb & off;
+                        ph = M_MLIT;
+                        pi = tb + off + mbit + 1;
+                    }
+                } else {
+                    ph = M_ISREP;
+                    pi = P_IS_REP + state;
+                }
+                break;
+            case M_LIT:
+            case M_MLIT:
+                m = (m << 1) | bit;
+                if (ph == M_MLIT) off &= bit ? mbit : ~mbit;  // leaves matched mode on mismatch
+                if (m >= 0x100) {
+                    io.put(m & 0xFF);
+                    state = state < 4 ? 0 : (state < 10 ? state - 3 : state - 6);
+                    ph = M_SYM;
+                } else if (ph == M_MLIT) {
+                    mb <<= 1;
+                    mbit = mb & off;
+                    pi = tb + off + mbit + m;
+                } else {
+                    pi = tb + m;
+                }
+                break;
+            case M_ISREP:
+                if (bit == 0) {  // simple match
+                    rep3 = rep2;
+                    rep2 = rep1;
+                    rep1 = rep0;
+                    lbase = P_LEN;
+                    state = state < 7 ? 7 : 10;
+                    ph = M_CHOICE;
+                    pi = lbase + L_CHOICE;
+                } else {  // repeated match
+                    if (dpos == 0) ZX_RET(ST_INVALID);  // dict_is_distance_valid(dict, 0)
+                    ph = M_G0;
+                    pi = P_IS_REP_G0 + state;
+                }
+                break;
+            case M_G0:
+                if (bit == 0) {
+                    ph = M_R0LONG;
+                    pi = P_IS_REP0_LONG + (state << 4) + pos_state;
+                } else {
+                    ph = M_G1;
+                    pi = P_IS_REP_G1 + state;
+                }
+                break;
+            case M_R0LONG:
+                if (bit == 0) {  // short rep: one byte at rep0
+                    state = state < 7 ? 9 : 11;
+                    io.put(io.back(rep0));
+                    ph = M_SYM;
+                } else {
+                    lbase = P_REP_LEN;
+                    state = state < 7 ? 8 : 11;
+                    ph = M_CHOICE;
+                    pi = lbase + L_CHOICE;
+                }
+                break;
+            case M_G1:
+            case M_G2:
+                if (ph == M_G1 && bit == 0) {
+                    dist = rep1;
+                } else if (ph == M_G1) {
+                    ph = M_G2;
+                    pi = P_IS_REP_G2 + state;
+                    break;
+                } else {
+                    if (bit == 0) {
+                        dist = rep2;
+                    } else {
+                        dist = rep3;
+                        rep3 = rep2;
+                    }
+                    rep2 = rep1;
+                }
+                rep1 = rep0;
+                rep0 = dist;
+                lbase = P_REP_LEN;
+                state = state < 7 ? 8 : 11;
+                ph = M_CHOICE;
+                pi = lbase + L_CHOICE;
+                break;
+            case M_CHOICE:
+                if (bit == 0) {
+                    tb = lbase + L_LOW + (pos_state << 3); tend = 8; tadd = 0;
+                    m = 1; cont = C_LEN; ph = M_TREE; pi = tb + 1;
+                } else {
+                    ph = M_CHOICE2;
+                    pi = lbase + L_CHOICE2;
+                }
+                break;
+            case M_CHOICE2:
+                if (bit == 0) {
+                    tb = lbase + L_MID + (pos_state << 3); tend = 8; tadd = 8;
+                } else {
+                    tb = lbase + L_HIGH; tend = 256; tadd = 16;
+                }
+                m = 1; cont = C_LEN; ph = M_TREE; pi = tb + 1;
+                break;
+            case M_TREE:
+                m = (m << 1) | bit;
+                if (m < tend) {
+                    pi = tb + m;
+                    break;
+                }
+                if (cont == C_LEN) {
+                    len = m - tend + tadd + 2;
+                    if (lbase == P_LEN) {
+                        const u32 lps = len - 2 < 3 ? len - 2 : 3;
+                        tb = P_POS_SLOT + (lps << 6); tend = 64; tadd = 0;
+                        m = 1; cont = C_SLOT; ph = M_TREE; pi = tb + 1;
+                    } else {
+                        do_copy = true;
+                    }
+                } else {
+                    const u32 slot = m - 64;
+                    if (slot < 4) {
+                        dist = slot;
+                        dist_done = true;
+                    } else {
+                        const u32 nd = (slot >> 1) - 1;
+                        dist = (2 | (slot & 1)) << nd;
+                        if (slot < 14) {
+                            tb = P_SPEC_POS + dist - slot - 1;
+                            m = 1; rk = 0; rn = nd; ph = M_REV; pi = tb + 1;
+                        } else {
+                            rn = nd - 4; rk = 0; m = 0; ph = M_DIRECT;
+                        }
+                    }
+                }
+                break;
+            case M_DIRECT:
+                m = (m << 1) + bit;
+                if (++rk == rn) {
+                    dist += m << 4;
+                    tb = P_ALIGN;
+                    m = 1; rk = 0; rn = 4; ph = M_REV; pi = tb + 1;
+                }
+                break;
+            case M_REV:
+                dist |= bit << rk;
+                m = (m << 1) | bit;
+                if (++rk < rn) pi = tb + m;
+                else dist_done = true;
+                break;
+            }
+            if (dist_done) {
+                rep0 = dist;
+                if (rep0 == 0xFFFFFFFFu) ZX_RET(ST_INVALID);  // EOPM with known size
+                const u32 dfull = dpos < dsz ? dpos : dsz;
+                if (rep0 >= dfull) ZX_RET(ST_INVALID);
+                do_copy = true;
+            }
+            if (do_copy) {  // copy, clipped at the dictionary limit
+                const u32 dlim = chunk_end < D ? chunk_end : D;
+                const u32 room = dlim - (u32)io.pos;
+                const u32 k = len <= room ? len : room;
+                io.copy((u64)rep0 + 1, k);
+                if (k < len) {
+                    if (dlim == chunk_end) ZX_RET(ST_INVALID);  // match crosses the chunk end
+                    if ((u32)io.pos > u_end) ZX_RET(ST_INVALID);
+                    ZX_SET_FULL();
+                    ZX_RET(ST_OK);  // output full, rest of the match pending
+                }
+                ph = M_SYM;
+            }
+        }
+#undef ZX_BIT
+#undef ZX_NORM
+out:
+    io_r = io;
+    j.ip = ip; j.lim = lim; j.full = full ? 1u : 0u;
+    j.rc_range = rc_range; j.rc_code = rc_code;
+    j.state = state; j.rep0 = rep0; j.rep1 = rep1; j.rep2 = rep2; j.rep3 = rep3;
+    return rv;
+#undef ZX_RET
+#undef ZX_STOP
+#undef ZX_SET_FULL
+}
+
+// IO concept (see zcg_xz.hip / tests/hostcore/host_cores.cpp):
+//   u64 n, D, pos;                       input size, output size, output pos
+//   u32 in(u64 i);                       input byte i (i < n)
+//   u32 pget(u32 i); void pset(u32 i, u32 v);   probability model
+//   void init_probs(u32 count);          all = 1024
+//   bool lclp_ok(u32 lclp);              false -> ST_NEED_BIG (LDS too small)
+//   void put(u32 b);                     append one byte
+//   u32 back(u64 dist);                  byte at pos-1-dist
+//   void copy(u64 d, u32 len);           append len bytes from d bytes back
+//   void copy_in(u64 ip, u32 len);       append input bytes [ip, ip+len)
+//   u64 check(u32 id, u64 a, u64 b);     CRC32 (id 1) / CRC64 (id 4) of out[a,b)
+//   void finish();                       make all output visible in dst
+template <class IO>
+ZX_INL int xz_decode(IO& io) {
+    const u64 n = io.n;
+    const u64 D = io.D;
+    u64 ip = 0;       // input position
+    u64 lim = n;      // visible input end (moves to the BufReader window end once full)
+    bool full = false;
+
+#define ZX_STOP() return full ? ST_OK : ST_EOF
+#define ZX_NEED(k) do { if (ip + (u64)(k) > lim) ZX_STOP(); } while (0)
+#define ZX_SET_FULL() do { full = true; u64 ve = ((ip - 1) / BUFREADER + 1) * BUFREADER; \
+                           lim = ve < n ? ve : n; } while (0)
+
+    if (D == 0) return ST_OK;  // read_exact of an empty buffer never reads
+    if (n >= 0xFFFFFFFFull || D >= 0xFFFFFFFFull) return ST_UNSUPPORTED;  // 32-bit positions
+
+    // ---- stream header (stream_flags_decoder.c: magic, CRC32, flags) ----
+    ZX_NEED(12);
+    {
+        if (io.in(0) != 0xFD || io.in(1) != 0x37 || io.in(2) != 0x7A || io.in(3) != 0x58 ||
+            io.in(4) != 0x5A || io.in(5) != 0x00)
+            return ST_INVALID;
+        u32 c = 0xFFFFFFFFu;
+        c = crc32_byte(c, io.in(6));
+        c = crc32_byte(c, io.in(7));
+        c = ~c;
+        const u32 stored = io.in(8) | (io.in(9) << 8) | (io.in(10) << 16) | (io.in(11) << 24);
+        if (c != stored) return ST_INVALID;
+        if (io.in(6) != 0 || (io.in(7) & 0xF0)) return ST_INVALID;
+    }
+    const u32 check_id = io.in(7) & 0x0F;
+    const u32 csz_check = check_size(check_id);
+    ip = 12;
+
+    IndexSums blocks = {0, 0, 0, 0, 0};
+
+    // ---- blocks ----------------------------------------------------------
+    for (;;) {
+        ZX_NEED(1);
+        const u32 b0 = io.in(ip);
+        if (b0 == 0) break;  // Index Indicator
+        const u32 hsize = (b0 + 1) * 4;
+        ZX_NEED(hsize);  // lzma_bufcpy of the whole header first
+        const u64 h0 = ip, hend = ip + hsize - 4;
+        {
+            u32 c = 0xFFFFFFFFu;
+            for (u64 q = h0; q < hend; q++) c = crc32_byte(c, io.in(q));
+            c = ~c;
+            const u32 stored = io.in(hend) | (io.in(hend + 1) << 8) | (io.in(hend + 2) << 16) |
+                               (io.in(hend + 3) << 24);
+            if (c != stored) return ST_INVALID;
+        }
+        const u32 bflags = io.in(h0 + 1);
+        if (bflags & 0x3C) return ST_INVALID;
+        u64 hp = h0 + 2;
+        u64 dec_csize = VLI_UNKNOWN, dec_usize = VLI_UNKNOWN;
+        // single-call lzma_vli_decode: running out of header is DATA_ERROR
+        auto vli_hdr = [&](u64* out) -> bool {
+            u64 v = 0;
+            for (u32 k = 0;; k++) {
+                if (hp >= hend) return false;
+                const u32 b = io.in(hp++);
+                v |= (u64)(b & 0x7F) << (7 * k);
+                if (!(b & 0x80)) {
+                    if (b == 0 && k > 0) return false;
+                    *out = v;
+                    return true;
+                }
+                if (k + 1 == 9) return false;
+            }
+        };
+        if (bflags & 0x40) {
+            if (!vli_hdr(&dec_csize)) return ST_INVALID;
+            // lzma_block_unpadded_size() == 0 -> DATA_ERROR
+            if (dec_csize == 0 || dec_csize > VLI_MAX) return ST_INVALID;
+            const u64 unp = dec_csize + hsize + csz_check;
+            if (unp > UNPADDED_MAX || unp < dec_csize) return ST_INVALID;
+        }
+        if (bflags & 0x80) {
+            if (!vli_hdr(&dec_usize)) return ST_INVALID;
+        }
+        const u32 nfilt = (bflags & 3) + 1;
+        u64 fid[4];
+        u32 dict_prop = 0;
+        bool unsupported_chain = false;
+        for (u32 f = 0; f < nfilt; f++) {
+            u64 id = 0, psz = 0;
+            if (!vli_hdr(&id)) return ST_INVALID;
+            if (id >= (1ull << 62)) return ST_INVALID;
+            if (!vli_hdr(&psz)) return ST_INVALID;
+            if (psz > hend - hp) return ST_INVALID;
+            fid[f] = id;
+            // lzma_properties_decode of the filters liblzma 5.2 knows
+            if (id == 0x21) {  // LZMA2
+                if (psz != 1) return ST_INVALID;
+                dict_prop = io.in(hp);
+                if (dict_prop > 40) return ST_INVALID;
+            } else if (id == 0x03) {  // delta
+                if (psz != 1) return ST_INVALID;
+                unsupported_chain = true;
+            } else if (id >= 0x04 && id <= 0x09) {  // BCJ filters
+                if (psz != 0 && psz != 4) return ST_INVALID;
+                unsupported_chain = true;
+            } else if (id == 0x4000000000000001ull) {  // LZMA1
+                if (psz != 5) return ST_INVALID;
+                unsupported_chain = true;
+            } else {
+                return ST_INVALID;  // unknown filter: OPTIONS_ERROR
+            }
+            hp += psz;
+        }
+        while (hp < hend)
+            if (io.in(hp++) != 0) return ST_INVALID;  // header padding
+        // validate_chain(): LZMA1/LZMA2 only as the last filter, last must be one
+        for (u32 f = 0; f < nfilt; f++) {
+            const bool lz = fid[f] == 0x21 || fid[f] == 0x4000000000000001ull;
+            if (lz != (f + 1 == nfilt)) return ST_INVALID;
+        }
+        if (unsupported_chain) return full ? ST_OK : ST_UNSUPPORTED;
+
+        ip = h0 + hsize;
+        const u64 cstart = ip;             // block compressed data start
+        const u64 ustart = io.pos;         // block uncompressed data start
+        const u64 climit = (dec_csize != VLI_UNKNOWN) ? dec_csize
+                                                       : (VLI_MAX & ~3ull) - hsize - csz_check;
+        const u64 c_end = (climit > n) ? ~0ull : cstart + climit;  // compressed bytes < c_end
+        const u64 u_end = (dec_usize != VLI_UNKNOWN) ? ustart + dec_usize : ~0ull;
+
+        // LZMA2 dictionary: lz_decoder rounds up to >= 4096 and a multiple of 16
+        u64 dsz = (dict_prop == 40) ? 0xFFFFFFFFull
+                                    : ((u64)(2 | (dict_prop & 1)) << (dict_prop / 2 + 11));
+        if (dsz < 4096) dsz = 4096;
+        dsz = (dsz + 15) & ~15ull;
+
+        // LZMA2 / LZMA state
+        bool need_dict_reset = true, need_props = true;
+        u64 dict_start = io.pos;
+        u32 lc = 0, lp = 0, pb = 0;
+        u32 state = 0, rep0 = 0, rep1 = 0, rep2 = 0, rep3 = 0;
+        u32 rc_range = 0xFFFFFFFFu, rc_code = 0;
+
+        for (;;) {  // LZMA2 chunks
+            ZX_NEED(1);
+            if (ip >= c_end) return ST_INVALID;
+            const u32 ctl = io.in(ip++);
+            if (ctl == 0) break;  // end of LZMA2 data
+            if (ctl >= 0xE0 || ctl == 1) {
+                need_props = true;
+                need_dict_reset = true;
+            } else if (need_dict_reset) {
+                return ST_INVALID;
+            }
+            bool new_props = false, state_reset = false;
+            if (ctl >= 0x80) {
+                if (ctl >= 0xC0) {
+                    need_props = false;
+                    new_props = true;
+                } else if (need_props) {
+                    return ST_INVALID;
+                } else if (ctl >= 0xA0) {
+                    state_reset = true;
+                }
+            } else if (ctl > 2) {
+                return ST_INVALID;
+            }
+            if (need_dict_reset) {
+                need_dict_reset = false;
+                dict_start = io.pos;  // dict_reset(): empty dictionary, prev byte 0
+                if (full) return ST_OK;  // decode_buffer returns after a reset when out is full
+            }
+            if (ctl >= 0x80) {
+                // ---- LZMA chunk header ----
+                ZX_NEED(4);
+                if (ip + 4 > c_end) return ST_INVALID;
+                const u32 usz = ((ctl & 0x1F) << 16) + (io.in(ip) << 8) + io.in(ip + 1) + 1;
+                const u32 csz = (io.in(ip + 2) << 8) + io.in(ip + 3) + 1;
+                ip += 4;
+                if (new_props) {
+                    ZX_NEED(1);
+                    if (ip >= c_end) return ST_INVALID;
+                    u32 pr = io.in(ip++);
+                    if (pr > (4 * 5 + 4) * 9 + 8) return ST_INVALID;
+                    pb = pr / (9 * 5);
+                    pr -= pb * 9 * 5;
+                    lp = pr / 9;
+                    lc = pr - lp * 9;
+                    if (lc + lp > 4) return ST_INVALID;
+                    if (!io.lclp_ok(lc + lp)) return ST_NEED_BIG;
+                    state_reset = true;
+                }
+                if (state_reset) {
+                    io.init_probs(probs_count(lc + lp));
+                    state = 0;
+                    rep0 = rep1 = rep2 = rep3 = 0;
+                }
+                const u64 kstart = ip;  // chunk compressed data start
+                const u64 rlim = (kstart + csz < c_end) ? kstart + csz : c_end;
+                // range decoder init: 5 bytes, the first one must be 0
+                rc_range = 0xFFFFFFFFu;
+                rc_code = 0;
+                for (int k = 0; k < 5; k++) {
+                    ZX_NEED(1);
+                    if (ip >= rlim) return ST_INVALID;
+                    const u32 b = io.in(ip++);
+                    if (k == 0 && b != 0) return ST_INVALID;
+                    rc_code = (rc_code << 8) | b;
+                    ZX_U32(rc_code);
+                }
+                LzJob j;
+                j.ip = (u32)ip; j.lim = (u32)lim; j.rlim = (u32)rlim; j.n = (u32)n; j.D = (u32)D;
+                j.chunk_end = (u32)(io.pos + usz); j.dict_start = (u32)dict_start;
+                j.dsz = dsz > 0xFFFFFFFFull ? 0xFFFFFFFFu : (u32)dsz;
+                j.u_end = u_end > 0xFFFFFFFFull ? 0xFFFFFFFFu : (u32)u_end;
+                j.kstart = (u32)kstart; j.csz = csz; j.full = full ? 1u : 0u;
+                j.rc_range = rc_range; j.rc_code = rc_code; j.lc = lc; j.lp = lp; j.pb = pb;
+                j.state = state; j.rep0 = rep0; j.rep1 = rep1; j.rep2 = rep2; j.rep3 = rep3;
+                const int r = lzma_symbols(io, j);
+                ip = j.ip; lim = j.lim; full = j.full != 0;
+                rc_range = j.rc_range; rc_code = j.rc_code;
+                state = j.state; rep0 = j.rep0; rep1 = j.rep1; rep2 = j.rep2; rep3 = j.rep3;
+                if (r != ST_CONT) return r;
+            } else {
+                // ---- uncompressed chunk ----
+                ZX_NEED(2);
+                if (ip + 2 > c_end) return ST_INVALID;
+                u32 left = ((io.in(ip) << 8) | io.in(ip + 1)) + 1;
+                ip += 2;
+                while (left > 0) {
+                    if (io.pos == D) return ST_OK;  // dict full: dict_write copies nothing
+                    ZX_NEED(1);
+                    u64 k = left;
+                    if (k > lim - ip) k = lim - ip;
+                    if (k > D - io.pos) k = D - io.pos;
+                    if (ip + k > c_end) return ST_INVALID;
+                    io.copy_in(ip, (u32)k);
+                    ip += k;
+                    left -= (u32)k;
+                    if (io.pos > u_end) return ST_INVALID;
+                    if (io.pos == D && !full) ZX_SET_FULL();
+                }
+            }
+        }
+        // ---- block end (block_decoder.c SEQ_CODE -> PADDING -> CHECK) ----
+        const u64 actual_c = ip - cstart;
+        const u64 actual_u = io.pos - ustart;
+        if (dec_csize != VLI_UNKNOWN && actual_c != dec_csize) return ST_INVALID;
+        if (dec_usize != VLI_UNKNOWN && actual_u != dec_usize) return ST_INVALID;
+        for (u64 padded = actual_c; padded & 3; padded++) {
+            ZX_NEED(1);
+            if (io.in(ip++) != 0) return ST_INVALID;
+        }
+        if (csz_check) {
+            ZX_NEED(csz_check);  // lzma_bufcpy of the whole check first
+            if (check_id == 1 || check_id == 4) {
+                io.finish();
+                const u64 c = io.check(check_id, ustart, io.pos);
+                for (u32 k = 0; k < csz_check; k++)
+                    if (io.in(ip + k) != (u32)((c >> (8 * k)) & 0xFF)) return ST_INVALID;
+            }
+            ip += csz_check;
+        }
+        sums_add(blocks, hsize + actual_c + csz_check, actual_u);
+    }
+
+    // ---- index (index_hash.c lzma_index_hash_decode) ----------------------
+    const u64 istart = ip;
+    u32 icrc = 0xFFFFFFFFu;
+    auto ibyte = [&](u32* b) -> int {  // 0 = ok, 1 = no input
+        if (ip >= lim) return 1;
+        *b = io.in(ip++);
+        icrc = crc32_byte(icrc, *b);
+        return 0;
+    };
+    // streaming lzma_vli_decode: partial input waits, padding zeros invalid
+    auto ivli = [&](u64* out) -> int {  // 0 ok, 1 no input, 2 invalid
+        u64 v = 0;
+        for (u32 k = 0;; k++) {
+            u32 b;
+            if (ibyte(&b)) return 1;
+            v |= (u64)(b & 0x7F) << (7 * k);
+            if (!(b & 0x80)) {
+                if (b == 0 && k > 0) return 2;
+                *out = v;
+                return 0;
+            }
+            if (k + 1 == 9) return 2;
+        }
+    };
+    {
+        u32 ind;
+        if (ibyte(&ind)) ZX_STOP();
+        (void)ind;  // == 0, checked by the block loop
+        u64 count = 0;
+        int r = ivli(&count);
+        if (r == 1) ZX_STOP();
+        if (r == 2 || count != blocks.count) return ST_INVALID;
+        IndexSums rec = {0, 0, 0, 0, 0};
+        for (u64 i = 0; i < count; i++) {
+            u64 unp = 0, usz = 0;
+            r = ivli(&unp);
+            if (r == 1) ZX_STOP();
+            if (r == 2) return ST_INVALID;
+            if (unp < UNPADDED_MIN || unp > UNPADDED_MAX) return ST_INVALID;
+            r = ivli(&usz);
+            if (r == 1) ZX_STOP();
+            if (r == 2) return ST_INVALID;
+            sums_add(rec, unp, usz);
+            if (blocks.blocks_size < rec.blocks_size || blocks.uncompressed < rec.uncompressed ||
+                blocks.list_size < rec.list_size)
+                return ST_INVALID;
+        }
+        const u64 unpadded_index = 1 + vli_size(count) + rec.list_size + 4;
+        for (u64 pad = (4 - (unpadded_index & 3)) & 3; pad > 0; pad--) {
+            u32 b;
+            if (ibyte(&b)) ZX_STOP();
+            if (b != 0) return ST_INVALID;
+        }
+        if (blocks.blocks_size != rec.blocks_size || blocks.uncompressed != rec.uncompressed ||
+            blocks.list_size != rec.list_size || blocks.hash != rec.hash)
+            return ST_INVALID;
+        const u32 crc = ~icrc;
+        for (int k = 0; k < 4; k++) {
+            if (ip >= lim) ZX_STOP();
+            if (io.in(ip++) != ((crc >> (8 * k)) & 0xFF)) return ST_INVALID;
+        }
+        const u64 index_size = (unpadded_index + 3) & ~3ull;
+        (void)istart;
+        // ---- stream footer ----
+        ZX_NEED(12);
+        if (io.in(ip + 10) != 0x59 || io.in(ip + 11) != 0x5A) return ST_INVALID;
+        u32 c = 0xFFFFFFFFu;
+        for (int k = 4; k < 10; k++) c = crc32_byte(c, io.in(ip + k));
+        c = ~c;
+        const u32 stored = io.in(ip) | (io.in(ip + 1) << 8) | (io.in(ip + 2) << 16) | (io.in(ip + 3) << 24);
+        if (c != stored) return ST_INVALID;
+        if (io.in(ip + 8) != 0 || (io.in(ip + 9) & 0xF0)) return ST_INVALID;
+        const u64 bsize = ((u64)(io.in(ip + 4) | (io.in(ip + 5) << 8) | (io.in(ip + 6) << 16) |
+                                 ((u32)io.in(ip + 7) << 24)) + 1) * 4;
+        if (bsize != index_size) return ST_INVALID;
+        if ((io.in(ip + 9) & 0x0F) != check_id) return ST_INVALID;
+        ip += 12;
+    }
+    // LZMA_STREAM_END: fewer than D bytes is UnexpectedEof
+    return full ? ST_OK : ST_EOF;
+#undef ZX_STOP
+#undef ZX_NEED
+#undef ZX_SET_FULL
+}
+
+}  // namespace zx
