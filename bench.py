@@ -44,7 +44,7 @@ METRIC = "decoded chunk GiB/s (device-resident) per CompressionType at 1/2/4/8 G
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
 GIB = float(1 << 30)
 KERNEL = {"gzip": "zcg::inflate_par_kernel", "lz4": "zcg::lz4_decode_kernel", "raw": "zcg::raw_kernel",
-          "xz": "zcg::xz_decode_kernel<7990u>"}
+          "xz": "zcg::xz_decode_kernel<7990u>", "bzip2": "zcg::bz2_decode_kernel"}
 
 
 def quant_chunk(idx: int) -> np.ndarray:
@@ -79,7 +79,10 @@ class _Batch:  # PackedStreams-shaped holder for BatchCodec.decode
 def workload(codec: str):
     """(meta, value generator, description) of each codec's bench shape."""
     from zarr_amd import ArrayMetadata, Gzip, Lz4, Raw
-    from zarr_amd.compression import Xz
+    from zarr_amd.compression import Bzip2, Xz
+    if codec == "bzip2":  # bzip.rs default blockSize 9 on the C2 data shape
+        meta = ArrayMetadata.new([256 * 64, 256 * 64, 4], [256, 256, 4], "<f4", Bzip2(9))
+        return meta, quant_chunk, "bzip2 level 9 f32 256x256x4 (1 MiB) chunks, decode"
     if codec == "xz":  # xz2 default preset 6 on the C2 data shape
         meta = ArrayMetadata.new([256 * 64, 256 * 64, 4], [256, 256, 4], "<f4", Xz(6))
         return meta, quant_chunk, "xz preset 6 f32 256x256x4 (1 MiB) chunks, decode"
@@ -118,6 +121,10 @@ def build_pool(codec, meta, gen, pool, threads, dev):
             streams = list(ex.map(lambda a: gzip_flate2(a.tobytes(), 6), vals))
     elif codec == "lz4":
         streams = gpu_encode_pool(meta, vals, dev)
+    elif codec == "bzip2":
+        import bz2
+        with ThreadPoolExecutor(threads) as ex:  # BzEncoder(Compression::new(9))
+            streams = list(ex.map(lambda a: bz2.compress(a.tobytes(), 9), vals))
     elif codec == "xz":
         import lzma
         with ThreadPoolExecutor(threads) as ex:  # xz2 XzEncoder = easy encoder, preset 6, CRC64
@@ -291,7 +298,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--codec", default="gzip", choices=["gzip", "lz4", "raw", "xz"])
+    ap.add_argument("--codec", default="gzip", choices=["gzip", "lz4", "raw", "xz", "bzip2"])
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--pool", type=int, default=64)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -328,11 +335,11 @@ def main():
 
     if not args.no_extra:
         per = {}
-        for c in ("gzip", "lz4", "raw", "xz"):
+        for c in ("gzip", "lz4", "raw", "xz", "bzip2"):
             if c == args.codec:
                 continue
-            n_c = {"lz4": 4096, "xz": 2048}.get(c, 1024)
-            r, _, s_c = decode_leg(c, n_c, 2 if c == "xz" else max(3, args.steps // 2), 1,
+            n_c = {"lz4": 4096, "xz": 2048, "bzip2": 2048}.get(c, 1024)
+            r, _, s_c = decode_leg(c, n_c, 2 if c in ("xz", "bzip2") else max(3, args.steps // 2), 1,
                                    args.pool, rank, world, dev, host_threads)
             if rank == 0 and world == 1 and not args.no_cpu_baseline and c != "raw":
                 r["cpu_baseline"] = cpu_leg(c, s_c, r["chunk_bytes"], 3.0, host_threads)

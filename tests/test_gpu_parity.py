@@ -21,7 +21,7 @@ from zarr_amd.compression import Bzip2, Xz
 
 pytestmark = pytest.mark.gpu
 
-GPU_DECODE = ["raw", "gzip", "lz4", "xz"]
+GPU_DECODE = ["raw", "gzip", "lz4", "xz", "bzip2"]
 COMP = {"raw": lambda p: Raw(), "gzip": lambda p: Gzip(p), "lz4": lambda p: Lz4(p),
         "bzip2": lambda p: Bzip2(p), "xz": lambda p: Xz(p)}
 NPT = {1: np.uint8, 2: np.uint16, 4: np.uint32, 8: np.uint64}
@@ -295,7 +295,7 @@ def test_raw_large_and_unaligned(dt):
 
 
 # ---- device batch API -------------------------------------------------------------
-@pytest.mark.parametrize("codec", ["gzip", "lz4", "raw", "xz"])
+@pytest.mark.parametrize("codec", ["gzip", "lz4", "raw", "xz", "bzip2"])
 def test_batch_api_device_resident(codec):
     import torch
     from zarr_amd.batch import BatchCodec, PackedStreams
@@ -372,7 +372,7 @@ def test_inflate_parallel_vs_serial_kernel(data):
             assert a.tobytes() == payload[:D]
 
 
-@pytest.mark.parametrize("codec", ["gzip", "lz4", "raw", "xz"])
+@pytest.mark.parametrize("codec", ["gzip", "lz4", "raw", "xz", "bzip2"])
 def test_decode_never_writes_past_n(codec):
     """read_exact stops at byte N even inside a long match: the bytes after
     N*elem_size in the caller's buffer stay untouched (chunk.rs:112-113)."""

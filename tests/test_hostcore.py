@@ -23,6 +23,8 @@ def host():
         _H = ctypes.CDLL(os.path.join(HERE, "libzcg_host.so"))
         _H.zh_xz_decode.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64]
         _H.zh_xz_decode.restype = ctypes.c_int
+        _H.zh_bz2_decode.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64]
+        _H.zh_bz2_decode.restype = ctypes.c_int
     return _H
 
 
@@ -92,3 +94,56 @@ def test_xz_core_reference_vectors():
         st, enc = zref.encode(zref.XZ, preset, v)
         assert st == 0
         same(enc, v.nbytes)
+
+
+def host_bz2(s: bytes, D: int):
+    out = np.zeros(max(D, 1), np.uint8)
+    a = np.frombuffer(s, np.uint8) if s else np.zeros(1, np.uint8)
+    st = host().zh_bz2_decode(a.ctypes.data, len(s), out.ctypes.data, D)
+    return st, out[:D].tobytes()
+
+
+def same_bz2(s, D):
+    r1 = zref.decode(zref.BZIP2, s, D)
+    r2 = host_bz2(s, D)
+    assert r1[0] == r2[0], (r1[0], r2[0], D, len(s))
+    if r1[0] == zref.OK:
+        assert r1[1] == r2[1]
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_bzip2_core_fuzz_vs_libbz2(seed):
+    """Block parsing, selectors, code lengths, libbz2's limit/base/perm
+    Huffman decoding, RUNA/RUNB + MTF, origPtr checks, the tPos walk,
+    unRLE_obuf_to_output_FAST, block/combined CRCs, randomised blocks and
+    the 32 KiB-window post-N behaviour, against libbz2 1.0.8."""
+    import bz2
+    rng = np.random.default_rng(seed)
+    for _ in range(80):
+        k = int(rng.integers(0, 5))
+        n = int(rng.choice([1, 7, 300, 4000, 40000, 250000]))
+        raw = (_data(rng, k, n) if k < 4 else
+               bytes(rng.integers(0, 3, n, dtype=np.uint8).repeat(7)[:n]))
+        s = bz2.compress(raw, int(rng.integers(1, 10)))
+        Ds = [len(raw), max(1, len(raw) // 3), len(raw) + 1]
+        for D in Ds:
+            same_bz2(s, D)
+        for t in rng.integers(0, len(s), 4):
+            same_bz2(s[:int(t)], len(raw))
+        for _ in range(12):
+            b = bytearray(s)
+            if rng.random() < 0.3:
+                p = len(b) - 1 - int(rng.integers(0, min(len(b), 24)))
+            else:
+                p = int(rng.integers(0, len(b)))
+            b[p] ^= 1 << int(rng.integers(0, 8)) if rng.random() < 0.5 else int(rng.integers(1, 256))
+            same_bz2(bytes(b), Ds[int(rng.integers(0, 3))])
+
+
+def test_bzip2_core_reference_vector():
+    """doc-spec vector (bzip.rs:55-72)."""
+    from golden_util import doc_spec
+    d = doc_spec()
+    st, out = host_bz2(bytes.fromhex(d["chunks"]["bzip2"]["hex"]), 12)
+    assert st == 0
+    assert np.frombuffer(out, ">i2").tolist() == d["expected_values"]

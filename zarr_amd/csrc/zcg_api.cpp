@@ -115,6 +115,7 @@ int zcg_codec_on_gpu(int32_t codec, int encode) {
     case ZCG_CODEC_LZ4: return 1;
     case ZCG_CODEC_GZIP: return 1;
     case ZCG_CODEC_XZ: return encode ? 0 : 1;
+    case ZCG_CODEC_BZIP2: return encode ? 0 : 1;
     default: return 0;
     }
 }
@@ -133,7 +134,8 @@ uint64_t zcg_encode_bound(const zcg_compression* c, uint64_t n) {
 }
 
 uint64_t zcg_workspace_bytes(const zcg_array* a, uint32_t n, int encode) {
-    (void)a; (void)n; (void)encode;
+    if (!a) return 0;
+    if (!encode && a->compression.codec == ZCG_CODEC_BZIP2) return bzip2_decode_ws_bytes(a, n);
     return 0;
 }
 
@@ -154,9 +156,12 @@ int zcg_decode_batch(zcg_ctx* ctx, const zcg_array* a, const zcg_chunk* d_chunks
                 : launch_inflate_par(a, d_chunks, n, d_status, s);
         break;
     case ZCG_CODEC_XZ: e = launch_xz_decode(a, d_chunks, n, d_status, nullptr, 0, s); break;
-    case ZCG_CODEC_BZIP2:
-        ctx->err = "codec has no GPU decoder in this build";
-        return ZCG_ERR_UNSUPPORTED;
+    case ZCG_CODEC_BZIP2: {
+        const int r = ensure_dev(ctx, &ctx->ws, &ctx->ws_bytes, bzip2_decode_ws_bytes(a, n));
+        if (r != ZCG_OK) return r;
+        e = launch_bzip2_decode(a, d_chunks, n, d_status, ctx->ws, ctx->ws_bytes, s);
+        break;
+    }
     default: return ZCG_ERR_INVALID_INPUT;
     }
     if (e != hipSuccess) return fail(ctx, e, "decode launch");

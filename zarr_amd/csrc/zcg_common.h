@@ -94,6 +94,20 @@ __device__ __forceinline__ u32 ld16le(const u8* p) { return *(const u16_ua*)p; }
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
+// Address-space-qualified views: global (HBM) and LDS accesses without flat
+// instructions, for code whose pointers travel through structs.
+typedef __attribute__((address_space(1))) u8 gu8;
+typedef __attribute__((address_space(1))) u32 gu32;
+typedef __attribute__((address_space(3))) u8 lu8;
+typedef __attribute__((address_space(3))) u16 lu16;
+typedef __attribute__((address_space(3))) u32 lu32;
+typedef __attribute__((address_space(1))) u32x4 gu32x4_ua __attribute__((aligned(1)));
+typedef __attribute__((address_space(1))) u32x2 gu32x2_ua __attribute__((aligned(1)));
+__device__ __forceinline__ u64 ru64(u64 x) {  // wave-uniform 64-bit value -> SGPRs
+    return ((u64)__builtin_amdgcn_readfirstlane((u32)(x >> 32)) << 32) |
+           (u32)__builtin_amdgcn_readfirstlane((u32)x);
+}
+
 // In-place element transform of a decoded chunk by the whole wave.
 __device__ inline void wave_transform(u8* dst, u64 D, const DType& t) {
     const int lane = lane_id();

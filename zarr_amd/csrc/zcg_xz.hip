@@ -121,14 +121,6 @@ __device__ __forceinline__ T wave_crc(const u8* dst, u64 a, u64 b) {
     return total;
 }
 
-typedef __attribute__((address_space(1))) u8 gu8;  // global (HBM) bytes: no flat ops
-typedef __attribute__((address_space(3))) u8 lu8;   // LDS
-typedef __attribute__((address_space(3))) u16 lu16;
-__device__ __forceinline__ u64 ru64(u64 x) {
-    return ((u64)__builtin_amdgcn_readfirstlane((u32)(x >> 32)) << 32) |
-           (u32)__builtin_amdgcn_readfirstlane((u32)x);
-}
-typedef __attribute__((address_space(1))) u32x4 gu32x4_ua __attribute__((aligned(1)));
 
 // Device IO of zx::xz_decode: LDS model + LDS ring + HBM output.
 struct XzDevIO {
