@@ -284,6 +284,31 @@ def test_lz4_errors():
     check("lz4", bytes(bad), "u1", len(payload))
 
 
+def test_lz4_corruption_sweep():
+    """Byte corruptions and truncations of LZ4 frames everywhere (block
+    headers, tokens, length bytes, offsets, literals, end mark, checksums),
+    batched, each classified and decoded like LZ4F_decompress (oracle)."""
+    rng = np.random.default_rng(31)
+    payloads = [rw(100000, seed=3).tobytes(), DATASETS["text_like"]()[:150000],
+                np.random.default_rng(8).integers(0, 4, 120000, dtype=np.uint8).tobytes()]
+    for k, payload in enumerate(payloads):
+        if k == 1:
+            s = zref.lz4_frame_custom(payload, block_checksum=True)
+        else:
+            st, s = zref.encode(zref.LZ4, 65536, np.frombuffer(payload, np.uint8))
+        for D in (len(payload), len(payload) // 2 + 3):
+            streams = [s[:int(t)] for t in rng.integers(0, len(s), 48)]
+            for _ in range(464):
+                b = bytearray(s)
+                p = int(rng.integers(0, len(b)))
+                b[p] ^= int(rng.integers(1, 256))
+                if rng.random() < 0.2:
+                    q = int(rng.integers(0, len(b)))
+                    b[q] = int(rng.integers(0, 256))
+                streams.append(bytes(b))
+            check_many("lz4", streams, "u1", D)
+
+
 @pytest.mark.parametrize("dt", ["<i2", ">i2", ">f8", "bool", "u1"])
 def test_raw_large_and_unaligned(dt):
     es, be, isb, npdt = dtype_info(dt)

@@ -25,8 +25,9 @@
 // block size > blockMax, block checksum mismatch, literal/match length
 // overruns, offsets before the block (or frame, for linked blocks) start and
 // matches ending in the last 5 bytes of the block capacity are INVALID_DATA;
-// a frame whose data ends before N bytes is UNEXPECTED_EOF.  Offset 0 is
-// rejected as the LZ4 block format specifies.
+// a frame whose data ends before N bytes is UNEXPECTED_EOF (after the
+// content-size and content-checksum checks LZ4F's suffix stage makes).
+// Offset 0 is accepted and yields zeros, as lz4 1.9.3 decodes it.
 #include "zcg_common.h"
 
 namespace zcg {
@@ -34,7 +35,8 @@ namespace zcg {
 constexpr u32 LZ4_MAGIC = 0x184D2204u;
 constexpr u32 LZ4_MIN_BMAX = 65536u;
 
-enum : u32 { F_BLOCK_CKSUM = 1, F_LINKED = 2, F_FRAME_END = 4, F_TRUNC = 8, F_CONTENT_CKSUM = 16 };
+enum : u32 { F_BLOCK_CKSUM = 1, F_LINKED = 2, F_FRAME_END = 4, F_TRUNC = 8, F_CONTENT_CKSUM = 16,
+             F_CONTENT_SIZE = 32 };
 
 struct Lz4Hdr {
     int st;       // header status
@@ -63,7 +65,7 @@ __device__ inline Lz4Hdr lz4_parse_header(const u8* s, u64 n) {
     if (hc != s[hl - 1]) { h.st = ZCG_ERR_INVALID_DATA; return h; }
     h.bmax = 1u << (8 + 2 * id);
     h.flags = ((flg & 0x10) ? F_BLOCK_CKSUM : 0) | ((flg & 0x20) ? 0 : F_LINKED) |
-              ((flg & 0x04) ? F_CONTENT_CKSUM : 0);
+              ((flg & 0x04) ? F_CONTENT_CKSUM : 0) | ((flg & 0x08) ? F_CONTENT_SIZE : 0);
     h.hdr_len = hl;
     return h;
 }
@@ -90,6 +92,45 @@ __device__ __forceinline__ u32x4 pattern16(const u32x4& b, u32 d, u32 ph) {
     return u32x4{r[0], r[1], r[2], r[3]};
 }
 
+// 16-byte register window over the compressed block: the token, length
+// bytes and offset of a sequence come from registers, so a sequence costs one
+// window load (prefetched before the previous match copy) instead of a chain
+// of dependent byte loads.
+__device__ __forceinline__ u32 win_byte(const u32x4& w, u32 d) {
+    const u32 word = d < 8 ? (d < 4 ? w.x : w.y) : (d < 12 ? w.z : w.w);
+    return (word >> ((d & 3) * 8)) & 0xFF;
+}
+// 16 bytes of the stream at q; bytes at or past `avail` read as 0
+__device__ __forceinline__ u32x4 win_load(const u8* __restrict__ src, u64 q, u64 avail) {
+    if (q + 16 <= avail) return ld16(src + q);
+    u64 lo = 0, hi = 0;
+    for (u32 k = 0; k < 16; k++) {
+        const u64 b = (q + k < avail) ? (u64)src[q + k] : 0ull;
+        if (k < 8) lo |= b << (8 * k);
+        else hi |= b << (8 * (k - 8));
+    }
+    return u32x4{(u32)lo, (u32)(lo >> 32), (u32)hi, (u32)(hi >> 32)};
+}
+// w shifted down by d (< 16) bytes, zero fill
+__device__ __forceinline__ u32x4 win_shift(const u32x4& w, u32 d) {
+    u64 lo = ((u64)w.y << 32) | w.x, hi = ((u64)w.w << 32) | w.z;
+    if (d >= 8) { lo = hi; hi = 0; d -= 8; }
+    if (d) { lo = (lo >> (8 * d)) | (hi << (64 - 8 * d)); hi >>= 8 * d; }
+    return u32x4{(u32)lo, (u32)(lo >> 32), (u32)hi, (u32)(hi >> 32)};
+}
+struct LzWin {  // 16 bytes of the stream at wb
+    const u8* src;
+    u64 avail;
+    u32x4 w;
+    u32 wb;
+    __device__ __forceinline__ u32 byte(u32 q) {
+        u32 d = q - wb;
+        if (d >= 16) { w = win_load(src, q, avail); wb = q; d = 0; }
+        return win_byte(w, d);
+    }
+    __device__ __forceinline__ void at(u32 q) { w = win_load(src, q, avail); wb = q; }
+};
+
 // Decode one LZ4 block (LZ4_decompress_safe semantics, capacity `cap`).
 //   src/csize: compressed block;  src_avail: readable bytes from src
 //   dst: chunk output base;  op0: output position of the block
@@ -102,15 +143,17 @@ __device__ int lz4_block(const u8* __restrict__ src, u32 csize, u64 src_avail, u
     u64 op = op0;
     const u64 oend = op0 + cap;
     const u64 wlim = oend < lim ? oend : lim;
+    LzWin in{src, src_avail, u32x4{0, 0, 0, 0}, 0};
+    in.at(0);
     for (;;) {
         if (ip >= iend) return ZCG_ERR_INVALID_DATA;
-        const u32 token = src[ip++];
+        const u32 token = in.byte(ip++);
         u32 lit = token >> 4;
         if (lit == 15) {
             if ((int64_t)ip >= (int64_t)iend - 15) return ZCG_ERR_INVALID_DATA;
             u32 s;
             do {
-                s = src[ip++];
+                s = in.byte(ip++);
                 lit += s;
             } while (s == 255 && (int64_t)ip < (int64_t)iend - 15);
         }
@@ -123,9 +166,14 @@ __device__ int lz4_block(const u8* __restrict__ src, u32 csize, u64 src_avail, u
             op = cpy;
             break;
         }
-        // literals
+        // literals: from the window when they lie in it, else 16 B copies
         if (cpy + 16 <= wlim && (u64)ip + lit + 16 <= src_avail) {
-            for (u32 i = 0; i < lit; i += 16) st16(dst + op + i, ld16(src + ip + i));
+            const u32 d = ip - in.wb;
+            if (d < 16 && d + lit <= 16) {
+                if (lit) st16(dst + op, win_shift(in.w, d));
+            } else {
+                for (u32 i = 0; i < lit; i += 16) st16(dst + op + i, ld16(src + ip + i));
+            }
         } else {
             for (u32 i = 0; i < lit; i++)
                 if (op + i < lim) dst[op + i] = src[ip + i];
@@ -133,23 +181,31 @@ __device__ int lz4_block(const u8* __restrict__ src, u32 csize, u64 src_avail, u
         ip += lit;
         op = cpy;
         // offset + match length
-        const u32 off = (u32)src[ip] | ((u32)src[ip + 1] << 8);
+        const u32 off = in.byte(ip) | (in.byte(ip + 1) << 8);
         ip += 2;
         u32 ml = token & 15;
         if (ml == 15) {
             u32 s;
             do {
-                s = src[ip++];
+                s = in.byte(ip++);
                 ml += s;
                 if ((int64_t)ip >= (int64_t)iend - 4) return ZCG_ERR_INVALID_DATA;
             } while (s == 255);
         }
         ml += 4;
-        if (off == 0 || op - low < off) return ZCG_ERR_INVALID_DATA;
+        if (op - low < off) return ZCG_ERR_INVALID_DATA;
         const u64 mend = op + ml;
         if (mend + 5 > oend) return ZCG_ERR_INVALID_DATA;
+        // next sequence's window (token + offset + a few length bytes), in
+        // flight during the match copy; kept when 8+ bytes of it remain
+        if (ip - in.wb > 8) in.at(ip);
         u8* const d = dst + op;
-        if (mend + 32 <= wlim) {
+        if (off == 0) {
+            // lz4 1.9.3 accepts offset 0: LZ4_write32(op, 0) then copies the
+            // match from itself, so the match bytes come out as zeros
+            for (u32 i = 0; i < ml; i++)
+                if (op + i < lim) dst[op + i] = 0;
+        } else if (mend + 32 <= wlim) {
             if (off >= 16) {
                 for (u32 i = 0; i < ml; i += 16) st16(d + i, ld16(d - off + i));
             } else {
@@ -194,7 +250,19 @@ __device__ int lz4_frame_serial(const u8* s, u64 n, u8* dst, u64 D, u32 vflags) 
         if (pos + 4 > n) return ZCG_ERR_UNEXPECTED_EOF;
         const u32 bs = ld32(s + pos);
         pos += 4;
-        if (bs == 0) return ZCG_ERR_UNEXPECTED_EOF;  // end mark before N bytes
+        if (bs == 0) {
+            // end mark before N bytes: LZ4F's dstage_getSuffix still checks the
+            // declared content size and the content checksum (lz4-rs feeds them)
+            if (h.flags & F_CONTENT_SIZE) {
+                const u64 declared = (u64)ld32(s + 6) | ((u64)ld32(s + 10) << 32);
+                if (declared != out) return ZCG_ERR_INVALID_DATA;
+            }
+            if (h.flags & F_CONTENT_CKSUM) {
+                if (pos + 4 > n) return ZCG_ERR_UNEXPECTED_EOF;
+                if (xxh32(dst, out, 0) != ld32(s + pos)) return ZCG_ERR_INVALID_DATA;
+            }
+            return ZCG_ERR_UNEXPECTED_EOF;
+        }
         const u32 cs = bs & 0x7FFFFFFFu;
         if (cs > h.bmax) return ZCG_ERR_INVALID_DATA;
         const u64 need = (u64)cs + ((h.flags & F_BLOCK_CKSUM) ? 4 : 0);
@@ -348,7 +416,9 @@ __global__ __launch_bounds__(64) void lz4_decode_kernel(const zcg_chunk* __restr
             if (st == ZCG_OK && total < D) {
                 // frame ended / input ran out before N bytes; a short last
                 // block followed by more blocks means the guess failed.
-                if (c_flags[j] & (F_FRAME_END | F_TRUNC)) st = ZCG_ERR_UNEXPECTED_EOF;
+                if (c_flags[j] & F_TRUNC) st = ZCG_ERR_UNEXPECTED_EOF;
+                else if (c_flags[j] & F_FRAME_END)  // suffix checks: exact serial path
+                    st = (c_flags[j] & (F_CONTENT_CKSUM | F_CONTENT_SIZE)) ? -1 : ZCG_ERR_UNEXPECTED_EOF;
                 else st = -1;
             }
         }
