@@ -194,222 +194,163 @@ ZX_HOT int lzma_symbols(IO& io_r, LzJob& j) {
         ZX_U32(rc_range); ZX_U32(rc_code); ZX_U32(bitvar);       \
     } while (0)
 
-        // The symbol decoder is a bit-level state machine with one
-        // probability-decode site (and one direct-bit site): every
-        // binary decision of LZMA goes through the same few
-        // instructions, which keeps the device code small and its
-        // state in scalar registers.
-        enum : u32 { M_SYM, M_ISMATCH, M_LIT, M_MLIT, M_ISREP, M_G0, M_R0LONG, M_G1, M_G2,
-                     M_CHOICE, M_CHOICE2, M_TREE, M_REV, M_DIRECT };
-        enum : u32 { C_LEN, C_SLOT };
-        u32 ph = M_SYM, pi = 0, tb = 0, m = 0, tend = 0, tadd = 0, cont = 0;
-        u32 lbase = 0, len = 0, dist = 0, rk = 0, rn = 0, mb = 0, off = 0, mbit = 0;
-        u32 pos_state = 0;
-        u32 dpos = 0;
+        // Structured symbol decoder: one loop iteration per LZMA symbol;
+        // every binary decision is the branch-free ZX_BIT sequence on
+        // wave-uniform (scalar) state.
+#define ZX_TREE(base, nbits, out)                                    \
+    do {                                                             \
+        u32 m_ = 1;                                                  \
+        for (u32 k_ = 0; k_ < (nbits); k_++) {                       \
+            u32 b_;                                                  \
+            ZX_BIT((base) + m_, b_);                                 \
+            m_ = (m_ << 1) | b_;                                     \
+        }                                                            \
+        out = m_ - (1u << (nbits));                                  \
+    } while (0)
         for (;;) {
-            ZX_U32(rc_range); ZX_U32(rc_code); ZX_U32(ph); ZX_U32(pi); ZX_U32(m);
-            ZX_U32(state); ZX_U32(ip); ZX_U64(io.pos);
-            if (ph == M_SYM) {
-                if ((u32)io.pos > u_end) ZX_RET(ST_INVALID);  // more than the declared size
-                if ((u32)io.pos == D && !full) ZX_SET_FULL();
-                const u32 dlim = chunk_end < D ? chunk_end : D;
-                if ((u32)io.pos == dlim) {
-                    // the main loop ends at the dictionary limit; one more
-                    // normalisation, then (chunk end) code must be 0
-                    ZX_NORM();
-                    if ((u32)io.pos != chunk_end) ZX_RET(ST_OK);  // output full mid-chunk
-                    if (rc_code != 0) ZX_RET(ST_INVALID);
-                    if (ip - kstart != csz) ZX_RET(ST_INVALID);
-                    ZX_RET(ST_CONT);
-                }
-                dpos = (u32)io.pos - dict_start;
-                pos_state = (u32)dpos & pb_mask;
-                pi = P_IS_MATCH + (state << 4) + pos_state;
-                ph = M_ISMATCH;
-            }
-            u32 bit;
-            if (ph == M_DIRECT) {
+            ZX_U32(rc_range); ZX_U32(rc_code); ZX_U32(state); ZX_U32(ip); ZX_U64(io.pos);
+            ZX_U32(rep0); ZX_U32(rep1); ZX_U32(rep2); ZX_U32(rep3);
+            if ((u32)io.pos > u_end) ZX_RET(ST_INVALID);  // more than the declared size
+            if ((u32)io.pos == D && !full) ZX_SET_FULL();
+            const u32 dlim = chunk_end < D ? chunk_end : D;
+            if ((u32)io.pos == dlim) {
+                // the main loop ends at the dictionary limit; one more
+                // normalisation, then (chunk end) code must be 0
                 ZX_NORM();
-                rc_range >>= 1;
-                rc_code -= rc_range;
-                const u32 t = 0u - (rc_code >> 31);
-                rc_code += rc_range & t;
-                bit = t + 1;
-                ZX_U32(rc_range); ZX_U32(rc_code); ZX_U32(bit);
-            } else {
-                ZX_BIT(pi, bit);
+                if ((u32)io.pos != chunk_end) ZX_RET(ST_OK);  // output full mid-chunk
+                if (rc_code != 0) ZX_RET(ST_INVALID);
+                if (ip - kstart != csz) ZX_RET(ST_INVALID);
+                ZX_RET(ST_CONT);
             }
-            bool dist_done = false, do_copy = false;
-            switch (ZX_UPH(ph)) {
-            case M_ISMATCH:
-                if (bit == 0) {  // literal
-                    const u32 prev = dpos ? io.back(0) : 0u;
-                    tb = P_LITERAL + 0x300u * ((((u32)dpos & lp_mask) << lc) + (prev >> (8 - lc)));
-                    m = 1;
-                    if (state < 7) {
-                        ph = M_LIT;
-                        pi = tb + 1;
-                    } else {
-                        mb = io.back(rep0) << 1;
-                        off = 0x100;
-                        mbit = mb & off;
-                        ph = M_MLIT;
-                        pi = tb + off + mbit + 1;
-                    }
+            const u32 dpos = (u32)io.pos - dict_start;
+            const u32 pos_state = dpos & pb_mask;
+            u32 bit;
+            ZX_BIT(P_IS_MATCH + (state << 4) + pos_state, bit);
+            if (bit == 0) {
+                // ---- literal ----
+                const u32 prev = dpos ? io.back(0) : 0u;
+                const u32 tb = P_LITERAL + 0x300u * (((dpos & lp_mask) << lc) + (prev >> (8 - lc)));
+                u32 m = 1;
+                if (state < 7) {
+                    do {
+                        ZX_BIT(tb + m, bit);
+                        m = (m << 1) | bit;
+                    } while (m < 0x100);
                 } else {
-                    ph = M_ISREP;
-                    pi = P_IS_REP + state;
+                    u32 mb = io.back(rep0);
+                    u32 off = 0x100;
+                    do {
+                        mb <<= 1;
+                        const u32 mbit = mb & off;
+                        ZX_BIT(tb + off + mbit + m, bit);
+                        m = (m << 1) | bit;
+                        off &= bit ? mbit : ~mbit;  // leaves matched mode on mismatch
+                        ZX_U32(off); ZX_U32(mb);
+                    } while (m < 0x100);
                 }
-                break;
-            case M_LIT:
-            case M_MLIT:
-                m = (m << 1) | bit;
-                if (ph == M_MLIT) off &= bit ? mbit : ~mbit;  // leaves matched mode on mismatch
-                if (m >= 0x100) {
-                    io.put(m & 0xFF);
-                    state = state < 4 ? 0 : (state < 10 ? state - 3 : state - 6);
-                    ph = M_SYM;
-                } else if (ph == M_MLIT) {
-                    mb <<= 1;
-                    mbit = mb & off;
-                    pi = tb + off + mbit + m;
-                } else {
-                    pi = tb + m;
-                }
-                break;
-            case M_ISREP:
-                if (bit == 0) {  // simple match
-                    rep3 = rep2;
-                    rep2 = rep1;
-                    rep1 = rep0;
-                    lbase = P_LEN;
-                    state = state < 7 ? 7 : 10;
-                    ph = M_CHOICE;
-                    pi = lbase + L_CHOICE;
-                } else {  // repeated match
-                    if (dpos == 0) ZX_RET(ST_INVALID);  // dict_is_distance_valid(dict, 0)
-                    ph = M_G0;
-                    pi = P_IS_REP_G0 + state;
-                }
-                break;
-            case M_G0:
-                if (bit == 0) {
-                    ph = M_R0LONG;
-                    pi = P_IS_REP0_LONG + (state << 4) + pos_state;
-                } else {
-                    ph = M_G1;
-                    pi = P_IS_REP_G1 + state;
-                }
-                break;
-            case M_R0LONG:
-                if (bit == 0) {  // short rep: one byte at rep0
-                    state = state < 7 ? 9 : 11;
-                    io.put(io.back(rep0));
-                    ph = M_SYM;
-                } else {
-                    lbase = P_REP_LEN;
-                    state = state < 7 ? 8 : 11;
-                    ph = M_CHOICE;
-                    pi = lbase + L_CHOICE;
-                }
-                break;
-            case M_G1:
-            case M_G2:
-                if (ph == M_G1 && bit == 0) {
-                    dist = rep1;
-                } else if (ph == M_G1) {
-                    ph = M_G2;
-                    pi = P_IS_REP_G2 + state;
-                    break;
-                } else {
-                    if (bit == 0) {
-                        dist = rep2;
-                    } else {
-                        dist = rep3;
-                        rep3 = rep2;
-                    }
-                    rep2 = rep1;
-                }
+                io.put(m & 0xFF);
+                state = state < 4 ? 0 : (state < 10 ? state - 3 : state - 6);
+                continue;
+            }
+            u32 lbase;
+            ZX_BIT(P_IS_REP + state, bit);
+            if (bit == 0) {  // simple match
+                rep3 = rep2;
+                rep2 = rep1;
                 rep1 = rep0;
-                rep0 = dist;
+                lbase = P_LEN;
+                state = state < 7 ? 7 : 10;
+            } else {  // repeated match
+                if (dpos == 0) ZX_RET(ST_INVALID);  // dict_is_distance_valid(dict, 0)
+                ZX_BIT(P_IS_REP_G0 + state, bit);
+                if (bit == 0) {
+                    ZX_BIT(P_IS_REP0_LONG + (state << 4) + pos_state, bit);
+                    if (bit == 0) {  // short rep: one byte at rep0
+                        state = state < 7 ? 9 : 11;
+                        io.put(io.back(rep0));
+                        continue;
+                    }
+                } else {
+                    u32 dist;
+                    ZX_BIT(P_IS_REP_G1 + state, bit);
+                    if (bit == 0) {
+                        dist = rep1;
+                    } else {
+                        ZX_BIT(P_IS_REP_G2 + state, bit);
+                        if (bit == 0) {
+                            dist = rep2;
+                        } else {
+                            dist = rep3;
+                            rep3 = rep2;
+                        }
+                        rep2 = rep1;
+                    }
+                    rep1 = rep0;
+                    rep0 = dist;
+                }
                 lbase = P_REP_LEN;
                 state = state < 7 ? 8 : 11;
-                ph = M_CHOICE;
-                pi = lbase + L_CHOICE;
-                break;
-            case M_CHOICE:
-                if (bit == 0) {
-                    tb = lbase + L_LOW + (pos_state << 3); tend = 8; tadd = 0;
-                    m = 1; cont = C_LEN; ph = M_TREE; pi = tb + 1;
-                } else {
-                    ph = M_CHOICE2;
-                    pi = lbase + L_CHOICE2;
-                }
-                break;
-            case M_CHOICE2:
-                if (bit == 0) {
-                    tb = lbase + L_MID + (pos_state << 3); tend = 8; tadd = 8;
-                } else {
-                    tb = lbase + L_HIGH; tend = 256; tadd = 16;
-                }
-                m = 1; cont = C_LEN; ph = M_TREE; pi = tb + 1;
-                break;
-            case M_TREE:
-                m = (m << 1) | bit;
-                if (m < tend) {
-                    pi = tb + m;
-                    break;
-                }
-                if (cont == C_LEN) {
-                    len = m - tend + tadd + 2;
-                    if (lbase == P_LEN) {
-                        const u32 lps = len - 2 < 3 ? len - 2 : 3;
-                        tb = P_POS_SLOT + (lps << 6); tend = 64; tadd = 0;
-                        m = 1; cont = C_SLOT; ph = M_TREE; pi = tb + 1;
-                    } else {
-                        do_copy = true;
-                    }
-                } else {
-                    const u32 slot = m - 64;
-                    if (slot < 4) {
-                        dist = slot;
-                        dist_done = true;
-                    } else {
-                        const u32 nd = (slot >> 1) - 1;
-                        dist = (2 | (slot & 1)) << nd;
-                        if (slot < 14) {
-                            tb = P_SPEC_POS + dist - slot - 1;
-                            m = 1; rk = 0; rn = nd; ph = M_REV; pi = tb + 1;
-                        } else {
-                            rn = nd - 4; rk = 0; m = 0; ph = M_DIRECT;
-                        }
-                    }
-                }
-                break;
-            case M_DIRECT:
-                m = (m << 1) + bit;
-                if (++rk == rn) {
-                    dist += m << 4;
-                    tb = P_ALIGN;
-                    m = 1; rk = 0; rn = 4; ph = M_REV; pi = tb + 1;
-                }
-                break;
-            case M_REV:
-                dist |= bit << rk;
-                m = (m << 1) | bit;
-                if (++rk < rn) pi = tb + m;
-                else dist_done = true;
-                break;
             }
-            if (dist_done) {
+            // ---- length ----
+            u32 len;
+            ZX_BIT(lbase + L_CHOICE, bit);
+            if (bit == 0) {
+                ZX_TREE(lbase + L_LOW + (pos_state << 3), 3, len);
+            } else {
+                ZX_BIT(lbase + L_CHOICE2, bit);
+                if (bit == 0) {
+                    ZX_TREE(lbase + L_MID + (pos_state << 3), 3, len);
+                    len += 8;
+                } else {
+                    ZX_TREE(lbase + L_HIGH, 8, len);
+                    len += 16;
+                }
+            }
+            len += 2;
+            if (lbase == P_LEN) {
+                // ---- distance ----
+                const u32 lps = len - 2 < 3 ? len - 2 : 3;
+                u32 slot;
+                ZX_TREE(P_POS_SLOT + (lps << 6), 6, slot);
+                u32 dist;
+                if (slot < 4) {
+                    dist = slot;
+                } else {
+                    const u32 nd = (slot >> 1) - 1;
+                    dist = (2 | (slot & 1)) << nd;
+                    u32 rb, rn;
+                    if (slot < 14) {
+                        rb = P_SPEC_POS + dist - slot - 1;
+                        rn = nd;
+                    } else {
+                        u32 direct = 0;
+                        for (u32 k = 0; k < nd - 4; k++) {
+                            ZX_NORM();
+                            rc_range >>= 1;
+                            rc_code -= rc_range;
+                            const u32 t = 0u - (rc_code >> 31);
+                            rc_code += rc_range & t;
+                            direct = (direct << 1) + (t + 1);
+                            ZX_U32(rc_range); ZX_U32(rc_code); ZX_U32(direct);
+                        }
+                        dist += direct << 4;
+                        rb = P_ALIGN;
+                        rn = 4;
+                    }
+                    u32 mm = 1;
+                    for (u32 k = 0; k < rn; k++) {
+                        ZX_BIT(rb + mm, bit);
+                        mm = (mm << 1) | bit;
+                        dist |= bit << k;
+                    }
+                }
                 rep0 = dist;
                 if (rep0 == 0xFFFFFFFFu) ZX_RET(ST_INVALID);  // EOPM with known size
                 const u32 dfull = dpos < dsz ? dpos : dsz;
                 if (rep0 >= dfull) ZX_RET(ST_INVALID);
-                do_copy = true;
             }
-            if (do_copy) {  // copy, clipped at the dictionary limit
-                const u32 dlim = chunk_end < D ? chunk_end : D;
+            // ---- copy, clipped at the dictionary limit ----
+            {
                 const u32 room = dlim - (u32)io.pos;
                 const u32 k = len <= room ? len : room;
                 io.copy((u64)rep0 + 1, k);
@@ -419,9 +360,9 @@ ZX_HOT int lzma_symbols(IO& io_r, LzJob& j) {
                     ZX_SET_FULL();
                     ZX_RET(ST_OK);  // output full, rest of the match pending
                 }
-                ph = M_SYM;
             }
         }
+#undef ZX_TREE
 #undef ZX_BIT
 #undef ZX_NORM
 out:
