@@ -136,12 +136,9 @@ def build_pool(codec, meta, gen, pool, threads, dev):
 
 
 def sync_max(t_local, world, dev):
-    import torch
-    if world == 1:
-        return t_local
-    t = torch.tensor([t_local], dtype=torch.float64, device=dev)
-    torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-    return float(t.item())
+    """Slowest rank's time (zarr_amd.shard.max_over_ranks; RCCL on GPU ranks)."""
+    from zarr_amd.shard import max_over_ranks
+    return max_over_ranks(t_local, dev) if world > 1 else t_local
 
 
 def barrier(world):
@@ -160,7 +157,10 @@ def decode_leg(codec, n, steps, warmup, pool, rank, world, dev, threads):
     D = vals[0].nbytes
     ALIGN = 256
     slot = [(len(s) + ALIGN - 1) // ALIGN * ALIGN for s in streams]
-    order = [(rank * n + i) % pool for i in range(n)]  # round-robin pool mapping
+    from zarr_amd.shard import round_robin_ids
+    # chunk g of the job goes to GPU g mod world; its content
+    # is pool entry g mod pool
+    order = [g % pool for g in round_robin_ids(rank, world, n)]
     offs = np.zeros(n + 1, np.int64)
     for i, u in enumerate(order):
         offs[i + 1] = offs[i] + slot[u]
@@ -234,7 +234,8 @@ def encode_leg(codec, n, steps, warmup, pool, rank, world, dev):
     meta, gen, desc_txt = workload(codec)
     vals = [gen(i) for i in range(pool)]
     D = vals[0].nbytes
-    host = np.concatenate([vals[(rank * n + i) % pool].view(np.uint8) for i in range(n)])
+    from zarr_amd.shard import round_robin_ids
+    host = np.concatenate([vals[g % pool].view(np.uint8) for g in round_robin_ids(rank, world, n)])
     elems = torch.from_numpy(host).to(dev)
     bc = BatchCodec(dev.index or 0)
     cap = bc.encode_bound(meta, D)
