@@ -258,6 +258,12 @@ def encode_leg(codec, n, steps, warmup, pool, rank, world, dev):
     ref_ratio = None
     if codec == "gzip":  # C5: ratio of the CPU reference library (zlib level 6) on the same pool
         ref_ratio = round(len(vals) * D / sum(len(gzip_flate2(v.tobytes(), 6)) for v in vals), 3)
+    elif codec == "xz":  # liblzma preset 6 (xz2's XzEncoder) on 8 pool chunks
+        import lzma
+        sub = vals[:8]
+        ref_ratio = round(len(sub) * D / sum(len(lzma.compress(v.tobytes(), format=lzma.FORMAT_XZ,
+                                                               check=lzma.CHECK_CRC64, preset=6))
+                                             for v in sub), 3)
     res = {"workload": desc_txt.replace("decode", "encode"), "direction": "encode",
            "ref_ratio": ref_ratio,
            "value": round(world * n * D * steps / t_max / GIB, 3), "unit": "GiB/s (input)",
@@ -349,6 +355,7 @@ def main():
             per[c] = r
         per["lz4_encode"] = encode_leg("lz4", 1024, 3, 1, args.pool, rank, world, dev)
         per["gzip_encode"] = encode_leg("gzip", 512, 2, 1, args.pool, rank, world, dev)  # C5 shape
+        per["xz_encode"] = encode_leg("xz", 1024, 2, 1, args.pool, rank, world, dev)
         result["per_codec"] = per
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

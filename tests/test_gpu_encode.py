@@ -267,3 +267,74 @@ def test_gzip_encode_quant_ratio():
     for a, s in zip(arrays, outs):
         check_gzip_member(s, a.tobytes(), 6)
     assert ours <= 1.4 * ref, (ours, ref)
+
+
+# ---- Xz (xz.rs:34-43: xz2 XzEncoder = lzma_easy_encoder(preset, CRC64)) ----
+def check_xz_stream(stream: bytes, content: bytes, preset: int):
+    """xz2's container conventions + liblzma (Python lzma = the reference's
+    decoder library) reproduces the content with every check verified."""
+    import lzma
+    assert stream[:12] == bytes.fromhex("fd377a585a000004e6d6b446")  # CRC64 stream
+    assert stream[-2:] == b"YZ" and stream[-4:-2] == b"\x00\x04"
+    if content:
+        lg = [18, 20, 21, 22, 22, 23, 23, 24, 25, 26][6 if preset < 0 or preset > 9 else preset]
+        assert stream[12:20] == bytes([0x02, 0x00, 0x21, 0x01, 2 * (lg - 12), 0, 0, 0])
+    d = lzma.LZMADecompressor(format=lzma.FORMAT_XZ)
+    assert d.decompress(stream) == content and d.eof and not d.unused_data
+
+
+@pytest.mark.parametrize("preset", [0, 6, 9])
+@pytest.mark.parametrize("kind", ["zeros", "uniform", "randwalk", "text", "ramp", "mixed"])
+def test_xz_encode_roundtrip(kind, preset):
+    from zarr_amd.compression import Xz
+    D = 1 << 20
+    arrays = [_data(kind, D, seed=s) for s in range(2)]
+    meta = ArrayMetadata.new([D * 2], [D], "u1", Xz(preset))
+    st, outs = encode_batch(meta, arrays)
+    assert (st == 0).all()
+    for a, s in zip(arrays, outs):
+        content = a.tobytes()
+        check_xz_stream(s, content, preset)
+        rst, dec = zref.decode(zref.XZ, s, D, 1, False, False)
+        assert rst == zref.OK and dec == content
+        back = DefaultChunk.read_chunk(s, meta, [0], np.uint8).get_data()
+        assert back.tobytes() == content
+
+
+@pytest.mark.parametrize("nbytes", [1, 2, 3, 5, 100, 65536, 65537, 300001])
+def test_xz_encode_edge_sizes(nbytes):
+    from zarr_amd.compression import Xz
+    arrays = [_data("text", nbytes, 1), _data("uniform", nbytes, 2), _data("zeros", nbytes)]
+    meta = ArrayMetadata.new([nbytes * 3], [nbytes], "u1", Xz(6))
+    st, outs = encode_batch(meta, arrays)
+    assert (st == 0).all()
+    for a, s in zip(arrays, outs):
+        check_xz_stream(s, a.tobytes(), 6)
+
+
+@pytest.mark.parametrize("dt", ["<i2", ">i2", ">f4", ">u8", "bool", "i1"])
+def test_xz_encode_dtypes(dt):
+    from zarr_amd.compression import Xz
+    rng = np.random.default_rng(6)
+    n = 150001
+    if dt == "bool":
+        data = rng.integers(0, 2, n).astype(bool)
+    else:
+        data = (np.cumsum(rng.integers(-3, 4, n)) % 100).astype(np.dtype(dt).newbyteorder("="))
+    meta = ArrayMetadata.new([n], [n], dt, Xz(6))
+    out = DefaultChunk.write_chunk(meta, SliceDataChunk([0], data))
+    check_xz_stream(out, serialised(data, dt), 6)
+    back = DefaultChunk.read_chunk(out, meta, [0], data.dtype).get_data()
+    assert np.array_equal(back, data)
+
+
+def test_xz_encode_doc_spec_decodes():
+    """tests.rs:147-159 pins xz's doc-spec bytes for liblzma's preset-6
+    encoder; a different LZMA parse is a different (valid) stream, so the GPU
+    stream must decode to the same values through the reference decoder."""
+    from zarr_amd.compression import Xz
+    d = doc_spec()
+    meta = ArrayMetadata.new([5, 6, 7], [1, 2, 3], ">i2", Xz(6))
+    out = DefaultChunk.write_chunk(meta, SliceDataChunk([0, 0, 0], np.array(d["expected_values"], np.int16)))
+    st, dec = zref.decode(zref.XZ, out, 12, 2, True)
+    assert st == zref.OK and np.frombuffer(dec, "<i2").tolist() == d["expected_values"]

@@ -114,7 +114,7 @@ int zcg_codec_on_gpu(int32_t codec, int encode) {
     case ZCG_CODEC_RAW: return 1;
     case ZCG_CODEC_LZ4: return 1;
     case ZCG_CODEC_GZIP: return 1;
-    case ZCG_CODEC_XZ: return encode ? 0 : 1;
+    case ZCG_CODEC_XZ: return 1;
     case ZCG_CODEC_BZIP2: return encode ? 0 : 1;
     default: return 0;
     }
@@ -184,6 +184,7 @@ int zcg_encode_batch(zcg_ctx* ctx, const zcg_array* a, const zcg_chunk* d_chunks
     case ZCG_CODEC_GZIP:
         e = launch_deflate(a, d_chunks, n, d_out_len, d_status, nullptr, 0, s);
         break;
+    case ZCG_CODEC_XZ: e = launch_xz_encode(a, d_chunks, n, d_out_len, d_status, s); break;
     default:
         ctx->err = "codec has no GPU encoder in this build";
         return ZCG_ERR_UNSUPPORTED;
