@@ -68,3 +68,29 @@ def test_bzip2_corruption_sweep():
                 b[p] ^= int(rng.integers(1, 256))
                 streams.append(bytes(b))
             check_many("bzip2", streams, "u1", D)
+
+
+def test_bzip2_two_streams_one_context():
+    """Batches enqueued on two HIP streams of one context must not share the
+    decoder's scratch (zcg_ctx keeps a workspace per stream)."""
+    import torch
+    from zarr_amd import ArrayMetadata
+    from zarr_amd.batch import BatchCodec, PackedStreams
+    from zarr_amd.compression import Bzip2
+    D = 300000
+    vals = [rw(D // 2, seed=s).tobytes() for s in range(6)]
+    streams = [bz2.compress(v, 9) for v in vals]
+    meta = ArrayMetadata.new([D * 6], [D], "u1", Bzip2(9))
+    codec = BatchCodec(0)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    p1 = PackedStreams(streams[:3], D, "cuda:0", slot_copies=8)
+    p2 = PackedStreams(streams[3:], D, "cuda:0", slot_copies=8)
+    for _ in range(2):
+        codec.decode(meta, p1, stream=s1)
+        codec.decode(meta, p2, stream=s2)
+    torch.cuda.synchronize()
+    for p, base in ((p1, 0), (p2, 3)):
+        assert (p.status.cpu().numpy() == 0).all()
+        out = p.dst.cpu().numpy().reshape(p.n, D)
+        for i in range(p.n):
+            assert out[i].tobytes() == vals[base + i % 3]

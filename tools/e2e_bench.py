@@ -22,8 +22,7 @@ sys.path.insert(0, ROOT)
 
 import torch  # noqa: E402  (device memory, streams, pinned host buffers)
 
-from bench import gzip_flate2, quant_chunk  # noqa: E402
-from zarr_amd import ArrayMetadata, Gzip  # noqa: E402
+from bench import build_pool, workload  # noqa: E402
 from zarr_amd.batch import BatchCodec  # noqa: E402
 
 GIB = float(1 << 30)
@@ -31,15 +30,17 @@ GIB = float(1 << 30)
 
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--codec", default="gzip", choices=["gzip", "lz4", "raw", "xz", "bzip2"])
     ap.add_argument("--chunks", type=int, default=1024)
     ap.add_argument("--sub", type=int, default=128)
     ap.add_argument("--streams", type=int, default=3)
     ap.add_argument("--reps", type=int, default=3)
     args = ap.parse_args()
     dev = torch.device("cuda:0")
-    D = 1 << 20
-    uniq = [quant_chunk(i).tobytes() for i in range(32)]
-    streams = [gzip_flate2(u, 6) for u in uniq]
+    meta, gen, _ = workload(args.codec)
+    vals, streams = build_pool(args.codec, meta, gen, 32, 16, dev)
+    uniq = [v.tobytes() for v in vals]
+    D = len(uniq[0])
     n, sub = args.chunks, args.sub
     assert n % sub == 0
     slot = max(len(s) for s in streams)
@@ -53,7 +54,6 @@ def main():
         s = streams[i % len(streams)]
         hs[i * slot:i * slot + len(s)] = np.frombuffer(s, np.uint8)
         lens[i] = len(s)
-    meta = ArrayMetadata.new([256, 256, 4 * n], [256, 256, 4], "<f4", Gzip(6))
     codec = BatchCodec(0)
     ns = args.streams
     strm = [torch.cuda.Stream(device=dev) for _ in range(ns)]
@@ -115,7 +115,7 @@ def main():
     torch.cuda.synchronize()
     dev_s = ev0.elapsed_time(ev1) / 4 * 1e-3
     out = {
-        "what": "e2e gzip decode, pinned host -> H2D -> decode -> D2H -> pinned host",
+        "what": f"e2e {args.codec} decode, pinned host -> H2D -> decode -> D2H -> pinned host",
         "chunks": n, "sub_batch": sub, "streams": ns, "chunk_bytes": D,
         "compressed_bytes": int(lens.sum()),
         "e2e_GiBps": round(n * D / best / GIB, 3),

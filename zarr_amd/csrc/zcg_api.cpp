@@ -19,8 +19,14 @@ struct zcg_ctx {
     int device = 0;
     hipStream_t stream = nullptr;  // internal stream of the host conveniences
     std::string err;
-    void* ws = nullptr;  // device workspace of the batch kernels
-    size_t ws_bytes = 0;
+    // device workspace of the batch kernels, one per stream, so batches
+    // enqueued on different streams of one ctx never share scratch
+    struct Ws {
+        void* stream;
+        void* p;
+        size_t bytes;
+    };
+    std::vector<Ws> ws;
     // host-convenience staging
     void* d_buf = nullptr;
     size_t d_buf_bytes = 0;
@@ -91,7 +97,8 @@ void zcg_destroy(zcg_ctx* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-    if (ctx->ws) (void)hipFree(ctx->ws);
+    for (auto& w : ctx->ws)
+        if (w.p) (void)hipFree(w.p);
     if (ctx->d_buf) (void)hipFree(ctx->d_buf);
     if (ctx->h_pin) (void)hipHostFree(ctx->h_pin);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -157,9 +164,16 @@ int zcg_decode_batch(zcg_ctx* ctx, const zcg_array* a, const zcg_chunk* d_chunks
         break;
     case ZCG_CODEC_XZ: e = launch_xz_decode(a, d_chunks, n, d_status, nullptr, 0, s); break;
     case ZCG_CODEC_BZIP2: {
-        const int r = ensure_dev(ctx, &ctx->ws, &ctx->ws_bytes, bzip2_decode_ws_bytes(a, n));
+        zcg_ctx::Ws* w = nullptr;
+        for (auto& x : ctx->ws)
+            if (x.stream == stream) w = &x;
+        if (!w) {
+            ctx->ws.push_back({stream, nullptr, 0});
+            w = &ctx->ws.back();
+        }
+        const int r = ensure_dev(ctx, &w->p, &w->bytes, bzip2_decode_ws_bytes(a, n));
         if (r != ZCG_OK) return r;
-        e = launch_bzip2_decode(a, d_chunks, n, d_status, ctx->ws, ctx->ws_bytes, s);
+        e = launch_bzip2_decode(a, d_chunks, n, d_status, w->p, w->bytes, s);
         break;
     }
     default: return ZCG_ERR_INVALID_INPUT;
