@@ -171,27 +171,27 @@ ZX_HOT int lzma_symbols(IO& io_r, LzJob& j) {
 
 #define ZX_NORM()                                                \
     do {                                                         \
-        if (ZX_UB(rc_range < (1u << 24))) {                      \
-            if (ZX_UB(ip >= lim)) ZX_STOP();                     \
-            if (ZX_UB(ip >= rlim)) ZX_RET(ST_INVALID);           \
+        if (rc_range < (1u << 24)) {                             \
+            if (ip >= lim) ZX_STOP();                            \
+            if (ip >= rlim) ZX_RET(ST_INVALID);                  \
             rc_range <<= 8;                                      \
             rc_code = (rc_code << 8) | io.in(ip++);              \
-            ZX_U32(rc_range); ZX_U32(rc_code); ZX_U32(ip);       \
         }                                                        \
     } while (0)
-// branch-free binary decision (the hot instruction sequence)
+// branch-free binary decision (the hot instruction sequence); the state is
+// scalar (wave-uniform) here, so the selects below are s_cselect / masks
 #define ZX_BIT(pidx, bitvar)                                     \
     do {                                                         \
         ZX_NORM();                                               \
         const u32 pi_ = (pidx);                                  \
         const u32 p_ = io.pget(pi_);                             \
         const u32 bound_ = (rc_range >> 11) * p_;                \
-        const u32 one_ = ZX_UB(rc_code >= bound_) ? 1u : 0u;     \
-        rc_range = one_ ? rc_range - bound_ : bound_;            \
-        rc_code = one_ ? rc_code - bound_ : rc_code;             \
-        io.pset(pi_, one_ ? p_ - (p_ >> 5) : p_ + ((2048 - p_) >> 5)); \
+        const u32 one_ = rc_code >= bound_ ? 1u : 0u;            \
+        const u32 m_ = 0u - one_;                                \
+        rc_range = bound_ + ((rc_range - bound_ - bound_) & m_); \
+        rc_code -= bound_ & m_;                                  \
+        io.pset(pi_, p_ + (((2048 - p_) >> 5) & ~m_) - ((p_ >> 5) & m_)); \
         bitvar = one_;                                           \
-        ZX_U32(rc_range); ZX_U32(rc_code); ZX_U32(bitvar);       \
     } while (0)
 
         // Structured symbol decoder: one loop iteration per LZMA symbol;
