@@ -40,38 +40,22 @@ struct XzDevIO {
     lu8* ring;
     u32 nprob_cap;
     u64 gfl;  // output bytes already stored to HBM (and fenced)
-    u64 wb;   // input window base
-    u32x4 w;
     int lane;
 
     __device__ __forceinline__ void make_uniform() {
-        n = ru64(n); D = ru64(D); pos = ru64(pos); gfl = ru64(gfl); wb = ru64(wb);
+        n = ru64(n); D = ru64(D); pos = ru64(pos); gfl = ru64(gfl);
         src = (const gu8*)ru64((u64)src); dst = (gu8*)ru64((u64)dst);
         probs = (lu16*)(uintptr_t)__builtin_amdgcn_readfirstlane((u32)(uintptr_t)probs);
         ring = (lu8*)(uintptr_t)__builtin_amdgcn_readfirstlane((u32)(uintptr_t)ring);
-        w.x = __builtin_amdgcn_readfirstlane(w.x); w.y = __builtin_amdgcn_readfirstlane(w.y);
-        w.z = __builtin_amdgcn_readfirstlane(w.z); w.w = __builtin_amdgcn_readfirstlane(w.w);
         nprob_cap = __builtin_amdgcn_readfirstlane(nprob_cap);
     }
-    __device__ __forceinline__ void refill(u64 i) {
-        wb = i;
-        if (i + 16 <= n) {
-            w = *(const gu32x4_ua*)(src + i);
-        } else {
-            u32 t[4] = {0, 0, 0, 0};
-            for (u64 q = i; q < n && q < i + 16; q++) t[(q - i) >> 2] |= (u32)src[q] << (8 * ((q - i) & 3));
-            w = u32x4{t[0], t[1], t[2], t[3]};
-        }
-        w.x = __builtin_amdgcn_readfirstlane(w.x);
-        w.y = __builtin_amdgcn_readfirstlane(w.y);
-        w.z = __builtin_amdgcn_readfirstlane(w.z);
-        w.w = __builtin_amdgcn_readfirstlane(w.w);
-    }
+    // one input byte through the scalar cache: the aligned dword holding it
+    // is loaded with s_load (constant address space), so the read never
+    // crosses the buffer's last aligned dword and needs no lane broadcast
     __device__ __forceinline__ u32 in(u64 i) {
-        u64 d = i - wb;
-        if (d >= 16) { refill(i); d = 0; }
-        const u32 word = d < 8 ? (d < 4 ? w.x : w.y) : (d < 12 ? w.z : w.w);
-        return __builtin_amdgcn_readfirstlane((word >> ((d & 3) * 8)) & 0xFF);
+        const u64 a = (u64)(uintptr_t)(src + i);
+        const u32 w = *(const __attribute__((address_space(4))) u32*)(uintptr_t)(a & ~3ull);
+        return (w >> ((u32)(a & 3) * 8)) & 0xFF;
     }
     // wave-uniform values are moved to SGPRs so the decoder runs on the SALU
     __device__ __forceinline__ u32 pget(u32 i) { return __builtin_amdgcn_readfirstlane(probs[i]); }
@@ -161,8 +145,6 @@ __global__ __launch_bounds__(64) void xz_decode_kernel(const zcg_chunk* __restri
     io.ring = (lu8*)ring;
     io.nprob_cap = NPROB;
     io.gfl = 0;
-    io.wb = ~0ull >> 1;
-    io.w = u32x4{0, 0, 0, 0};
     io.lane = lane;
     int st = zx::xz_decode(io);
     io.finish();

@@ -136,6 +136,49 @@ ZX_INL void sums_add(IndexSums& s, u64 unpadded, u64 usize) {
     s.hash = pair_hash(s.hash, unpadded, usize);
 }
 
+// One adaptive binary decision of the LZMA range decoder (liblzma
+// rc_bit: bound = (range >> 11) * p; code < bound -> bit 0, p += (2048-p)>>5;
+// else bit 1, range -= bound, code -= bound, p -= p>>5).  On the device the
+// state is wave-uniform, and the sequence is written as 14 SALU instructions
+// (one compare, four SCC selects) — the compiler's own lowering of the
+// selects round-trips the compare through a lane mask three times.
+ZX_INL u32 rc_bit(u32& range, u32& code, u32& p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    u32 b, rb, t, q0, q1, bit;
+    ZX_U32(range); ZX_U32(code); ZX_U32(p);  // folded away when already scalar
+    asm("s_lshr_b32 %[b], %[r], 11\n\t"
+        "s_mul_i32 %[b], %[b], %[p]\n\t"
+        "s_sub_u32 %[rb], %[r], %[b]\n\t"
+        "s_sub_u32 %[t], %[c], %[b]\n\t"
+        "s_sub_u32 %[q0], 0x800, %[p]\n\t"
+        "s_lshr_b32 %[q0], %[q0], 5\n\t"
+        "s_add_u32 %[q0], %[p], %[q0]\n\t"
+        "s_lshr_b32 %[q1], %[p], 5\n\t"
+        "s_sub_u32 %[q1], %[p], %[q1]\n\t"
+        "s_cmp_lt_u32 %[c], %[b]\n\t"
+        "s_cselect_b32 %[r], %[b], %[rb]\n\t"
+        "s_cselect_b32 %[c], %[c], %[t]\n\t"
+        "s_cselect_b32 %[p], %[q0], %[q1]\n\t"
+        "s_cselect_b32 %[bit], 0, 1"
+        : [r] "+s"(range), [c] "+s"(code), [p] "+s"(p), [b] "=&s"(b), [rb] "=&s"(rb),
+          [t] "=&s"(t), [q0] "=&s"(q0), [q1] "=&s"(q1), [bit] "=&s"(bit)
+        :
+        : "scc");
+    return bit;
+#else
+    const u32 bound = (range >> 11) * p;
+    if (code < bound) {
+        range = bound;
+        p += (2048 - p) >> 5;
+        return 0;
+    }
+    range -= bound;
+    code -= bound;
+    p -= p >> 5;
+    return 1;
+#endif
+}
+
 // The LZMA symbol loop of one LZMA2 chunk: a separate (non-inlined on the
 // device) function so its ~50 live values get their own register allocation,
 // all 32-bit (the kernel restricts streams and chunks to < 4 GiB).  Returns
@@ -164,19 +207,24 @@ ZX_HOT int lzma_symbols(IO& io_r, LzJob& j) {
     bool full = fullw != 0;
     const u32 pb_mask = (1u << pb) - 1, lp_mask = (1u << lp) - 1;
     int rv = ST_CONT;
-#define ZX_RET(v) do { rv = (v); goto out; } while (0)
-#define ZX_STOP() ZX_RET(full ? ST_OK : ST_EOF)
+    // An input overrun inside a symbol is recorded here and reported at the
+    // next symbol boundary (or at any earlier return, which it overrides);
+    // the rest of that symbol decodes zero bytes, so the bit loops have no
+    // exits.  liblzma returns the same status at the same input position.
+    int frv = ST_CONT;
+#define ZX_RET(v) do { rv = frv != ST_CONT ? frv : (v); goto out; } while (0)
 #define ZX_SET_FULL() do { full = true; u32 ve = (u32)((((u64)ip - 1) / BUFREADER + 1) * BUFREADER); \
                            lim = ve < n ? ve : n; } while (0)
 
-#define ZX_NORM()                                                \
-    do {                                                         \
-        if (rc_range < (1u << 24)) {                             \
-            if (ip >= lim) ZX_STOP();                            \
-            if (ip >= rlim) ZX_RET(ST_INVALID);                  \
-            rc_range <<= 8;                                      \
-            rc_code = (rc_code << 8) | io.in(ip++);              \
-        }                                                        \
+#define ZX_NORM()                                                              \
+    do {                                                                       \
+        if (rc_range < (1u << 24)) {                                           \
+            const bool ok_ = ip < lim && ip < rlim;                            \
+            if (!ok_ && frv == ST_CONT) frv = ip >= lim ? (full ? ST_OK : ST_EOF) : ST_INVALID; \
+            rc_range <<= 8;                                                    \
+            rc_code = (rc_code << 8) | (ok_ ? io.in(ip) : 0u);                 \
+            ip += ok_ ? 1u : 0u;                                               \
+        }                                                                      \
     } while (0)
 // branch-free binary decision (the hot instruction sequence); the state is
 // scalar (wave-uniform) here, so the selects below are s_cselect / masks
@@ -184,14 +232,9 @@ ZX_HOT int lzma_symbols(IO& io_r, LzJob& j) {
     do {                                                         \
         ZX_NORM();                                               \
         const u32 pi_ = (pidx);                                  \
-        const u32 p_ = io.pget(pi_);                             \
-        const u32 bound_ = (rc_range >> 11) * p_;                \
-        const u32 one_ = rc_code >= bound_ ? 1u : 0u;            \
-        const u32 m_ = 0u - one_;                                \
-        rc_range = bound_ + ((rc_range - bound_ - bound_) & m_); \
-        rc_code -= bound_ & m_;                                  \
-        io.pset(pi_, p_ + (((2048 - p_) >> 5) & ~m_) - ((p_ >> 5) & m_)); \
-        bitvar = one_;                                           \
+        u32 p_ = io.pget(pi_);                                   \
+        bitvar = rc_bit(rc_range, rc_code, p_);                  \
+        io.pset(pi_, p_);                                        \
     } while (0)
 
         // Structured symbol decoder: one loop iteration per LZMA symbol;
@@ -210,6 +253,7 @@ ZX_HOT int lzma_symbols(IO& io_r, LzJob& j) {
         for (;;) {
             ZX_U32(rc_range); ZX_U32(rc_code); ZX_U32(state); ZX_U32(ip); ZX_U64(io.pos);
             ZX_U32(rep0); ZX_U32(rep1); ZX_U32(rep2); ZX_U32(rep3);
+            if (frv != ST_CONT) ZX_RET(frv);
             if ((u32)io.pos > u_end) ZX_RET(ST_INVALID);  // more than the declared size
             if ((u32)io.pos == D && !full) ZX_SET_FULL();
             const u32 dlim = chunk_end < D ? chunk_end : D;
@@ -244,8 +288,7 @@ ZX_HOT int lzma_symbols(IO& io_r, LzJob& j) {
                         const u32 mbit = mb & off;
                         ZX_BIT(tb + off + mbit + m, bit);
                         m = (m << 1) | bit;
-                        off &= bit ? mbit : ~mbit;  // leaves matched mode on mismatch
-                        ZX_U32(off); ZX_U32(mb);
+                        off &= mbit ^ (bit - 1u);  // leaves matched mode on mismatch
                     } while (m < 0x100);
                 }
                 io.put(m & 0xFF);
