@@ -258,6 +258,10 @@ def encode_leg(codec, n, steps, warmup, pool, rank, world, dev):
     ref_ratio = None
     if codec == "gzip":  # C5: ratio of the CPU reference library (zlib level 6) on the same pool
         ref_ratio = round(len(vals) * D / sum(len(gzip_flate2(v.tobytes(), 6)) for v in vals), 3)
+    elif codec == "bzip2":  # libbz2 level 9 (bzip2-rs BzEncoder) on 8 pool chunks
+        import bz2
+        sub = vals[:8]
+        ref_ratio = round(len(sub) * D / sum(len(bz2.compress(v.tobytes(), 9)) for v in sub), 3)
     elif codec == "xz":  # liblzma preset 6 (xz2's XzEncoder) on 8 pool chunks
         import lzma
         sub = vals[:8]
@@ -356,6 +360,7 @@ def main():
         per["lz4_encode"] = encode_leg("lz4", 1024, 3, 1, args.pool, rank, world, dev)
         per["gzip_encode"] = encode_leg("gzip", 512, 2, 1, args.pool, rank, world, dev)  # C5 shape
         per["xz_encode"] = encode_leg("xz", 1024, 2, 1, args.pool, rank, world, dev)
+        per["bzip2_encode"] = encode_leg("bzip2", 512, 2, 1, args.pool, rank, world, dev)
         result["per_codec"] = per
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

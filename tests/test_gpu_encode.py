@@ -338,3 +338,127 @@ def test_xz_encode_doc_spec_decodes():
     out = DefaultChunk.write_chunk(meta, SliceDataChunk([0, 0, 0], np.array(d["expected_values"], np.int16)))
     st, dec = zref.decode(zref.XZ, out, 12, 2, True)
     assert st == zref.OK and np.frombuffer(dec, "<i2").tolist() == d["expected_values"]
+
+
+# ---- Bzip2 (bzip.rs:36-45: bzip2-rs BzEncoder = libbz2 BZ2_bzCompressInit(block_size)) ----
+def check_bz2_stream(stream: bytes, content: bytes, level: int):
+    """A single bzip2 stream for this level that libbz2 (Python bz2 = the
+    reference decoder's library) decodes to the content, every block and the
+    stream CRC verified, every block within the level's 100 000*L limit."""
+    import bz2
+    assert stream[:4] == b"BZh" + bytes([0x30 + level])
+    d = bz2.BZ2Decompressor()
+    assert d.decompress(stream) == content and d.eof and not d.unused_data
+
+
+@pytest.mark.parametrize("level", [1, 9])
+@pytest.mark.parametrize("kind", ["zeros", "uniform", "randwalk", "text", "ramp", "mixed"])
+def test_bzip2_encode_roundtrip(kind, level):
+    from zarr_amd.compression import Bzip2
+    D = 1 << 20
+    arrays = [_data(kind, D, seed=s) for s in range(2)]
+    meta = ArrayMetadata.new([D * 2], [D], "u1", Bzip2(level))
+    st, outs = encode_batch(meta, arrays)
+    assert (st == 0).all()
+    for a, s in zip(arrays, outs):
+        content = a.tobytes()
+        check_bz2_stream(s, content, level)
+        rst, dec = zref.decode(zref.BZIP2, s, D, 1, False, False)
+        assert rst == zref.OK and dec == content
+        back = DefaultChunk.read_chunk(s, meta, [0], np.uint8).get_data()
+        assert back.tobytes() == content
+
+
+@pytest.mark.parametrize("nbytes", [1, 2, 3, 4, 5, 6, 255, 256, 259, 1000, 99981, 100000, 300001])
+def test_bzip2_encode_edge_sizes(nbytes):
+    from zarr_amd.compression import Bzip2
+    arrays = [_data("text", nbytes, 1), _data("uniform", nbytes, 2), _data("zeros", nbytes),
+              np.full(nbytes, 0xFB, np.uint8)]
+    meta = ArrayMetadata.new([nbytes * 4], [nbytes], "u1", Bzip2(1))
+    st, outs = encode_batch(meta, arrays)
+    assert (st == 0).all()
+    for a, s in zip(arrays, outs):
+        check_bz2_stream(s, a.tobytes(), 1)
+
+
+def test_bzip2_encode_runs():
+    """RLE1 pieces of every length around 4 and 255 (libbz2 ADD_CHAR_TO_BLOCK),
+    runs that straddle the level-1 block limit."""
+    from zarr_amd.compression import Bzip2
+    rng = np.random.default_rng(3)
+    parts = []
+    for ln in list(range(1, 12)) + [250, 251, 252, 253, 254, 255, 256, 257, 258, 259, 260, 509, 510, 511, 5000]:
+        parts.append(np.full(ln, rng.integers(0, 256), np.uint8))
+    base = np.concatenate(parts)
+    a = np.resize(base, 400000)
+    b = np.concatenate([np.full(99978, 1, np.uint8), np.full(300, 2, np.uint8), np.arange(100, dtype=np.uint8)])
+    b = np.resize(b, 400000)
+    meta = ArrayMetadata.new([800000], [400000], "u1", Bzip2(1))
+    st, outs = encode_batch(meta, [a, b])
+    assert (st == 0).all()
+    for x, s in zip([a, b], outs):
+        check_bz2_stream(s, x.tobytes(), 1)
+
+
+def test_bzip2_encode_empty():
+    from zarr_amd.compression import Bzip2
+    meta = ArrayMetadata.new([0], [0], "u1", Bzip2(9))
+    st, outs = encode_batch(meta, [np.zeros(0, np.uint8)] * 2)
+    assert (st == 0).all()
+    import bz2
+    for s in outs:
+        assert s == bz2.compress(b"", 9)  # "BZh9" + end-of-stream record, CRC 0
+
+
+@pytest.mark.parametrize("dt", ["<i2", ">i2", ">f4", ">u8", "bool", "i1"])
+def test_bzip2_encode_dtypes(dt):
+    from zarr_amd.compression import Bzip2
+    rng = np.random.default_rng(6)
+    n = 150001
+    if dt == "bool":
+        data = rng.integers(0, 2, n).astype(bool)
+    else:
+        data = (np.cumsum(rng.integers(-3, 4, n)) % 100).astype(np.dtype(dt).newbyteorder("="))
+    meta = ArrayMetadata.new([n], [n], dt, Bzip2(9))
+    out = DefaultChunk.write_chunk(meta, SliceDataChunk([0], data))
+    check_bz2_stream(out, serialised(data, dt), 9)
+    back = DefaultChunk.read_chunk(out, meta, [0], data.dtype).get_data()
+    assert np.array_equal(back, data)
+
+
+def test_bzip2_encode_doc_spec_decodes():
+    """bzip.rs:83-84: the reference's own doc-spec bzip2 encode vector is not
+    libbz2's output either, so the GPU stream must decode to the doc-spec
+    values through the reference decoder library."""
+    from zarr_amd.compression import Bzip2
+    d = doc_spec()
+    meta = ArrayMetadata.new([5, 6, 7], [1, 2, 3], ">i2", Bzip2(9))
+    out = DefaultChunk.write_chunk(meta, SliceDataChunk([0, 0, 0], np.array(d["expected_values"], np.int16)))
+    st, dec = zref.decode(zref.BZIP2, out, 12, 2, True)
+    assert st == zref.OK and np.frombuffer(dec, "<i2").tolist() == d["expected_values"]
+
+
+def test_bzip2_encode_quant_ratio():
+    """C2-shaped f32 chunks: same Huffman machinery as libbz2, so the ratio
+    must be close to libbz2 level 9's on the same data."""
+    import bz2
+    from test_gpu_parity import quant_f32
+    from zarr_amd.compression import Bzip2
+    arrays = [quant_f32(s) for s in range(4)]
+    D = arrays[0].nbytes
+    meta = ArrayMetadata.new([256 * 4, 256, 4], [256, 256, 4], "<f4", Bzip2(9))
+    st, outs = encode_batch(meta, arrays)
+    assert (st == 0).all()
+    ours = sum(len(s) for s in outs)
+    ref = sum(len(bz2.compress(a.tobytes(), 9)) for a in arrays)
+    for a, s in zip(arrays, outs):
+        check_bz2_stream(s, a.tobytes(), 9)
+    assert ours <= ref * 1.05, (ours, ref)
+
+
+def test_bzip2_encode_bad_level():
+    from zarr_amd.compression import Bzip2
+    meta = ArrayMetadata.new([100], [100], "u1", Bzip2(0))
+    with pytest.raises(ZarrIOError) as e:
+        DefaultChunk.write_chunk(meta, SliceDataChunk([0], np.zeros(100, np.uint8)))
+    assert e.value.kind == "InvalidInput"

@@ -74,6 +74,21 @@ int ensure_pin(zcg_ctx* ctx, size_t need) {
 
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
+// the workspace of batches enqueued on `stream`, grown to at least `need` bytes
+int stream_ws(zcg_ctx* ctx, void* stream, size_t need, zcg_ctx::Ws** out) {
+    zcg_ctx::Ws* w = nullptr;
+    for (auto& x : ctx->ws)
+        if (x.stream == stream) w = &x;
+    if (!w) {
+        ctx->ws.push_back({stream, nullptr, 0});
+        w = &ctx->ws.back();
+    }
+    if (w->bytes < need) (void)hipStreamSynchronize((hipStream_t)stream);  // old scratch may be in use
+    const int r = ensure_dev(ctx, &w->p, &w->bytes, need);
+    *out = w;
+    return r;
+}
+
 }  // namespace
 
 extern "C" {
@@ -122,7 +137,7 @@ int zcg_codec_on_gpu(int32_t codec, int encode) {
     case ZCG_CODEC_LZ4: return 1;
     case ZCG_CODEC_GZIP: return 1;
     case ZCG_CODEC_XZ: return 1;
-    case ZCG_CODEC_BZIP2: return encode ? 0 : 1;
+    case ZCG_CODEC_BZIP2: return 1;
     default: return 0;
     }
 }
@@ -136,13 +151,16 @@ uint64_t zcg_encode_bound(const zcg_compression* c, uint64_t n) {
         const uint64_t b = (uint64_t)zcg_effective_lz4_block_size(c->lz4_block_size);
         return 15 + (n / b + 1) * (b + 8) + 8;
     }
+    case ZCG_CODEC_BZIP2:  // RLE1 can grow a block by 5/4; Huffman of that stays below 9/8
+        return n + n / 4 + 65536;
     default: return n + n / 8 + 65536;
     }
 }
 
 uint64_t zcg_workspace_bytes(const zcg_array* a, uint32_t n, int encode) {
     if (!a) return 0;
-    if (!encode && a->compression.codec == ZCG_CODEC_BZIP2) return bzip2_decode_ws_bytes(a, n);
+    if (a->compression.codec == ZCG_CODEC_BZIP2)
+        return encode ? bzip2_encode_ws_bytes(a, n) : bzip2_decode_ws_bytes(a, n);
     return 0;
 }
 
@@ -165,13 +183,7 @@ int zcg_decode_batch(zcg_ctx* ctx, const zcg_array* a, const zcg_chunk* d_chunks
     case ZCG_CODEC_XZ: e = launch_xz_decode(a, d_chunks, n, d_status, nullptr, 0, s); break;
     case ZCG_CODEC_BZIP2: {
         zcg_ctx::Ws* w = nullptr;
-        for (auto& x : ctx->ws)
-            if (x.stream == stream) w = &x;
-        if (!w) {
-            ctx->ws.push_back({stream, nullptr, 0});
-            w = &ctx->ws.back();
-        }
-        const int r = ensure_dev(ctx, &w->p, &w->bytes, bzip2_decode_ws_bytes(a, n));
+        const int r = stream_ws(ctx, stream, bzip2_decode_ws_bytes(a, n), &w);
         if (r != ZCG_OK) return r;
         e = launch_bzip2_decode(a, d_chunks, n, d_status, w->p, w->bytes, s);
         break;
@@ -199,6 +211,18 @@ int zcg_encode_batch(zcg_ctx* ctx, const zcg_array* a, const zcg_chunk* d_chunks
         e = launch_deflate(a, d_chunks, n, d_out_len, d_status, nullptr, 0, s);
         break;
     case ZCG_CODEC_XZ: e = launch_xz_encode(a, d_chunks, n, d_out_len, d_status, s); break;
+    case ZCG_CODEC_BZIP2: {
+        const int32_t lv = a->compression.bzip2_block_size;
+        if (lv < 1 || lv > 9) {  // BZ2_bzCompressInit rejects it (bzip2-rs panics)
+            ctx->err = "bzip2 block size must be 1..9";
+            return ZCG_ERR_INVALID_INPUT;
+        }
+        zcg_ctx::Ws* w = nullptr;
+        const int r = stream_ws(ctx, stream, bzip2_encode_ws_bytes(a, n), &w);
+        if (r != ZCG_OK) return r;
+        e = launch_bzip2_encode(a, d_chunks, n, d_out_len, d_status, w->p, w->bytes, s);
+        break;
+    }
     default:
         ctx->err = "codec has no GPU encoder in this build";
         return ZCG_ERR_UNSUPPORTED;

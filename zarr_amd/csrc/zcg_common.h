@@ -239,6 +239,10 @@ uint64_t deflate_ws_bytes(const zcg_array* a, uint32_t n);
 hipError_t launch_bzip2_decode(const zcg_array* a, const zcg_chunk* d_chunks, uint32_t n,
                                int32_t* d_status, void* ws, uint64_t ws_bytes, hipStream_t s);
 uint64_t bzip2_decode_ws_bytes(const zcg_array* a, uint32_t n);
+hipError_t launch_bzip2_encode(const zcg_array* a, const zcg_chunk* d_chunks, uint32_t n,
+                               uint64_t* d_out_len, int32_t* d_status, void* ws, uint64_t ws_bytes,
+                               hipStream_t s);
+uint64_t bzip2_encode_ws_bytes(const zcg_array* a, uint32_t n);
 hipError_t launch_xz_decode(const zcg_array* a, const zcg_chunk* d_chunks, uint32_t n,
                             int32_t* d_status, void* ws, uint64_t ws_bytes, hipStream_t s);
 uint64_t xz_decode_ws_bytes(const zcg_array* a, uint32_t n);
