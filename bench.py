@@ -147,6 +147,20 @@ def barrier(world):
         torch.distributed.barrier()
 
 
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
+
+
+def pmc_traffic(kernel, n):
+    """HBM bytes per launch of `kernel` at batch n, from the committed
+    rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE passes over this same bench leg
+    (tools/pmc_traffic.sh -> tools/pmc_traffic.py), scaled to n chunks."""
+    try:
+        e = json.load(open(TRAFFIC_FILE))["kernels"][kernel]
+    except (OSError, KeyError, ValueError):
+        return None
+    return int(e["traffic_bytes"] * n / e["batch_per_gpu"])
+
+
 def decode_leg(codec, n, steps, warmup, pool, rank, world, dev, threads):
     """Decode `n` device-resident chunks per rank, `steps` timed launches.
     Returns (result dict, vals, streams)."""
@@ -218,7 +232,9 @@ def decode_leg(codec, n, steps, warmup, pool, rank, world, dev, threads):
         "ms_per_step": round(t_max / steps * 1e3, 3), "batch_per_gpu": n, "chunk_bytes": D,
         "compressed_bytes_per_gpu": comp_bytes, "ratio": round(n * D / comp_bytes, 3),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
+                     "traffic": pmc_traffic(KERNEL[codec], n),
+                     "traffic_source": "profiles/r01_pmc_traffic.json (2*FETCH_SIZE + WRITE_SIZE per launch)",
                      "kernel": KERNEL[codec], "kernel_ms": round(kern_ms, 4),
                      "algorithmic_bytes_per_launch": algo_bytes},
     }
