@@ -164,6 +164,44 @@ int zcg_read_chunks_host(zcg_ctx* ctx, const zcg_array* array, uint32_t n,
                          const void* const* srcs, const uint64_t* src_lens, void* const* dsts,
                          int32_t* status);
 
+/* ---- region assembly ----------------------------
+ * Replaces ZarrNdarrayReader::read_ndarray / read_ndarray_into_with_buffer
+ * (ndarray.rs:153-268): decoded chunks that already sit in HBM are
+ * scattered into one bounding box on the device.  Chunk order is the
+ * array's memory layout (ndarray.rs:453-462: ColumnMajor -> dim 0 fastest,
+ * RowMajor -> last dim fastest); the output is any strided view of
+ * bbox_shape (out_strides in elements, ndarray's ArrayViewMut).  Edge chunks
+ * overhang the array and are read over their full nominal extent
+ * (get_chunk_bounds, ndarray.rs:434-446); chunks are the ones
+ * bounded_coord_iter visits (ndarray.rs:410-432). */
+#define ZCG_MAX_DIMS 8
+typedef struct zcg_region {
+    uint32_t ndim;         /* 1..ZCG_MAX_DIMS                                   */
+    uint32_t elem_size;    /* 1, 2, 4, 8 (decoded, host-native element bytes)    */
+    uint32_t chunk_order;  /* 0 = RowMajor (C), 1 = ColumnMajor (F), lib.rs Order */
+    uint32_t fill_missing; /* 1: read_ndarray — every element no chunk covers gets
+                              fill_value (Array::from_elem, ndarray.rs:164-171);
+                              0: read_ndarray_into — such elements are untouched */
+    uint64_t array_shape[ZCG_MAX_DIMS];
+    uint64_t chunk_shape[ZCG_MAX_DIMS];
+    uint64_t bbox_offset[ZCG_MAX_DIMS];
+    uint64_t bbox_shape[ZCG_MAX_DIMS];
+    int64_t out_strides[ZCG_MAX_DIMS]; /* per array dim, in elements */
+    uint64_t fill_value;   /* elem_size low bytes, host order (get_effective_fill_value) */
+} zcg_region;
+
+/* The chunk grid range a region reads: grid_lo[d] .. grid_lo[d]+grid_n[d]
+ * (bounded_coord_iter, ndarray.rs:410-432).  Returns the number of chunks
+ * (0 when the box misses the array). */
+uint64_t zcg_region_grid(const zcg_region* r, uint64_t* grid_lo, uint64_t* grid_n);
+
+/* d_chunk_table: device array of zcg_region_grid() DEVICE pointers to the
+ * decoded chunks (N*elem_size bytes each), C order over the grid range
+ * (dim 0 slowest); NULL = chunk absent (read_chunk -> Ok(None)).  d_out is
+ * the base of the output view.  Asynchronous on `stream`. */
+int zcg_read_region(zcg_ctx* ctx, const zcg_region* r, const void* const* d_chunk_table,
+                    void* d_out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,153 @@
+"""Region assembly on the GPU (read_ndarray / read_ndarray_into,
+ndarray.rs:153-268) against the numpy oracle (oracle/region_ref.py) and the
+reference's own ndarray tests (tests/ndarray.rs)."""
+import itertools
+import os
+import sys
+
+import numpy as np
+import pytest
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
+import region_ref  # noqa: E402  (oracle: checker only)
+
+from test_region_host import ref_test_chunks  # noqa: E402
+from zarr_amd import ArrayMetadata, FilesystemHierarchy, Gzip, Lz4, Raw, SliceDataChunk  # noqa: E402
+from zarr_amd.compression import Bzip2, Xz  # noqa: E402
+from zarr_amd.region import BoundingBox, read_ndarray, read_ndarray_into  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+def test_reference_read_ndarray(tmp_path):
+    """tests/ndarray.rs:14-100 through the filesystem, GPU decode + region."""
+    shape, cs, chunks = ref_test_chunks()
+    h = FilesystemHierarchy.open_or_create(str(tmp_path))
+    meta = ArrayMetadata.new(shape, cs, "<i4")
+    h.create_array("test/array/group", meta)
+    for c, d in chunks.items():
+        h.write_chunk("test/array/group", meta, SliceDataChunk(list(c), d))
+    a = read_ndarray(h, "test/array/group", meta, BoundingBox([0, 5, 4, 3], [3, 35, 15, 7]), np.int32)
+    assert a.flags.f_contiguous
+    x = np.arange(35)[:, None, None]
+    y = np.arange(15)[None, :, None]
+    z = np.arange(7)[None, None, :]
+    assert (a[0] == 1005 + x + 0 * y + 0 * z).all()
+    assert (a[1] == 2004 + y + 0 * x + 0 * z).all()
+    assert (a[2] == 3003 + z + 0 * x + 0 * y).all()
+
+
+def test_reference_read_ndarray_oob(tmp_path):
+    """tests/ndarray.rs:102-133."""
+    h = FilesystemHierarchy.open_or_create(str(tmp_path))
+    meta = ArrayMetadata.new([100, 200], [50, 100], "<i4")
+    h.create_array("test/array/group", meta)
+    d = np.zeros(5000, np.int32)
+    d[0] = 1
+    h.write_chunk("test/array/group", meta, SliceDataChunk([1, 1], d))
+    a = read_ndarray(h, "test/array/group", meta, BoundingBox([45, 175], [50, 50]), np.int32)
+    assert a.shape == (50, 50) and (a == 0).all()
+
+
+def test_reference_write_read_ndarray(tmp_path):
+    """tests/ndarray.rs:135-176: whole chunks written from a random array,
+    read back with read_ndarray (F) and read_ndarray_into a C-order array."""
+    h = FilesystemHierarchy.open_or_create(str(tmp_path))
+    cs = [3, 4, 2, 1]
+    meta = ArrayMetadata.new([3, 300, 200, 100], cs, "<i4", Gzip(6))
+    h.create_array("test/array/group", meta)
+    rng = np.random.default_rng(11)
+    arr = rng.integers(-2**31, 2**31 - 1, (3, 36, 16, 7), dtype=np.int32)
+    off = [0, 4, 4, 3]  # chunk-aligned so every chunk is written whole
+    for c in itertools.product(*[range(o // s, (o + n) // s) for o, n, s in zip(off, arr.shape, cs)]):
+        sl = tuple(slice(ci * s - o, ci * s - o + s) for ci, s, o in zip(c, cs, off))
+        h.write_chunk("test/array/group", meta, SliceDataChunk(list(c), arr[sl].reshape(-1, order="F")))
+    bbox = BoundingBox(off, list(arr.shape))
+    a = read_ndarray(h, "test/array/group", meta, bbox, np.int32)
+    assert np.array_equal(a, arr)
+    a_c = np.zeros(arr.shape, np.int32)
+    read_ndarray_into(h, "test/array/group", meta, bbox, a_c, np.int32)
+    assert np.array_equal(a_c, arr)
+
+
+CODECS = [Raw(), Gzip(1), Lz4(65536), Bzip2(1), Xz(0)]
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_region_random_vs_oracle(tmp_path, seed):
+    """Random shapes/chunks/orders/dtypes/boxes (partly outside the array),
+    missing chunks, overhanging edge chunks, fill values."""
+    rng = np.random.default_rng(100 + seed)
+    nd = int(rng.integers(1, 5))
+    dt = ["<i2", "<u1", "<f8", "<i4", "bool", ">u2", ">f4"][seed % 7]
+    npdt = np.dtype("bool") if dt == "bool" else np.dtype(dt).newbyteorder("=")
+    for attempt in range(50):
+        shape = [int(rng.integers(1, 30 if nd < 3 else 12)) for _ in range(nd)]
+        cs = [int(rng.integers(1, 9)) for _ in range(nd)]
+        off = [int(rng.integers(0, s + 3)) for s in shape]
+        shp = [int(rng.integers(0, 25 if nd < 3 else 10)) for _ in range(nd)]
+        meta = ArrayMetadata.new(shape, cs, dt, CODECS[seed % len(CODECS)])
+        coords = region_ref.bounded_coord_iter(shape, cs, off, shp)
+        if all(meta.in_bounds(c) for c in coords):
+            break
+    meta.chunk_memory_layout = "F" if seed % 2 else "C"
+    if seed % 3 == 0 and dt != "bool":
+        meta.fill_value = 7
+    h = FilesystemHierarchy.open_or_create(str(tmp_path))
+    h.create_array("a", meta)
+    n_el = int(np.prod(cs))
+    chunks = {}
+    grid = [(s + c - 1) // c for s, c in zip(shape, cs)]
+    for c in itertools.product(*[range(g) for g in grid]):
+        if rng.random() < 0.25:
+            continue  # absent chunk -> fill / untouched
+        if dt == "bool":
+            d = rng.integers(0, 2, n_el).astype(bool)
+        elif npdt.kind == "f":
+            d = rng.standard_normal(n_el).astype(npdt)
+        else:
+            d = rng.integers(0, 200, n_el).astype(npdt)
+        chunks[c] = d
+        h.write_chunk("a", meta, SliceDataChunk(list(c), d))
+    fill = 7 if meta.fill_value is not None else 0
+    bbox = BoundingBox(off, shp)
+    want = region_ref.read_ndarray(shape, cs, meta.chunk_memory_layout, off, shp, chunks.get, npdt, fill)
+    got = read_ndarray(h, "a", meta, bbox, npdt)
+    assert got.shape == tuple(shp) and np.array_equal(got, want)
+    # read_ndarray_into keeps what no chunk covers, on a strided view
+    base = np.full([s * 2 for s in shp] or [1], 3 if dt != "bool" else True, dtype=npdt)
+    view = base[tuple(slice(None, None, 2) for _ in shp)]
+    exp = view.copy()
+    region_ref.read_ndarray_into(shape, cs, meta.chunk_memory_layout, off, shp, chunks.get, exp)
+    read_ndarray_into(h, "a", meta, bbox, view, npdt)
+    assert np.array_equal(view, exp)
+
+
+def test_region_device_large_unaligned():
+    """Device-level assembly of a big box straddling chunk boundaries at an
+    odd offset (vector path + run path), against numpy on the host."""
+    import torch
+    from zarr_amd.region import assemble_region
+    meta = ArrayMetadata.new([1000, 600, 40], [100, 64, 8], "<i2")
+    meta.chunk_memory_layout = "C"
+    off, shp = [37, 5, 3], [900, 590, 33]
+    lo = [o // c for o, c in zip(off, meta.chunk_shape)]
+    hi = [(o + s + c - 1) // c for o, s, c in zip(off, shp, meta.chunk_shape)]
+    coords = list(itertools.product(*[range(a, b) for a, b in zip(lo, hi)]))
+    rng = np.random.default_rng(1)
+    full = rng.integers(-30000, 30000, [g * c for g, c in zip(hi, meta.chunk_shape)], dtype=np.int16)
+    N = int(np.prod(meta.chunk_shape))
+    dev = torch.device("cuda", 0)
+    slots = torch.empty(len(coords) * N, dtype=torch.int16, device=dev)
+    host = np.empty((len(coords), N), np.int16)
+    for i, c in enumerate(coords):
+        sl = tuple(slice(ci * s, ci * s + s) for ci, s in zip(c, meta.chunk_shape))
+        host[i] = full[sl].reshape(-1)
+    slots.copy_(torch.from_numpy(host.reshape(-1)))
+    table = torch.tensor([slots.data_ptr() + i * N * 2 for i in range(len(coords))], dtype=torch.int64, device=dev)
+    out = torch.empty(int(np.prod(shp)), dtype=torch.int16, device=dev)
+    st = [shp[1] * shp[2], shp[2], 1]
+    assemble_region(meta, BoundingBox(off, shp), 2, table, out, st, True, 0)
+    torch.cuda.synchronize()
+    want = full[tuple(slice(o, o + s) for o, s in zip(off, shp))]
+    assert np.array_equal(out.cpu().numpy().reshape(shp), want)

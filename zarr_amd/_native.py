@@ -57,6 +57,18 @@ class Chunk(ctypes.Structure):
                 ("dst", ctypes.c_void_p), ("dst_cap", ctypes.c_uint64)]
 
 
+MAX_DIMS = 8
+
+
+class Region(ctypes.Structure):
+    _fields_ = [("ndim", ctypes.c_uint32), ("elem_size", ctypes.c_uint32),
+                ("chunk_order", ctypes.c_uint32), ("fill_missing", ctypes.c_uint32),
+                ("array_shape", ctypes.c_uint64 * MAX_DIMS), ("chunk_shape", ctypes.c_uint64 * MAX_DIMS),
+                ("bbox_offset", ctypes.c_uint64 * MAX_DIMS), ("bbox_shape", ctypes.c_uint64 * MAX_DIMS),
+                ("out_strides", ctypes.c_int64 * MAX_DIMS), ("fill_value", ctypes.c_uint64)]
+
+
+assert ctypes.sizeof(Region) == 16 + 5 * 8 * MAX_DIMS + 8
 assert ctypes.sizeof(Compression) == 24 and ctypes.sizeof(Array) == 40
 assert ctypes.sizeof(Chunk) == 32
 
@@ -106,6 +118,11 @@ def load_library(path: str = LIB_PATH):
         L.zcg_write_chunk.restype = ctypes.c_int
         L.zcg_read_chunks_host.argtypes = [vp, ctypes.POINTER(Array), u32, vp, vp, vp, vp]
         L.zcg_read_chunks_host.restype = ctypes.c_int
+        L.zcg_region_grid.argtypes = [ctypes.POINTER(Region), ctypes.c_void_p, ctypes.c_void_p]
+        L.zcg_region_grid.restype = ctypes.c_uint64
+        L.zcg_read_region.argtypes = [ctypes.c_void_p, ctypes.POINTER(Region), ctypes.c_void_p,
+                                      ctypes.c_void_p, ctypes.c_void_p]
+        L.zcg_read_region.restype = ctypes.c_int
         _lib = L
         return L
 

@@ -5,6 +5,7 @@
 // (src/chunk.rs:270-323) around the device batch kernels.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -335,6 +336,73 @@ int zcg_write_chunk(zcg_ctx* ctx, const zcg_array* a, const void* elems, uint64_
     e = hipMemcpy(out, dp + off_dst, len, hipMemcpyDeviceToHost);
     if (e != hipSuccess) return fail(ctx, e, "D2H");
     *out_len = len;
+    return ZCG_OK;
+}
+
+uint64_t zcg_region_grid(const zcg_region* r, uint64_t* grid_lo, uint64_t* grid_n) {
+    if (!r || r->ndim < 1 || r->ndim > ZCG_MAX_DIMS) return 0;
+    uint64_t cnt = 1;
+    for (uint32_t d = 0; d < r->ndim; d++) {
+        const uint64_t cs = r->chunk_shape[d] ? r->chunk_shape[d] : 1;
+        // bounded_coord_iter (ndarray.rs:410-432): bbox intersected with the
+        // array bounds (BoundingBox::intersect, saturating), floor/ceil by chunk
+        const uint64_t o = r->bbox_offset[d];
+        const uint64_t e = std::min(r->bbox_offset[d] + r->bbox_shape[d], r->array_shape[d]);
+        const uint64_t s = e > o ? e - o : 0;
+        const uint64_t lo = o / cs, hi = (o + s + cs - 1) / cs;
+        if (grid_lo) grid_lo[d] = lo;
+        if (grid_n) grid_n[d] = hi - lo;
+        cnt *= hi - lo;
+    }
+    return cnt;
+}
+
+int zcg_read_region(zcg_ctx* ctx, const zcg_region* r, const void* const* d_chunk_table, void* d_out,
+                    void* stream) {
+    if (!ctx || !r || r->ndim < 1 || r->ndim > ZCG_MAX_DIMS) return ZCG_ERR_INVALID_INPUT;
+    const uint32_t es = r->elem_size;
+    if (es != 1 && es != 2 && es != 4 && es != 8) return ZCG_ERR_INVALID_INPUT;
+    const uint32_t nd = r->ndim;
+    uint64_t lo[ZCG_MAX_DIMS], gn[ZCG_MAX_DIMS];
+    const uint64_t nchunks = zcg_region_grid(r, lo, gn);
+    RegionArgs a{};
+    a.nd = nd;
+    a.es = es;
+    a.fill = r->fill_missing ? 1u : 0u;
+    a.V = 16 / es;
+    a.fillv = r->fill_value;
+    uint64_t tstr_arr[ZCG_MAX_DIMS];
+    {
+        uint64_t st = 1;
+        for (int d = (int)nd - 1; d >= 0; d--) { tstr_arr[d] = st; st *= gn[d]; }
+    }
+    uint64_t total = 1, cst = 1;
+    for (uint32_t k = 0; k < nd; k++) {
+        const uint32_t d = r->chunk_order == 1 ? k : nd - 1 - k;  // fast-first
+        const uint64_t cs = r->chunk_shape[d], bs = r->bbox_shape[d];
+        if (cs == 0 || cs >= (1ull << 32)) return ZCG_ERR_INVALID_INPUT;
+        const uint64_t orr = r->bbox_offset[d] % cs;
+        if (bs + orr >= (1ull << 32)) {
+            ctx->err = "region: box extent along a dimension must stay below 2^32 elements";
+            return ZCG_ERR_UNSUPPORTED;
+        }
+        a.bs[k] = (uint32_t)bs;
+        a.orr[k] = (uint32_t)orr;
+        a.cs[k] = (uint32_t)cs;
+        a.ob[k] = lo[d];
+        a.gn[k] = gn[d];
+        a.tstr[k] = tstr_arr[d];
+        a.cstr[k] = cst;
+        a.ostr[k] = r->out_strides[d];
+        cst *= cs;
+        total *= bs;
+    }
+    a.total = total;
+    if (total == 0) return ZCG_OK;
+    if (!d_out || (nchunks && !d_chunk_table)) return ZCG_ERR_INVALID_INPUT;
+    (void)hipSetDevice(ctx->device);
+    const hipError_t e = launch_region(a, d_chunk_table, d_out, (hipStream_t)stream);
+    if (e != hipSuccess) return fail(ctx, e, "region launch");
     return ZCG_OK;
 }
 

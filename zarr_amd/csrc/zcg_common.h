@@ -14,6 +14,7 @@ typedef uint16_t u16;
 typedef uint32_t u32;
 typedef uint64_t u64;
 typedef int32_t i32;
+typedef int64_t i64;
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
@@ -215,6 +216,22 @@ static __constant__ u32 g_crc32_table[256] = {
     0x54de5729u, 0x23d967bfu, 0xb3667a2eu, 0xc4614ab8u, 0x5d681b02u, 0x2a6f2b94u,
     0xb40bbe37u, 0xc30c8ea1u, 0x5a05df1bu, 0x2d02ef8du};
 
+// Region assembly arguments (zcg_region.hip), built by zcg_read_region.
+struct RegionArgs {
+    u32 nd, es, fill, V;       // dims, element bytes, fill flag, elements per thread (16/es)
+    u64 total;                 // elements in the box
+    u64 fillv;                 // fill element, replicated to 16 bytes below
+    // per dim, fast-first order (the chunks' memory order)
+    u32 bs[ZCG_MAX_DIMS];      // box extent
+    u32 orr[ZCG_MAX_DIMS];     // box offset mod chunk extent
+    u32 cs[ZCG_MAX_DIMS];      // chunk extent
+    u64 ob[ZCG_MAX_DIMS];      // box offset / chunk extent  (= grid_lo)
+    u64 gn[ZCG_MAX_DIMS];      // visited chunks along the dim
+    u64 tstr[ZCG_MAX_DIMS];    // chunk-table stride
+    u64 cstr[ZCG_MAX_DIMS];    // element stride inside a chunk
+    i64 ostr[ZCG_MAX_DIMS];    // element stride of the output view
+};
+
 }  // namespace zcg
 
 // Internal launchers (zcg_*.hip) used by zcg_api.cpp.
@@ -246,6 +263,8 @@ uint64_t bzip2_encode_ws_bytes(const zcg_array* a, uint32_t n);
 hipError_t launch_xz_decode(const zcg_array* a, const zcg_chunk* d_chunks, uint32_t n,
                             int32_t* d_status, void* ws, uint64_t ws_bytes, hipStream_t s);
 uint64_t xz_decode_ws_bytes(const zcg_array* a, uint32_t n);
+struct RegionArgs;
+hipError_t launch_region(const RegionArgs& a, const void* const* d_table, void* d_out, hipStream_t s);
 hipError_t launch_xz_encode(const zcg_array* a, const zcg_chunk* d_chunks, uint32_t n,
                             uint64_t* d_out_len, int32_t* d_status, hipStream_t s);
 }  // namespace zcg
