@@ -295,6 +295,55 @@ def encode_leg(codec, n, steps, warmup, pool, rank, world, dev):
     return res
 
 
+def region_leg(steps, dev):
+    """Region assembly (read_ndarray's scatter, ndarray.rs:195-268) of 1 024
+    decoded f32 256x256x4 chunks (1 GiB, F order) already in HBM into a box
+    at an unaligned offset; roofline bytes = box bytes read + written."""
+    import torch
+    from zarr_amd import ArrayMetadata
+    from zarr_amd.region import BoundingBox, assemble_region, region_grid, _strides
+    meta = ArrayMetadata.new([256 * 32, 256 * 32, 4], [256, 256, 4], "<f4")
+    off, shp = [100, 37, 0], [256 * 32 - 200, 256 * 32 - 100, 4]
+    bbox = BoundingBox(off, shp)
+    lo, n = region_grid(meta, bbox)
+    N = 256 * 256 * 4
+    nch = n[0] * n[1] * n[2]
+    g = torch.Generator(device=dev).manual_seed(3)
+    slots = torch.randint(-2**31, 2**31 - 1, (nch * N,), dtype=torch.int32, device=dev, generator=g)
+    table = torch.tensor([slots.data_ptr() + i * N * 4 for i in range(nch)], dtype=torch.int64, device=dev)
+    total = shp[0] * shp[1] * shp[2]
+    out = torch.empty(total, dtype=torch.int32, device=dev)
+    st = _strides(shp, "F")
+    stream = torch.cuda.current_stream(dev)
+    assemble_region(meta, bbox, 4, table, out, st, True, 0, dev.index or 0, stream)
+    torch.cuda.synchronize()
+    # gate: 4096 random elements against the index math of ndarray.rs:234-258
+    rng = np.random.default_rng(0)
+    idx = [rng.integers(0, s, 4096) for s in shp]
+    gpos = [i + o for i, o in zip(idx, off)]
+    c = [p // cs for p, cs in zip(gpos, meta.chunk_shape)]
+    w = [p % cs for p, cs in zip(gpos, meta.chunk_shape)]
+    ci = (c[0] - lo[0]) * n[1] * n[2] + (c[1] - lo[1]) * n[2] + (c[2] - lo[2])
+    src = torch.from_numpy(ci * N + w[0] + 256 * (w[1] + 256 * w[2])).to(dev)
+    dst = torch.from_numpy(idx[0] + shp[0] * (idx[1] + shp[1] * idx[2])).to(dev)
+    assert bool((out[dst] == slots[src]).all()), "region: assembled elements differ"
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record(stream)
+    for _ in range(steps):
+        assemble_region(meta, bbox, 4, table, out, st, True, 0, dev.index or 0, stream)
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    ms = ev0.elapsed_time(ev1) / steps
+    byts = 2 * total * 4
+    achieved = byts / (ms * 1e-3) / 1e9
+    return {"workload": "read_ndarray region assembly: 1024 decoded f32 256x256x4 chunks (F order) -> "
+                        f"box {shp} at offset {off}", "value": round(total * 4 / (ms * 1e-3) / GIB, 2),
+            "unit": "GiB/s (box)", "ms_per_step": round(ms, 3),
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "kernel": "zcg::region_rows_kernel",
+                         "algorithmic_bytes_per_launch": byts}}
+
+
 CPU_LIB = {"gzip": "zlib 1.2.11 inflate + flate2 header rules",
            "lz4": "liblz4 1.9.3 LZ4F (lz4-rs feeding)", "raw": "memcpy",
            "xz": "liblzma 5.2.5 stream decoder (xz2 feeding)",
@@ -377,6 +426,7 @@ def main():
         per["gzip_encode"] = encode_leg("gzip", 512, 2, 1, args.pool, rank, world, dev)  # C5 shape
         per["xz_encode"] = encode_leg("xz", 1024, 2, 1, args.pool, rank, world, dev)
         per["bzip2_encode"] = encode_leg("bzip2", 512, 2, 1, args.pool, rank, world, dev)
+        per["region"] = region_leg(max(3, args.steps), dev)
         result["per_codec"] = per
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

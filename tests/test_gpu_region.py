@@ -151,3 +151,47 @@ def test_region_device_large_unaligned():
     torch.cuda.synchronize()
     want = full[tuple(slice(o, o + s) for o, s in zip(off, shp))]
     assert np.array_equal(out.cpu().numpy().reshape(shp), want)
+
+
+@pytest.mark.parametrize("es,order,ostride_c", [(2, "F", False), (8, "F", False), (1, "C", False),
+                                                 (4, "F", True)])
+def test_region_device_long_rows(es, order, ostride_c):
+    """Row-per-wave path (long fast dimension): unaligned offsets, chunk
+    boundaries inside 16-byte pieces, absent chunks with fill, and a
+    non-unit output stride along the fast dimension."""
+    import torch
+    from zarr_amd.region import assemble_region, region_grid, _strides
+    dt = {1: np.uint8, 2: np.int16, 4: np.int32, 8: np.int64}[es]
+    meta = ArrayMetadata.new([700, 50, 9], [301, 7, 4], {1: "u1", 2: "<i2", 4: "<i4", 8: "<i8"}[es])
+    meta.chunk_memory_layout = order
+    if order == "C":
+        meta = ArrayMetadata.new([9, 50, 700], [4, 7, 301], "u1")
+        meta.chunk_memory_layout = "C"
+        off, shp = [1, 3, 13], [8, 40, 680]
+    else:
+        off, shp = [13, 3, 1], [680, 40, 8]
+    bbox = BoundingBox(off, shp)
+    lo, n = region_grid(meta, bbox)
+    coords = list(itertools.product(*[range(a, a + k) for a, k in zip(lo, n)]))
+    cs = meta.chunk_shape
+    N = int(np.prod(cs))
+    rng = np.random.default_rng(es)
+    full = rng.integers(0, 120, [(l + k) * c for l, k, c in zip(lo, n, cs)]).astype(dt)
+    dev = torch.device("cuda", 0)
+    host = np.empty((len(coords), N), dt)
+    absent = set(i for i in range(len(coords)) if rng.random() < 0.2)
+    for i, c in enumerate(coords):
+        sl = tuple(slice(ci * s, ci * s + s) for ci, s in zip(c, cs))
+        host[i] = full[sl].reshape(-1, order=order)
+        if i in absent:
+            full[sl] = 99
+    slots = torch.from_numpy(host.reshape(-1).view(np.uint8).copy()).to(dev)
+    table = torch.tensor([0 if i in absent else slots.data_ptr() + i * N * es for i in range(len(coords))],
+                         dtype=torch.int64, device=dev)
+    st = _strides(shp, "C" if ostride_c else order)
+    out = torch.zeros(int(np.prod(shp)) * es, dtype=torch.uint8, device=dev)
+    assemble_region(meta, bbox, es, table, out, st, True, 99)
+    torch.cuda.synchronize()
+    got = np.ndarray(tuple(shp), dtype=dt, buffer=out.cpu().numpy(), strides=tuple(s * es for s in st))
+    want = full[tuple(slice(o, o + s) for o, s in zip(off, shp))]
+    assert np.array_equal(got, want)

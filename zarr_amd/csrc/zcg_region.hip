@@ -141,10 +141,97 @@ __global__ __launch_bounds__(RG_T) void region_kernel(RegionArgs a, const u8* co
     }
 }
 
+// Long box rows (the common case: the fast dimension spans many 16-byte
+// pieces): one wave per box row.  The row's coordinates, chunk-table and
+// chunk-offset contributions of the slow dimensions are scalar, computed once
+// per row; lanes stream the row 16 bytes each.
+__global__ __launch_bounds__(RG_T) void region_rows_kernel(RegionArgs a, u64 nrows,
+                                                           const u8* const* __restrict__ table,
+                                                           u8* __restrict__ out) {
+    const u32 lane = threadIdx.x & 63;
+    const u64 wid = ((u64)blockIdx.x * RG_T + threadIdx.x) >> 6;
+    const u64 nwaves = ((u64)gridDim.x * RG_T) >> 6;
+    u64 fv = a.fillv;
+    if (a.es == 1) fv = (fv & 0xFF) * 0x0101010101010101ull;
+    else if (a.es == 2) fv = (fv & 0xFFFF) * 0x0001000100010001ull;
+    else if (a.es == 4) fv = (fv & 0xFFFFFFFFull) * 0x0000000100000001ull;
+    const u32x4 fill16 = {(u32)fv, (u32)(fv >> 32), (u32)fv, (u32)(fv >> 32)};
+    const u32 V = a.V, bs0 = a.bs[0], cs0 = a.cs[0], orr0 = a.orr[0];
+    const i64 es = a.es;
+    for (u64 row = ru64(wid); row < nrows; row += nwaves) {
+        // slow-dimension coordinates of this row (scalar)
+        u64 e = row, ti = 0, wi = 0;
+        i64 drow = 0;
+        bool ok = true;
+        for (u32 k = 1; k < ZCG_MAX_DIMS; k++) {
+            if (k >= a.nd) break;
+            const u64 qd = e / a.bs[k];
+            const u32 x = (u32)(e - qd * a.bs[k]);
+            e = qd;
+            const u32 r = a.orr[k] + x;
+            const u32 q = r / a.cs[k];
+            ok &= (u64)q < a.gn[k];
+            ti += (u64)q * a.tstr[k];
+            wi += (u64)(r - q * a.cs[k]) * a.cstr[k];
+            drow += (i64)x * a.ostr[k];
+        }
+        u8* drow_p = out + drow * es;
+        // four pieces per lane in flight: loads first, then stores
+        constexpr u32 U = 4;
+        for (u32 xb = lane * V; xb < bs0; xb += U * 64 * V) {
+            u32x4 v[U];
+            u8* dp[U];
+            u32 mode[U];  // 0 skip, 1 load+store, 2 fill, 3 element runs
+#pragma unroll
+            for (u32 u = 0; u < U; u++) {
+                const u32 x0 = xb + u * 64 * V;
+                mode[u] = 0;
+                dp[u] = drow_p + (i64)x0 * a.ostr[0] * es;
+                if (x0 >= bs0) continue;
+                const u32 r = orr0 + x0;
+                const u32 q = r / cs0;
+                const u32 w0 = r - q * cs0;
+                const bool here = ok && (u64)q < a.gn[0];
+                const u8* base = here ? table[ti + (u64)q * a.tstr[0]] : nullptr;
+                if (!(bs0 - x0 >= V && w0 + V <= cs0 && a.ostr[0] == 1)) { mode[u] = 3; continue; }
+                if (base) { v[u] = ld16(base + (wi + w0) * (u64)es); mode[u] = 1; }
+                else if (a.fill) { v[u] = fill16; mode[u] = 2; }
+            }
+#pragma unroll
+            for (u32 u = 0; u < U; u++)
+                if (mode[u] == 1 || mode[u] == 2) st16(dp[u], v[u]);
+#pragma unroll
+            for (u32 u = 0; u < U; u++) {
+                if (mode[u] != 3) continue;
+                const u32 x0 = xb + u * 64 * V;
+                const u32 rem = bs0 - x0 < V ? bs0 - x0 : V;
+                // the piece crosses a chunk boundary or ends the row: per element
+                for (u32 j = 0; j < rem; j++) {
+                    const u32 rj = orr0 + x0 + j;
+                    const u32 qj = rj / cs0;
+                    const bool hj = ok && (u64)qj < a.gn[0];
+                    const u8* bj = hj ? table[ti + (u64)qj * a.tstr[0]] : nullptr;
+                    u8* dj = drow_p + (i64)(x0 + j) * a.ostr[0] * es;
+                    if (bj) copy_elem(dj, bj + (wi + (rj - qj * cs0)) * (u64)es, a.es);
+                    else if (a.fill) fill_elem(dj, fv, a.es);
+                }
+            }
+        }
+    }
+}
+
 }  // namespace
 
 hipError_t launch_region(const RegionArgs& a, const void* const* d_table, void* d_out, hipStream_t s) {
     if (a.total == 0) return hipSuccess;
+    if (a.bs[0] >= 32u * a.V) {  // long rows: a wave per row
+        const u64 nrows = a.total / a.bs[0];
+        const u64 wgs = (nrows + 3) / 4;
+        const u32 grid = (u32)(wgs < 65536 ? wgs : 65536);
+        hipLaunchKernelGGL(region_rows_kernel, dim3(grid), dim3(RG_T), 0, s, a, nrows, (const u8* const*)d_table,
+                           (u8*)d_out);
+        return hipGetLastError();
+    }
     const u64 tiles = (a.total + (u64)RG_T * a.V - 1) / ((u64)RG_T * a.V);
     const u32 grid = (u32)(tiles < 262144 ? tiles : 262144);
     hipLaunchKernelGGL(region_kernel, dim3(grid), dim3(RG_T), 0, s, a, (const u8* const*)d_table, (u8*)d_out);
