@@ -49,8 +49,9 @@ def test_struct_layout_matches_header():
 #include <stdio.h>
 #include "zchunk_gpu.h"
 #include <stddef.h>
-int main(){printf("%zu %zu %zu %zu %zu\n", sizeof(zcg_compression), sizeof(zcg_dtype),
- sizeof(zcg_array), sizeof(zcg_chunk), offsetof(zcg_array, chunk_num_elements));return 0;}
+int main(){printf("%zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(zcg_compression), sizeof(zcg_dtype),
+ sizeof(zcg_array), sizeof(zcg_chunk), offsetof(zcg_array, chunk_num_elements), sizeof(zcg_region),
+ offsetof(zcg_region, out_strides), offsetof(zcg_region, fill_value));return 0;}
 '''
     with tempfile.TemporaryDirectory() as d:
         c = os.path.join(d, "t.c")
@@ -60,4 +61,5 @@ int main(){printf("%zu %zu %zu %zu %zu\n", sizeof(zcg_compression), sizeof(zcg_d
         out = subprocess.run([exe], check=True, capture_output=True, text=True).stdout.split()
     assert [int(x) for x in out] == [ctypes.sizeof(_native.Compression), ctypes.sizeof(_native.DType),
                                      ctypes.sizeof(_native.Array), ctypes.sizeof(_native.Chunk),
-                                     _native.Array.chunk_num_elements.offset]
+                                     _native.Array.chunk_num_elements.offset, ctypes.sizeof(_native.Region),
+                                     _native.Region.out_strides.offset, _native.Region.fill_value.offset]

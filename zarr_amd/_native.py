@@ -29,6 +29,7 @@ EXPORTED_SYMBOLS = (
     "zcg_effective_gzip_level", "zcg_effective_lz4_block_size", "zcg_codec_on_gpu",
     "zcg_decode_batch", "zcg_encode_batch", "zcg_encode_bound", "zcg_workspace_bytes",
     "zcg_read_chunk", "zcg_write_chunk", "zcg_read_chunks_host",
+    "zcg_region_grid", "zcg_read_region",
 )
 
 
