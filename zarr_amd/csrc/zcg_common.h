@@ -266,5 +266,7 @@ uint64_t xz_decode_ws_bytes(const zcg_array* a, uint32_t n);
 struct RegionArgs;
 hipError_t launch_region(const RegionArgs& a, const void* const* d_table, void* d_out, hipStream_t s);
 hipError_t launch_xz_encode(const zcg_array* a, const zcg_chunk* d_chunks, uint32_t n,
-                            uint64_t* d_out_len, int32_t* d_status, hipStream_t s);
+                            uint64_t* d_out_len, int32_t* d_status, void* ws, uint64_t ws_bytes,
+                            hipStream_t s);
+uint64_t xz_encode_ws_bytes(const zcg_array* a, uint32_t n);
 }  // namespace zcg

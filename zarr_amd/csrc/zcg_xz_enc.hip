@@ -9,23 +9,36 @@
 // (stream flags 00 04, block header 02 00 21 01 <dict prop> 00 00 00 + CRC32,
 // LZMA2 lc=3 lp=0 pb=2 as in every liblzma preset).
 //
-// One wave per chunk, wave-uniform like the decoder (zcg_xz_core.h):
-//   * greedy parse: at each position the rep0 candidate and a 4-byte-hash
-//     candidate (4 096-entry LDS table) are measured 64 bytes per step with a
-//     wave ballot; a rep0 match of >= 2 that is not shorter than the hash
-//     match by more than one byte wins (LZMA codes rep0 matches cheaply);
+// Match finding runs ahead of the coder, data-parallel over every position of
+// a sub-batch (<= 128 MiB of input), so the whole chunk is the dictionary as in
+// liblzma (whose presets' dictionaries cover a 1 MiB chunk):
+//   * xe_keys + a hipCUB radix sort of (chunk, 20-bit hash of 4 bytes) keys
+//     with the positions as values (stable: ascending positions per key);
+//   * xe_chain: each position's predecessor with the same key = hash chain;
+//   * xe_best: one thread per position walks its chain up to XE_DEPTH
+//     candidates inside the preset's dictionary and keeps the longest match
+//     (nearest on ties), up to XE_NICE bytes (then it stops walking).
+// The coder is one wave per chunk, wave-uniform like the decoder (zcg_xz_core.h):
+//   * parse: at each position the rep0 candidate (measured 64 bytes per step
+//     with a wave ballot) and the precomputed best match; a rep0 match of >= 2
+//     that is not shorter than the best match by more than one byte wins
+//     (LZMA codes rep0 cheaply); one-step lazy evaluation (a literal when the
+//     next position's match is longer by more than one byte);
 //   * the LZMA range encoder (the decoder's model, LDS probabilities) emits
 //     bytes into a lane-distributed 64-byte staging group, stored coalesced;
 //   * LZMA2 chunks end before 64 KiB of compressed data (chunk header
 //     patched in place), the first with dictionary + state reset and props;
 //   * CRC64 of the serialised chunk by 64 lane segments (zcg_crc.h).
 // '>'-types and bool are serialised on the fly (write_data, chunk.rs:118-140).
+#include <hipcub/hipcub.hpp>
+
 #include "zcg_common.h"
 #include "zcg_crc.h"
 
 namespace zcg {
 
-constexpr u32 XE_HBITS = 12;
+constexpr u32 XE_DEPTH = 16;  // hash-chain candidates per position (liblzma fast mode: 4 + nice/4)
+constexpr u32 XE_NICE = 64;   // stop walking at a match this long
 constexpr u32 XE_PROBS = 1846 + (0x300u << 3);  // lc + lp = 3
 constexpr u32 XE_CMAX = 65536 - 64;             // compressed bytes per LZMA2 chunk (+ margin)
 constexpr u32 XE_UMAX = (1u << 21) - 273;       // uncompressed bytes per LZMA2 chunk
@@ -198,14 +211,17 @@ __device__ __forceinline__ u32 xe_match_len(const XeEnc& e, u64 a, u64 b, u32 mx
     return mx;
 }
 
-__global__ __launch_bounds__(64) void xz_encode_kernel(const zcg_chunk* __restrict__ chunks, u32 nch,
+__global__ __launch_bounds__(64) void xz_encode_kernel(const zcg_chunk* __restrict__ chunks, u32 c0, u32 cnt,
                                                        u64 D, DType t, int preset,
+                                                       const u16* __restrict__ g_blen,
+                                                       const u32* __restrict__ g_bdist,
                                                        u64* __restrict__ out_len,
                                                        i32* __restrict__ status) {
     __shared__ u16 probs[XE_PROBS];
-    __shared__ u32 htab[1u << XE_HBITS];
-    const u32 c = blockIdx.x;
-    if (c >= nch) return;
+    if (blockIdx.x >= cnt) return;
+    const u32 c = c0 + blockIdx.x;
+    const u16* blen = g_blen + (u64)blockIdx.x * D;    // best match length per position (0: none)
+    const u32* bdist = g_bdist + (u64)blockIdx.x * D;  // its distance (p - q)
     const int lane = lane_id();
     const zcg_chunk ch = chunks[c];
     XeEnc e;
@@ -243,9 +259,23 @@ __global__ __launch_bounds__(64) void xz_encode_kernel(const zcg_chunk* __restri
         const u64 cdata0 = e.pos;
 
         for (u32 i = lane; i < XE_PROBS; i += 64) probs[i] = 1024;
-        for (u32 i = lane; i < (1u << XE_HBITS); i += 64) htab[i] = 0;
         u32 state = 0, rep0 = 0;
         bool first = true;
+        // Per-lane window of 64 consecutive positions: the serialised byte, the
+        // byte rep0 + 1 back, and the precomputed best match, so literal runs
+        // need no dependent memory access per position.
+        u64 wb = 0;
+        u32 wrep = 0xFFFFFFFFu, wbyte = 0, wrb = 0, wlen = 0, wdist = 0;
+        auto refill = [&](u64 base) {
+            wb = base;
+            wrep = rep0;
+            const u64 q = base + (u64)lane;
+            const bool in = q < n;
+            wbyte = in ? e.sb(q) : 0u;
+            wrb = (in && q > rep0) ? e.sb(q - rep0 - 1) : 0x100u;
+            wlen = in ? (u32)blen[q] : 0u;
+            wdist = in ? bdist[q] : 0u;
+        };
         u64 p = 0;
         while (p < n) {
             // ---- one LZMA2 chunk ----
@@ -258,17 +288,26 @@ __global__ __launch_bounds__(64) void xz_encode_kernel(const zcg_chunk* __restri
             while (p < n && (p - u0) < XE_UMAX && (e.pos - data0) + e.cache_size + 5 < XE_CMAX) {
                 const u32 ps = (u32)p & ((1u << XE_PB) - 1);
                 const u32 mx = (n - p) < 273 ? (u32)(n - p) : 273u;
+                // the 64-position window [wb, wb+64) holds p-1 .. p+1 for the current rep0
+                if (p + 1 >= wb + 64 || p < wb + (p ? 1 : 0) || rep0 != wrep) refill(p ? p - 1 : 0);
+                const u32 i = (u32)(p - wb);
+                const u32 sym = __builtin_amdgcn_readlane(wbyte, i);
                 u32 rl = 0, hl = 0, hd = 0;
-                if (p > rep0 && mx >= 2) rl = xe_match_len(e, p, p - rep0 - 1, mx);
+                if (p > rep0 && mx >= 2 && sym == (u32)__builtin_amdgcn_readlane(wrb, i) &&
+                    __builtin_amdgcn_readlane(wbyte, i + 1) == __builtin_amdgcn_readlane(wrb, i + 1))
+                    rl = xe_match_len(e, p, p - rep0 - 1, mx);
                 if (mx >= 4) {
-                    const u32 x = e.sb(p) | (e.sb(p + 1) << 8) | (e.sb(p + 2) << 16) | (e.sb(p + 3) << 24);
-                    const u32 h = (x * 2654435761u) >> (32 - XE_HBITS);
-                    const u32 cand = htab[h];
-                    htab[h] = (u32)p + 1;
-                    if (cand && (u64)p - cand < dsize) {  // within the declared dictionary
-                        hd = (u32)p - cand;  // 0-based distance: p - (cand - 1) - 1
-                        hl = xe_match_len(e, p, cand - 1, mx);
-                        if (hl < 4) hl = 0;
+                    hl = __builtin_amdgcn_readlane(wlen, i);
+                    if (hl >= 4) {
+                        hd = __builtin_amdgcn_readlane(wdist, i) - 1;  // 0-based distance
+                        if (hl > mx) hl = mx;
+                        // lazy: the next position's match is longer by more than one byte
+                        if (p + 1 < n && hl < XE_NICE && rl + 1 < hl) {
+                            const u32 nl = __builtin_amdgcn_readlane(wlen, i + 1);
+                            if (nl > hl + 1) { hl = 0; rl = 0; }
+                        }
+                    } else {
+                        hl = 0;
                     }
                 }
                 if (rl >= 2 && rl + 1 >= hl) {
@@ -289,16 +328,15 @@ __global__ __launch_bounds__(64) void xz_encode_kernel(const zcg_chunk* __restri
                     state = state < 7 ? 7 : 10;
                     p += hl;
                 } else {
-                    const u32 sym = e.sb(p);
-                    const u32 prev = p ? e.sb(p - 1) : 0u;
+                    const u32 prev = p ? (u32)__builtin_amdgcn_readlane(wbyte, i - 1) : 0u;
                     const u32 base = E_LITERAL + 0x300u * (prev >> (8 - XE_LC));
                     e.bit(E_IS_MATCH + (state << 4) + ps, 0);
                     if (state < 7) {
                         e.tree(base, 8, sym);
                     } else {
-                        u32 mb = e.sb(p - rep0 - 1), off = 0x100, m = 1;
-                        for (int i = 7; i >= 0; i--) {
-                            const u32 b = (sym >> i) & 1;
+                        u32 mb = __builtin_amdgcn_readlane(wrb, i), off = 0x100, m = 1;
+                        for (int k = 7; k >= 0; k--) {
+                            const u32 b = (sym >> k) & 1;
                             mb <<= 1;
                             const u32 mbit = mb & off;
                             e.bit(base + off + mbit + m, b);
@@ -372,14 +410,167 @@ __global__ __launch_bounds__(64) void xz_encode_kernel(const zcg_chunk* __restri
     }
 }
 
+namespace {
+
+constexpr u32 XE_KEYBITS = 20;            // hash bits of the match-finder keys
+constexpr u64 XE_SUB_BYTES = 128ull << 20;  // input bytes per match-finder sub-batch (sort scratch)
+constexpr u64 XE_SUPER_BYTES = 1ull << 30;  // input bytes per coder launch (match arrays kept)
+
+struct XeLayout {
+    u32 m;    // chunks per match-finder sub-batch
+    u32 sm;   // chunks per coder launch (a multiple of m)
+    u64 tot;  // m * D positions
+    u64 cub_bytes;
+    u64 off_ka, off_kb, off_va, off_vb, off_prev, off_blen, off_bdist, off_cub, total;
+};
+
+XeLayout xe_layout(u64 D, u32 n) {
+    XeLayout y{};
+    u64 m = D ? XE_SUB_BYTES / D : n;
+    if (m < 1) m = 1;
+    if (m > n) m = n;
+    if (m > 4096) m = 4096;
+    y.m = (u32)m;
+    y.tot = m * D;
+    u64 sm = D ? XE_SUPER_BYTES / D : n;
+    sm = sm / m * m;
+    if (sm < m) sm = m;
+    if (sm > n) sm = n;
+    y.sm = (u32)sm;
+    size_t cb = 0;
+    hipcub::DoubleBuffer<u32> k(nullptr, nullptr), v(nullptr, nullptr);
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, cb, k, v, (int)(y.tot ? y.tot : 1), 0, 32);
+    y.cub_bytes = (cb + 511) & ~255ull;
+    u64 p = 0;
+    auto take = [&](u64 bytes) { const u64 o = p; p = (p + bytes + 255) & ~255ull; return o; };
+    y.off_ka = take(4 * y.tot);
+    y.off_kb = take(4 * y.tot);
+    y.off_va = take(4 * y.tot);
+    y.off_vb = take(4 * y.tot);
+    y.off_prev = take(4 * y.tot);
+    y.off_blen = take(2 * (u64)y.sm * D);
+    y.off_bdist = take(4 * (u64)y.sm * D);
+    y.off_cub = take(y.cub_bytes);
+    y.total = p;
+    return y;
+}
+
+// serialised bytes x..x+3 of a chunk (little-endian in the result)
+__device__ __forceinline__ u32 xe_ser4(const u8* src, u64 x, const DType& t) {
+    if (!t.swap && !t.isbool) return ld32(src + x);
+    return (u32)norm_byte(src[swap_pos(x, t)], t) | ((u32)norm_byte(src[swap_pos(x + 1, t)], t) << 8) |
+           ((u32)norm_byte(src[swap_pos(x + 2, t)], t) << 16) | ((u32)norm_byte(src[swap_pos(x + 3, t)], t) << 24);
+}
+
+__device__ __forceinline__ u32 xe_ser1(const u8* src, u64 x, const DType& t) {
+    return norm_byte(src[swap_pos(x, t)], t);
+}
+
+__global__ void xe_keys(const zcg_chunk* __restrict__ chunks, u32 c0, u64 D, u64 tot, DType t, u32 cshift,
+                        u32* __restrict__ keys, u32* __restrict__ vals) {
+    const u64 g = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= tot) return;
+    const u32 cl = (u32)(g / D);
+    const u64 p = g - (u64)cl * D;
+    u32 h = 0;
+    if (p + 4 <= D) h = (xe_ser4((const u8*)chunks[c0 + cl].src, p, t) * 2654435761u) >> (32 - XE_KEYBITS);
+    keys[g] = (cl << cshift) | h;
+    vals[g] = (u32)g;
+}
+
+__global__ void xe_chain(u64 tot, const u32* __restrict__ keys, const u32* __restrict__ vals,
+                         u32* __restrict__ prev) {
+    const u64 j = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= tot) return;
+    prev[vals[j]] = (j > 0 && keys[j] == keys[j - 1]) ? vals[j - 1] : 0xFFFFFFFFu;
+}
+
+__global__ void xe_best(const zcg_chunk* __restrict__ chunks, u32 c0, u64 D, u64 tot, DType t, u64 dsize,
+                        const u32* __restrict__ prev, u16* __restrict__ blen, u32* __restrict__ bdist) {
+    const u64 g = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= tot) return;
+    const u32 cl = (u32)(g / D);
+    const u64 p = g - (u64)cl * D;
+    u32 best = 0, bd = 0;
+    if (p + 4 <= D) {
+        const u8* src = (const u8*)chunks[c0 + cl].src;
+        const u64 cbase = (u64)cl * D;
+        const u32 mx = (D - p) < 273 ? (u32)(D - p) : 273u;
+        const u32 v0 = xe_ser4(src, p, t);
+        u32 q = prev[g];
+        for (u32 dep = 0; dep < XE_DEPTH && q != 0xFFFFFFFFu; dep++) {
+            const u64 qp = q - cbase;
+            if (p - qp >= dsize) break;  // beyond the preset's dictionary
+            if (xe_ser4(src, qp, t) == v0) {
+                u32 k = 4;
+                bool diff = false;
+                while (k + 4 <= mx) {
+                    const u32 x = xe_ser4(src, p + k, t) ^ xe_ser4(src, qp + k, t);
+                    if (x) { k += (u32)__builtin_ctz(x) >> 3; diff = true; break; }
+                    k += 4;
+                }
+                if (!diff)
+                    while (k < mx && xe_ser1(src, p + k, t) == xe_ser1(src, qp + k, t)) k++;
+                if (k > best) { best = k; bd = (u32)(p - qp); }
+                if (best >= XE_NICE) break;
+            }
+            q = prev[q];
+        }
+    }
+    blen[g] = (u16)best;
+    bdist[g] = bd;
+}
+
+}  // namespace
+
+uint64_t xz_encode_ws_bytes(const zcg_array* a, uint32_t n) {
+    const DType t = make_dtype(a->dtype);
+    const u64 D = a->chunk_num_elements * (u64)t.es;
+    if (n == 0) return 0;
+    return xe_layout(D, n).total;
+}
+
 hipError_t launch_xz_encode(const zcg_array* a, const zcg_chunk* d_chunks, uint32_t n,
-                            uint64_t* d_out_len, int32_t* d_status, hipStream_t s) {
+                            uint64_t* d_out_len, int32_t* d_status, void* ws, uint64_t ws_bytes, hipStream_t s) {
     if (n == 0) return hipSuccess;
     const DType t = make_dtype(a->dtype);
     const u64 D = a->chunk_num_elements * (u64)t.es;
-    hipLaunchKernelGGL(xz_encode_kernel, dim3(n), dim3(64), 0, s, d_chunks, n, D, t,
-                       a->compression.xz_preset, d_out_len, d_status);
-    return hipGetLastError();
+    const XeLayout y = xe_layout(D, n);
+    if (ws_bytes < y.total || y.tot >= (1ull << 31)) return hipErrorInvalidValue;
+    u8* w = (u8*)ws;
+    const int preset = a->compression.xz_preset;
+    const int pr = (preset < 0 || preset > 9) ? 6 : preset;
+    const u32 dlg = pr == 0 ? 18u : (pr == 1 ? 20u : (pr == 2 ? 21u : (pr <= 4 ? 22u : (pr <= 6 ? 23u : (u32)(pr + 17)))));
+    u32 cbits = 0;
+    while ((1u << cbits) < y.m) cbits++;
+    for (u32 s0 = 0; s0 < n; s0 += y.sm) {
+        const u32 scnt = (n - s0) < y.sm ? (n - s0) : y.sm;
+        for (u32 c0 = s0; c0 < s0 + scnt; c0 += y.m) {  // match finding, sub-batch by sub-batch
+            const u32 cnt = (s0 + scnt - c0) < y.m ? (s0 + scnt - c0) : y.m;
+            const u64 tot = (u64)cnt * D;
+            if (!tot) continue;
+            u32 *ka = (u32*)(w + y.off_ka), *kb = (u32*)(w + y.off_kb);
+            u32 *va = (u32*)(w + y.off_va), *vb = (u32*)(w + y.off_vb);
+            const u32 G = (u32)((tot + 255) / 256);
+            hipLaunchKernelGGL(xe_keys, dim3(G), dim3(256), 0, s, d_chunks, c0, D, tot, t, XE_KEYBITS, ka, va);
+            hipcub::DoubleBuffer<u32> dk(ka, kb), dv(va, vb);
+            size_t cb = y.cub_bytes;
+            hipError_t e = hipcub::DeviceRadixSort::SortPairs(w + y.off_cub, cb, dk, dv, (int)tot, 0,
+                                                              (int)(XE_KEYBITS + cbits), s);
+            if (e != hipSuccess) return e;
+            hipLaunchKernelGGL(xe_chain, dim3(G), dim3(256), 0, s, tot, dk.Current(), dv.Current(),
+                               (u32*)(w + y.off_prev));
+            const u64 mo = (u64)(c0 - s0) * D;  // this sub-batch's slice of the match arrays
+            hipLaunchKernelGGL(xe_best, dim3(G), dim3(256), 0, s, d_chunks, c0, D, tot, t, 1ull << dlg,
+                               (const u32*)(w + y.off_prev), (u16*)(w + y.off_blen) + mo,
+                               (u32*)(w + y.off_bdist) + mo);
+        }
+        hipLaunchKernelGGL(xz_encode_kernel, dim3(scnt), dim3(64), 0, s, d_chunks, s0, scnt, D, t, preset,
+                           (const u16*)(w + y.off_blen), (const u32*)(w + y.off_bdist), d_out_len, d_status);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 }  // namespace zcg
