@@ -10,13 +10,18 @@
 // follows zlib's _tr_flush_block, which is what reproduces the doc-spec vector.
 //
 // Layout (stream-ordered kernels):
+//   0. match finding over whole chunks, data-parallel (<= 128 MiB per
+//      sub-batch): keys (chunk, the 3 serialised bytes) sorted with the
+//      positions as values (hipCUB radix sort, stable), df_chain links each
+//      position to its predecessor with the same 3 bytes, df_best walks up to
+//      zlib's max_chain (capped at 64) candidates within 32 KiB and keeps the
+//      longest match (nearest on ties, zlib's nice_length stops the walk).
 //   1. deflate_segment: one wave per 16 KiB input segment.  The segment and
 //      the 32 KiB before it (deflate's window) are staged in LDS with the
 //      dtype transform applied (write_data's byte order, chunk.rs:118-140).
-//      The history is pre-inserted in a 4096-entry hash table; 64 lanes look
-//      up 64 consecutive positions, the first verified candidate is the next
-//      match (one-step lazy evaluation at level >= 4; positions inside matches
-//      are inserted at level >= 4).  Pass A runs the parse for symbol
+//      Every position's longest match comes precomputed (step 0); the
+//      64 lanes read 64 consecutive positions' matches and the wave walks them
+//      greedily (one-step lazy evaluation at level >= 4).  Pass A runs the parse for symbol
 //      frequencies; the wave builds length-limited Huffman codes (zlib's
 //      bl_count overflow rule) and picks stored/fixed/dynamic; pass B re-runs
 //      the same deterministic parse and emits the bits through an LDS ring
@@ -26,6 +31,8 @@
 //   2. deflate_finalize: per chunk, the gzip header and segment compaction.
 //   3. gzip_crc32: per chunk, 64 lanes CRC their slices, lane 0 combines them
 //      with a precomputed GF(2) shift operator; CRC32 + ISIZE trailer.
+#include <hipcub/hipcub.hpp>
+
 #include "zcg_common.h"
 
 namespace zcg {
@@ -34,7 +41,6 @@ constexpr u32 DF_SEG = 16384;               // input bytes per segment (one defl
 constexpr u32 DF_HIST = 32768;              // deflate window
 constexpr u32 DF_WIN = DF_SEG + DF_HIST;
 constexpr u32 DF_SLOT = DF_SEG + 128;       // output slot per segment (stored worst case + sync)
-constexpr u32 DF_HBITS = 12;
 constexpr u32 DF_RING = 1024;               // output ring words
 constexpr u32 DF_FLUSH = 512;
 constexpr u32 DF_HDR = 10;
@@ -67,8 +73,6 @@ __device__ __forceinline__ u32 rev_bits(u32 v, u32 n) { return n ? __builtin_bit
 
 struct DefLds {
     u8 win[DF_WIN + 64];
-    u16 t0[1u << DF_HBITS];    // per 3-byte hash: latest position + 1 (0 = empty)
-    u16 t1[1u << DF_HBITS];    // ... and the one before it
     u32 lfreq[288], dfreq[32], cfreq[20];
     u32 lcode[288], dcode[32], ccode[20];  // (length << 16) | bit-reversed code
     u32 ring[DF_RING];
@@ -219,38 +223,10 @@ struct ParseCfg {
 
 // One pass of the segment parse over window positions [h0, wend).
 // EMIT=false: symbol frequencies.  EMIT=true: bits into the ring (bp, fw).
-__device__ __forceinline__ u32 hash3(u32 v) { return ((v & 0xFFFFFFu) * 2654435761u) >> (32 - DF_HBITS); }
-
-// Insert position p (hash h) at the head of its 2-slot bucket.  Lanes of one
-// instruction that share a bucket resolve in hardware order; every candidate
-// is verified before use, and pass B checks that it only emits coded symbols
-// (else the segment is stored), so the stream never depends on that order.
-__device__ __forceinline__ void ins2(DefLds& L, u32 h, u32 p) {
-    const u16 old = L.t0[h];
-    L.t1[h] = old;
-    L.t0[h] = (u16)(p + 1);
-}
-
-// One pass of the segment parse over window positions [h0, wend).
-// EMIT=false: symbol frequencies.  EMIT=true: bits into the ring (bp, fw).
 template <bool EMIT>
-__device__ void parse_pass(DefLds& L, u32 h0, u32 wend, ParseCfg cfg, u32* bp, u32* fw, u8* out) {
+__device__ void parse_pass(DefLds& L, u32 h0, u32 wend, ParseCfg cfg, u32* bp, u32* fw, u8* out,
+                           const u32* __restrict__ mt) {
     const u32 lane = lane_id();
-    auto rd32 = [&](u32 p) -> u32 {
-        const u32* w = (const u32*)L.win;
-        return __builtin_amdgcn_alignbit(w[(p >> 2) + 1], w[p >> 2], (p & 3) * 8);
-    };
-    // fresh buckets; insert the history positions (no matching)
-    for (u32 q = lane; q < (1u << DF_HBITS) / 2; q += 64) { ((u32*)L.t0)[q] = 0; ((u32*)L.t1)[q] = 0; }
-    __syncthreads();
-    for (u32 g = 0; g < h0; g += 64) {
-        const u32 p = g + lane;
-        const bool on = p < h0 && p + 3 <= wend;
-        const u32 h = on ? hash3(rd32(p)) : 0u;
-        if (on) ins2(L, h, p);
-        __builtin_amdgcn_wave_barrier();
-    }
-    __syncthreads();
     u32 ip = h0;
     // literal emission for positions [a, b) (b - a <= 64)
     auto literals = [&](u32 a, u32 b) {
@@ -274,82 +250,18 @@ __device__ void parse_pass(DefLds& L, u32 h0, u32 wend, ParseCfg cfg, u32* bp, u
         if (on) ring_put(L, *bp + x - nb, cw & 0xFFFF, nb);
         *bp += tot;
     };
-    auto match_len = [&](u32 p, u32 r) -> u32 {  // 3 bytes verified; extend to <= 258, < wend
-        u32 e = p + 3;
-        const u32 lim = (p + 258 < wend) ? p + 258 : wend;
-        for (;;) {
-            const u32 x = e + lane;
-            const bool ok = x < lim && L.win[x] == L.win[x - (p - r)];
-            const unsigned long long bm = __ballot(!ok);
-            const u32 run = bm ? (u32)__builtin_ctzll(bm) : 64u;
-            e += run;
-            if (run < 64) break;
-        }
-        return e - p;
-    };
-    // best (length, ref) of lane `l`'s two candidates (wave-uniform call)
-    auto best_of = [&](u32 l, u32 r0, u32 r1, u32 ok0, u32 ok1, u32* blen, u32* bref) {
-        const u32 p = ip + l;
-        const u32 a0 = (u32)__shfl((int)r0, (int)l, 64), a1 = (u32)__shfl((int)r1, (int)l, 64);
-        const u32 k0 = (u32)__shfl((int)ok0, (int)l, 64), k1 = (u32)__shfl((int)ok1, (int)l, 64);
-        u32 bl = 0, br = 0;
-        if (k0) { const u32 ln = match_len(p, a0); bl = ln; br = a0; }
-        if (k1) {
-            const u32 ln = match_len(p, a1);
-            if (ln > bl) { bl = ln; br = a1; }
-        }
-        if (bl == 3 && p - br > 4096) bl = 0;  // zlib TOO_FAR: a far 3-byte match does not pay
-        *blen = bl;
-        *bref = br;
-    };
-    constexpr u32 LCAP = 32;  // per-lane match measurement cap
-    // lane-local match length from 3 verified bytes, capped at min(LCAP, wend - p)
-    auto ext = [&](u32 p, u32 r) -> u32 {
-        const u32 lim = (wend - p) < LCAP ? (wend - p) : LCAP;
-        u32 k = 3;
-        while (k < lim) {
-            const u32 x = rd32(p + k) ^ rd32(r + k);
-            if (x) { k += (u32)__builtin_ctz(x) >> 3; break; }
-            k += 4;
-        }
-        return k < lim ? k : lim;
-    };
     while (ip < wend) {
         // keep the ring from wrapping: a group adds < 2 Kbit
         if (EMIT && (*bp >> 5) >= *fw + DF_FLUSH) ring_flush(L, out, fw, *bp >> 5);
         const u32 gend = (wend - ip) < 64 ? (wend - ip) : 64u;  // positions of this group
         const u32 p = ip + lane;
         const bool valid = lane < gend && p + 3 <= wend;
-        const u32 v = valid ? rd32(p) : 0u;
-        const u32 h = hash3(v);
-        const u32 e0 = valid ? (u32)L.t0[h] : 0u, e1 = valid ? (u32)L.t1[h] : 0u;
-        const u32 r0 = e0 - 1, r1 = e1 - 1;
-        auto cand_len = [&](u32 e, u32 r) -> u32 {
-            if (!valid || e == 0 || r >= p || p - r > DF_HIST) return 0u;
-            if (((rd32(r) ^ v) & 0xFFFFFFu) != 0) return 0u;
-            const u32 ln = ext(p, r);
-            return (ln == 3 && p - r > 4096) ? 0u : ln;  // zlib TOO_FAR
-        };
-        const u32 l0 = cand_len(e0, r0), l1 = cand_len(e1, r1);
-        u32 bl = l1 > l0 ? l1 : l0;                  // ties: the nearer (t0)
-        u32 br = l1 > l0 ? r1 : r0;
-        // positions of this group are not in the buckets yet: try the nearest
-        // of a few short distances inside the group (periodic element data)
-        {
-            u32 dn = 0;
-#pragma unroll
-            for (u32 dd = 1; dd <= 32; dd <<= 1) {
-                const u32 vd = (u32)__shfl_up((int)v, dd, 64);
-                if (!dn && lane >= dd && ((vd ^ v) & 0xFFFFFFu) == 0) dn = dd;
-            }
-            if (valid && dn) {
-                const u32 ln = ext(p, p - dn);
-                if (ln > bl) { bl = ln; br = p - dn; }
-            }
-        }
+        // the precomputed longest match of this position (df_best), clipped to the segment
+        const u32 m = valid ? mt[p] : 0u;
+        u32 bl = m & 0x1FF, br = p - ((m >> 16) + 1);
+        if (bl > wend - p) bl = wend - p;
+        if (bl < 3 || (bl == 3 && p - br > 4096)) bl = 0;  // zlib TOO_FAR
         const unsigned long long mask = __ballot(bl >= 3);
-        if (valid) ins2(L, h, p);  // all lookups of the group are done
-        __builtin_amdgcn_wave_barrier();
         // walk the group: successive greedy (lazy) matches from the lane lengths
         u32 pos = 0;
         while (pos < gend) {
@@ -362,20 +274,6 @@ __device__ void parse_pass(DefLds& L, u32 h0, u32 wend, ParseCfg cfg, u32* bp, u
                 if (l2 > mlen) { f = f + 1; mlen = l2; mref = (u32)__shfl((int)br, (int)f, 64); }
             }
             const u32 mpos = ip + f;
-            if (mlen == LCAP) {  // measured to the cap: extend wave-parallel up to 258
-                u32 e = mpos + LCAP;
-                const u32 lim = (mpos + 258 < wend) ? mpos + 258 : wend;
-                const u32 d = mpos - mref;
-                for (;;) {
-                    const u32 x = e + lane;
-                    const bool okb = x < lim && L.win[x] == L.win[x - d];
-                    const unsigned long long bm = __ballot(!okb);
-                    const u32 run = bm ? (u32)__builtin_ctzll(bm) : 64u;
-                    e += run;
-                    if (run < 64) break;
-                }
-                mlen = e - mpos;
-            }
             if (f > pos) literals(ip + pos, ip + f);
             const u32 d = mpos - mref;
             const u32 lc = len_code(mlen), dc = dist_code(d);
@@ -396,27 +294,21 @@ __device__ void parse_pass(DefLds& L, u32 h0, u32 wend, ParseCfg cfg, u32* bp, u
                 *bp += nl + el + nd + ed;
             }
             pos = f + mlen;
-            if (pos > gend) {  // the match runs past the group: insert its last two positions
-                const u32 endp = ip + pos;
-                if (lane < 2) {
-                    const u32 q = endp - 2 + lane;
-                    if (q + 3 <= wend && q >= ip + gend) ins2(L, hash3(rd32(q)), q);
-                }
-                __builtin_amdgcn_wave_barrier();
-            }
         }
         ip += pos;
     }
     if (EMIT && (*bp >> 5) >= *fw + DF_FLUSH) ring_flush(L, out, fw, *bp >> 5);
 }
 
-__global__ __launch_bounds__(64) void deflate_segment(const zcg_chunk* __restrict__ chunks, u32 n, u64 D,
-                                                      u32 nseg, u64 bound, DType t, u32 level) {
+__global__ __launch_bounds__(64) void deflate_segment(const zcg_chunk* __restrict__ chunks, u32 c0, u32 n, u64 D,
+                                                      u32 nseg, u64 bound, DType t, u32 level,
+                                                      const u32* __restrict__ match) {
     extern __shared__ __attribute__((aligned(16))) u8 smem_raw[];
     DefLds& L = *(DefLds*)smem_raw;
     const u32 lane = threadIdx.x;
-    const u32 c = blockIdx.x / nseg, k = blockIdx.x % nseg;
-    if (c >= n) return;
+    const u32 cl = blockIdx.x / nseg, k = blockIdx.x % nseg;
+    if (cl >= n) return;
+    const u32 c = c0 + cl;
     const zcg_chunk ch = chunks[c];
     if (ch.dst_cap < bound || ch.src_len < D) return;
     const u8* src = (const u8*)ch.src;
@@ -447,7 +339,7 @@ __global__ __launch_bounds__(64) void deflate_segment(const zcg_chunk* __restric
     u32 hlit = 257, hdist = 1, hclen = 4, nrle = 0;
     if (level > 0) {
         const ParseCfg cfg{level >= 4, level >= 4};
-        parse_pass<false>(L, hist, wend, cfg, &bp, &fw, out);
+        parse_pass<false>(L, hist, wend, cfg, &bp, &fw, out, match + (u64)cl * D + w0);
         if (lane == 0) L.lfreq[256] += 1;  // end of block
         __syncthreads();
         // ---- codes and the block type (zlib _tr_flush_block) ------------------------
@@ -570,7 +462,7 @@ __global__ __launch_bounds__(64) void deflate_segment(const zcg_chunk* __restric
     if (lane == 0) L.ctl[CTL_ERR] = 0;
     __syncthreads();
     const ParseCfg cfg{level >= 4, level >= 4};
-    parse_pass<true>(L, hist, wend, cfg, &bp, &fw, out);
+    parse_pass<true>(L, hist, wend, cfg, &bp, &fw, out, match + (u64)cl * D + w0);
     if (lane == 0) {
         u32 b = bp;
         const u32 cw = L.lcode[256];
@@ -737,10 +629,121 @@ static void crc_shift_op(u64 len, u32* out) {
     for (int i = 0; i < 32; i++) out[i] = res[i];
 }
 
+namespace {
+
+constexpr u64 DF_SUB_BYTES = 128ull << 20;  // input bytes per match-finder sub-batch
+constexpr u64 DF_SUPER_BYTES = 1ull << 30;  // input bytes per segment launch
+
+struct DfLayout {
+    u32 m, sm;
+    u64 tot, cub_bytes;
+    u64 off_ka, off_kb, off_va, off_vb, off_prev, off_match, off_cub, total;
+};
+
+DfLayout df_layout(u64 D, u32 n) {
+    DfLayout y{};
+    u64 m = D ? DF_SUB_BYTES / D : n;
+    if (m < 1) m = 1;
+    if (m > n) m = n;
+    if (m > 256) m = 256;  // chunk id + 24 key bits fit 32
+    y.m = (u32)m;
+    y.tot = m * D;
+    u64 sm = D ? DF_SUPER_BYTES / D : n;
+    sm = sm / m * m;
+    if (sm < m) sm = m;
+    if (sm > n) sm = n;
+    y.sm = (u32)sm;
+    size_t cb = 0;
+    hipcub::DoubleBuffer<u32> k(nullptr, nullptr), v(nullptr, nullptr);
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, cb, k, v, (int)(y.tot ? y.tot : 1), 0, 32);
+    y.cub_bytes = (cb + 511) & ~255ull;
+    u64 p = 0;
+    auto take = [&](u64 bytes) { const u64 o = p; p = (p + bytes + 255) & ~255ull; return o; };
+    y.off_ka = take(4 * y.tot);
+    y.off_kb = take(4 * y.tot);
+    y.off_va = take(4 * y.tot);
+    y.off_vb = take(4 * y.tot);
+    y.off_prev = take(4 * y.tot);
+    y.off_match = take(4 * (u64)y.sm * D);
+    y.off_cub = take(y.cub_bytes);
+    y.total = p;
+    return y;
+}
+
+__device__ __forceinline__ u32 df_ser1(const u8* src, u64 x, const DType& t) {
+    return norm_byte(src[swap_pos(x, t)], t);
+}
+__device__ __forceinline__ u32 df_ser4(const u8* src, u64 x, const DType& t) {  // bytes x..x+3, LE
+    if (!t.swap && !t.isbool) return ld32(src + x);
+    return df_ser1(src, x, t) | (df_ser1(src, x + 1, t) << 8) | (df_ser1(src, x + 2, t) << 16) |
+           (df_ser1(src, x + 3, t) << 24);
+}
+
+__global__ void df_keys(const zcg_chunk* __restrict__ chunks, u32 c0, u64 D, u64 tot, DType t,
+                        u32* __restrict__ keys, u32* __restrict__ vals) {
+    const u64 g = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= tot) return;
+    const u32 cl = (u32)(g / D);
+    const u64 p = g - (u64)cl * D;
+    const u8* src = (const u8*)chunks[c0 + cl].src;
+    u32 v = 0;
+    if (p + 3 <= D) v = df_ser1(src, p, t) | (df_ser1(src, p + 1, t) << 8) | (df_ser1(src, p + 2, t) << 16);
+    keys[g] = (cl << 24) | v;
+    vals[g] = (u32)g;
+}
+
+__global__ void df_chain(u64 tot, const u32* __restrict__ keys, const u32* __restrict__ vals,
+                         u32* __restrict__ prev) {
+    const u64 j = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= tot) return;
+    prev[vals[j]] = (j > 0 && keys[j] == keys[j - 1]) ? vals[j - 1] : 0xFFFFFFFFu;
+}
+
+// match[g] = len | (dist - 1) << 16 of the longest match at g (len 0: none)
+__global__ void df_best(const zcg_chunk* __restrict__ chunks, u32 c0, u64 D, u64 tot, DType t, u32 depth,
+                        u32 nice, const u32* __restrict__ prev, u32* __restrict__ match) {
+    const u64 g = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= tot) return;
+    const u32 cl = (u32)(g / D);
+    const u64 p = g - (u64)cl * D;
+    u32 best = 0, bd = 0;
+    if (p + 3 <= D) {
+        const u8* src = (const u8*)chunks[c0 + cl].src;
+        const u64 cbase = (u64)cl * D;
+        const u32 mx = (D - p) < 258 ? (u32)(D - p) : 258u;
+        u32 q = prev[g];
+        for (u32 dep = 0; dep < depth && q != 0xFFFFFFFFu; dep++) {
+            const u64 qp = q - cbase;
+            if (p - qp > DF_HIST) break;
+            u32 k = 3;  // the 3 key bytes are equal
+            bool diff = false;
+            while (k + 4 <= mx) {
+                const u32 x = df_ser4(src, p + k, t) ^ df_ser4(src, qp + k, t);
+                if (x) { k += (u32)__builtin_ctz(x) >> 3; diff = true; break; }
+                k += 4;
+            }
+            if (!diff)
+                while (k < mx && df_ser1(src, p + k, t) == df_ser1(src, qp + k, t)) k++;
+            if (k > best && !(k == 3 && p - qp > 4096)) { best = k; bd = (u32)(p - qp); }
+            if (best >= nice) break;
+            q = prev[q];
+        }
+    }
+    match[g] = best ? (best | ((bd - 1) << 16)) : 0u;
+}
+
+}  // namespace
+
+uint64_t deflate_ws_bytes(const zcg_array* a, uint32_t n) {
+    const DType t = make_dtype(a->dtype);
+    const u64 D = a->chunk_num_elements * (u64)t.es;
+    if (n == 0) return 0;
+    return df_layout(D, n).total;
+}
+
 hipError_t launch_deflate(const zcg_array* a, const zcg_chunk* d_chunks, uint32_t n,
                           uint64_t* d_out_len, int32_t* d_status, void* ws, uint64_t ws_bytes,
                           hipStream_t s) {
-    (void)ws; (void)ws_bytes;
     if (n == 0) return hipSuccess;
     const DType t = make_dtype(a->dtype);
     const u64 D = a->chunk_num_elements * (u64)t.es;
@@ -748,6 +751,12 @@ hipError_t launch_deflate(const zcg_array* a, const zcg_chunk* d_chunks, uint32_
     const u32 xfl = level >= 9 ? 2u : (level <= 1 ? 4u : 0u);
     const u32 nseg = (u32)((D + DF_SEG - 1) / DF_SEG);
     const u64 bound = zcg_encode_bound(&a->compression, D);
+    const DfLayout y = df_layout(D, n);
+    if (nseg && (ws_bytes < y.total || y.tot >= (1ull << 31))) return hipErrorInvalidValue;
+    // zlib's configuration_table: max_chain (capped for the GPU) and nice_length
+    static const u32 chain[10] = {0, 4, 8, 32, 16, 32, 64, 64, 64, 64};
+    static const u32 nice[10] = {0, 8, 16, 32, 16, 32, 128, 128, 258, 258};
+    u8* w = (u8*)ws;
     if (nseg) {
         static bool attr = false;
         if (!attr) {
@@ -757,10 +766,35 @@ hipError_t launch_deflate(const zcg_array* a, const zcg_chunk* d_chunks, uint32_
             if (e != hipSuccess) return e;
             attr = true;
         }
-        const u64 nb = (u64)n * nseg;
-        if (nb > 0x7FFFFFFFull) return hipErrorInvalidValue;
-        hipLaunchKernelGGL(deflate_segment, dim3((u32)nb), dim3(64), sizeof(DefLds), s, d_chunks, n, D,
-                           nseg, bound, t, level);
+        for (u32 s0 = 0; s0 < n; s0 += y.sm) {
+            const u32 scnt = (n - s0) < y.sm ? (n - s0) : y.sm;
+            if (level > 0) {
+                for (u32 c0 = s0; c0 < s0 + scnt; c0 += y.m) {
+                    const u32 cnt = (s0 + scnt - c0) < y.m ? (s0 + scnt - c0) : y.m;
+                    const u64 tot = (u64)cnt * D;
+                    u32 *ka = (u32*)(w + y.off_ka), *kb = (u32*)(w + y.off_kb);
+                    u32 *va = (u32*)(w + y.off_va), *vb = (u32*)(w + y.off_vb);
+                    const u32 G = (u32)((tot + 255) / 256);
+                    u32 cbits = 0;
+                    while ((1u << cbits) < cnt) cbits++;
+                    hipLaunchKernelGGL(df_keys, dim3(G), dim3(256), 0, s, d_chunks, c0, D, tot, t, ka, va);
+                    hipcub::DoubleBuffer<u32> dk(ka, kb), dv(va, vb);
+                    size_t cb = y.cub_bytes;
+                    hipError_t e = hipcub::DeviceRadixSort::SortPairs(w + y.off_cub, cb, dk, dv, (int)tot, 0,
+                                                                      (int)(24 + cbits), s);
+                    if (e != hipSuccess) return e;
+                    hipLaunchKernelGGL(df_chain, dim3(G), dim3(256), 0, s, tot, dk.Current(), dv.Current(),
+                                       (u32*)(w + y.off_prev));
+                    hipLaunchKernelGGL(df_best, dim3(G), dim3(256), 0, s, d_chunks, c0, D, tot, t, chain[level],
+                                       nice[level], (const u32*)(w + y.off_prev),
+                                       (u32*)(w + y.off_match) + (u64)(c0 - s0) * D);
+                }
+            }
+            const u64 nb = (u64)scnt * nseg;
+            if (nb > 0x7FFFFFFFull) return hipErrorInvalidValue;
+            hipLaunchKernelGGL(deflate_segment, dim3((u32)nb), dim3(64), sizeof(DefLds), s, d_chunks, s0, scnt, D,
+                               nseg, bound, t, level, (const u32*)(w + y.off_match));
+        }
     }
     hipLaunchKernelGGL(deflate_finalize, dim3(n), dim3(256), 0, s, d_chunks, n, D, nseg, bound, xfl,
                        (u64*)d_out_len, d_status);
