@@ -72,7 +72,6 @@ __device__ __forceinline__ u32 dist_code(u32 d) {  // 1..32768 -> 0..29
 __device__ __forceinline__ u32 rev_bits(u32 v, u32 n) { return n ? __builtin_bitreverse32(v) >> (32 - n) : 0u; }
 
 struct DefLds {
-    u8 win[DF_WIN + 64];
     u32 lfreq[288], dfreq[32], cfreq[20];
     u32 lcode[288], dcode[32], ccode[20];  // (length << 16) | bit-reversed code
     u32 ring[DF_RING];
@@ -225,14 +224,14 @@ struct ParseCfg {
 // EMIT=false: symbol frequencies.  EMIT=true: bits into the ring (bp, fw).
 template <bool EMIT>
 __device__ void parse_pass(DefLds& L, u32 h0, u32 wend, ParseCfg cfg, u32* bp, u32* fw, u8* out,
-                           const u32* __restrict__ mt) {
+                           const u32* __restrict__ mt, const u8* __restrict__ src, u64 w0, DType t) {
     const u32 lane = lane_id();
     u32 ip = h0;
     // literal emission for positions [a, b) (b - a <= 64)
     auto literals = [&](u32 a, u32 b) {
         const u32 p = a + lane;
         const bool on = p < b;
-        const u32 byte = on ? L.win[p] : 0u;
+        const u32 byte = on ? (u32)norm_byte(src[swap_pos(w0 + p, t)], t) : 0u;  // serialised byte
         if (!EMIT) {
             if (on) atomicAdd(&L.lfreq[byte], 1u);
             return;
@@ -320,15 +319,6 @@ __global__ __launch_bounds__(64) void deflate_segment(const zcg_chunk* __restric
     const u64 w0 = s0 - hist;
     const u32 wend = hist + S;
     const bool final_seg = (k + 1 == nseg);
-    // ---- stage [w0, s0 + S) transformed ----------------------------------------
-    for (u32 q = lane * 16; q < wend; q += 64 * 16) {
-        if (q + 16 <= wend) {
-            *(u32x4*)(L.win + q) = transform16(ld16(src + w0 + q), t);
-        } else {
-            for (u32 i = q; i < wend; i++) L.win[i] = norm_byte(src[swap_pos(w0 + i, t)], t);
-        }
-    }
-    for (u32 q = wend + lane; q < wend + 64; q += 64) L.win[q] = 0;
     for (u32 q = lane; q < 288; q += 64) L.lfreq[q] = 0;
     if (lane < 32) L.dfreq[lane] = 0;
     if (lane < 20) L.cfreq[lane] = 0;
@@ -339,7 +329,7 @@ __global__ __launch_bounds__(64) void deflate_segment(const zcg_chunk* __restric
     u32 hlit = 257, hdist = 1, hclen = 4, nrle = 0;
     if (level > 0) {
         const ParseCfg cfg{level >= 4, level >= 4};
-        parse_pass<false>(L, hist, wend, cfg, &bp, &fw, out, match + (u64)cl * D + w0);
+        parse_pass<false>(L, hist, wend, cfg, &bp, &fw, out, match + (u64)cl * D + w0, src, w0, t);
         if (lane == 0) L.lfreq[256] += 1;  // end of block
         __syncthreads();
         // ---- codes and the block type (zlib _tr_flush_block) ------------------------
@@ -428,7 +418,7 @@ __global__ __launch_bounds__(64) void deflate_segment(const zcg_chunk* __restric
             out[1] = (u8)S; out[2] = (u8)(S >> 8);
             out[3] = (u8)~S; out[4] = (u8)(~S >> 8);
         }
-        for (u32 q = lane; q < S; q += 64) out[5 + q] = L.win[hist + q];
+        for (u32 q = lane; q < S; q += 64) out[5 + q] = norm_byte(src[swap_pos(s0 + q, t)], t);
         if (lane == 0) { const u32 len = 5 + S; slot[0] = (u8)len; slot[1] = (u8)(len >> 8); slot[2] = (u8)(len >> 16); slot[3] = (u8)(len >> 24); }
         return;
     }
@@ -462,7 +452,7 @@ __global__ __launch_bounds__(64) void deflate_segment(const zcg_chunk* __restric
     if (lane == 0) L.ctl[CTL_ERR] = 0;
     __syncthreads();
     const ParseCfg cfg{level >= 4, level >= 4};
-    parse_pass<true>(L, hist, wend, cfg, &bp, &fw, out, match + (u64)cl * D + w0);
+    parse_pass<true>(L, hist, wend, cfg, &bp, &fw, out, match + (u64)cl * D + w0, src, w0, t);
     if (lane == 0) {
         u32 b = bp;
         const u32 cw = L.lcode[256];
@@ -483,7 +473,7 @@ __global__ __launch_bounds__(64) void deflate_segment(const zcg_chunk* __restric
             out[1] = (u8)S; out[2] = (u8)(S >> 8);
             out[3] = (u8)~S; out[4] = (u8)(~S >> 8);
         }
-        for (u32 q = lane; q < S; q += 64) out[5 + q] = L.win[hist + q];
+        for (u32 q = lane; q < S; q += 64) out[5 + q] = norm_byte(src[swap_pos(s0 + q, t)], t);
         if (lane == 0) { const u32 len = 5 + S; slot[0] = (u8)len; slot[1] = (u8)(len >> 8); slot[2] = (u8)(len >> 16); slot[3] = (u8)(len >> 24); }
         return;
     }
