@@ -11,17 +11,25 @@
 // is a correct encoding, checked by round trips through the oracle.
 //
 // Kernels (stream-ordered):
-//   1. lz4_block_compress: one wave per block.  The block is parsed in 64 KiB
-//      windows staged in LDS (dtype transform applied: the stream holds the
-//      array's serialised bytes, chunk.rs:118-140).  The 64 lanes hash 64
-//      consecutive positions at once; the first lane whose hash candidate
-//      verifies is the next greedy match; matches extend 64 bytes per step.
+//   0. match finding, data-parallel over every position of a sub-batch
+//      (<= 128 MiB): keys (block, 20-bit hash of 4 serialised bytes) sorted
+//      with the positions as values (hipCUB radix sort, stable), lz_chain links
+//      each position to its predecessor with the same key, lz_best walks up to
+//      LZ_DEPTH candidates with offsets <= 65535 and keeps the longest match
+//      that ends before the block's last 5 literals (LZ4's end-of-block rules).
+//   1. lz4_block_compress: one wave per block, greedy like LZ4's fast
+//      encoder: the 64 lanes hold 64 consecutive positions' precomputed
+//      matches and the first one starts the next sequence; literals are read
+//      from HBM with the dtype transform (write_data's byte order,
+//      chunk.rs:118-140), so the kernel uses no LDS.
 //      Block k is written at its upper-bound slot 7 + k*(B+4) of dst.
 //   2. lz4_frame_finalize: one workgroup per chunk writes the frame header,
 //      compacts the blocks to their final offsets (tile copies, dst <= src),
 //      writes the end mark and the output length.
 //   3. lz4_content_xxh32: 4 lanes per chunk (one XXH32 accumulator each)
 //      hash the serialised content and write the content checksum.
+#include <hipcub/hipcub.hpp>
+
 #include "zcg_common.h"
 
 namespace zcg {
@@ -32,19 +40,7 @@ constexpr u32 LE_MFLIMIT = 12;      // last match starts >= 12 bytes before bloc
 constexpr u32 LE_LASTLIT = 5;       // last 5 bytes are literals
 constexpr u32 LE_MINLEN = 13;       // shorter blocks are literals only
 constexpr u32 LE_HDR = 7;           // frame header bytes
-
-struct LzEncLds {
-    u8 win[LE_WIN + 64];            // window bytes (+ slack for 4-byte reads)
-    u16 tab[1u << LE_HBITS];        // position + 1 of the latest position per hash, 0 = empty
-                                    // (match starts are < 65536 - 12, so p + 1 fits)
-};
-
-// 4 bytes at LDS window offset p (any alignment).
-__device__ __forceinline__ u32 win_rd32(const u8* win, u32 p) {
-    const u32* w = (const u32*)win;
-    const u32 a = w[p >> 2], b = w[(p >> 2) + 1];
-    return __builtin_amdgcn_alignbit(b, a, (p & 3) * 8);
-}
+constexpr u32 LE_MCAP = 32;         // match bytes measured by lz_best (longer ones are extended here)
 
 // Logical (serialised) byte x of the chunk: the stream holds elements in the
 // array's byte order; bool as 0/1.
@@ -76,108 +72,73 @@ __device__ void put_len(u8* out, u64 o, u32 v) {  // v >= 15; writes len_bytes(v
     if (lane == 0) out[o + nb - 1] = (u8)((v - 15) % 255);
 }
 
-__global__ __launch_bounds__(64) void lz4_block_compress(const zcg_chunk* __restrict__ chunks, u32 n,
-                                                         u64 D, u32 B, u32 nbpc, u64 bound, DType t) {
-    extern __shared__ __attribute__((aligned(16))) u8 smem_raw[];
-    LzEncLds& L = *(LzEncLds*)smem_raw;
+__global__ __launch_bounds__(64) void lz4_block_compress(const zcg_chunk* __restrict__ chunks, u32 c0, u32 n,
+                                                         u64 D, u32 B, u32 nbpc, u64 bound, DType t,
+                                                         const u32* __restrict__ match) {
     const u32 lane = threadIdx.x;
-    const u32 c = blockIdx.x / nbpc, k = blockIdx.x % nbpc;
-    if (c >= n) return;
+    const u32 cl = blockIdx.x / nbpc, k = blockIdx.x % nbpc;
+    if (cl >= n) return;
+    const u32 c = c0 + cl;
     const zcg_chunk ch = chunks[c];
     if (ch.dst_cap < bound || ch.src_len < D) return;  // finalize reports the status
     const u8* src = (const u8*)ch.src;
     u8* dst = (u8*)ch.dst;
     const u64 b0 = (u64)k * B;                          // logical start of the block
     const u32 S = (u32)((D - b0) < B ? (D - b0) : B);   // block bytes
+    const u32* mt = match + (u64)cl * D + b0;           // precomputed matches of the block
     u8* hdr = dst + LE_HDR + (u64)k * (B + 4);
     u8* out = hdr + 4;
     u64 op = 0;          // output bytes of this block
     bool stored = S < LE_MINLEN;
     u64 anchor = 0;      // block-relative start of the pending literal run
-    for (u32 wb = 0; wb < S && !stored; wb += LE_WIN) {
-        const u32 wl = (S - wb) < LE_WIN ? (S - wb) : LE_WIN;
-        // ---- stage the window (transformed), clear the hash table ----------
-        const u64 g0 = b0 + wb;
-        for (u32 q = lane * 16; q < wl; q += 64 * 16) {
-            if (q + 16 <= wl) {
-                const u32x4 v = transform16(ld16(src + g0 + q), t);
-                *(u32x4*)(L.win + q) = v;
-            } else {
-                for (u32 i = q; i < wl; i++) L.win[i] = src_byte(src, g0 + i, t);
-            }
-        }
-        for (u32 q = wl + lane; q < wl + 64; q += 64) L.win[q] = 0;
-        for (u32 q = lane; q < (1u << LE_HBITS) / 2; q += 64) ((u32*)L.tab)[q] = 0;
-        __syncthreads();
-        // match starts < S - MFLIMIT (block-relative), match ends <= S - LASTLIT
-        const u32 mfl = (S - LE_MFLIMIT > wb) ? (S - LE_MFLIMIT - wb) : 0;
-        const u32 mflim = mfl < wl ? mfl : wl;
-        const u32 mlim_b = S - LE_LASTLIT;
-        const u32 mlim = (mlim_b > wb) ? ((mlim_b - wb) < wl ? (mlim_b - wb) : wl) : 0;
-        u32 ip = (anchor > wb) ? (u32)(anchor - wb) : 0;
+    if (!stored) {
+        // match starts < S - MFLIMIT, match ends <= S - LASTLIT (lz_best clips)
+        const u32 mflim = S - LE_MFLIMIT;
+        u32 ip = 0;
+        u32 wbase = 0xFFFFFFFFu, wm = 0;  // 64 positions' matches, one per lane
         while (ip < mflim) {
-            const u32 p = ip + lane;
-            const bool valid = p < mflim && p + 4 <= wl;
-            const u32 v = valid ? win_rd32(L.win, p) : 0u;
-            const u32 h = (v * 2654435761u) >> (32 - LE_HBITS);
-            const u32 e = valid ? (u32)L.tab[h] : 0u;
-            const u32 ref = e - 1;
-            const bool cand = valid && e != 0 && ref < p && win_rd32(L.win, ref) == v;
-            const unsigned long long m = __ballot(cand);
-            // insert the positions scanned up to (and including) the chosen
-            // match start, like LZ4's sequential loop; positions after it are
-            // scanned again after the match and must not find themselves.
-            // Same-hash lanes: the store of the highest lane lands; any entry
-            // is only a candidate (verified above), so the stream stays valid.
-            const u32 f = m ? (u32)__builtin_ctzll(m) : 63u;
-            if (valid && lane <= f) L.tab[h] = (u16)(p + 1);
-            if (!m) { ip += 64; continue; }
-            u32 mpos = ip + f;
-            u32 mref = (u32)__shfl((int)ref, (int)f, 64);
-            // backward extension (bounded by the pending literals and the window)
-            {
-                const u32 lo = (anchor > wb) ? (u32)(anchor - wb) : 0u;
+            if (ip < wbase || ip >= wbase + 64) {
+                wbase = ip;
+                const u32 p = ip + lane;
+                wm = p < mflim ? mt[p] : 0u;
+            }
+            const u32 sh = ip - wbase;
+            const unsigned long long m = __ballot((wm & 0xFFFF) >= 4) & (~0ull << sh);
+            if (!m) { ip = wbase + 64; continue; }
+            const u32 f = (u32)__builtin_ctzll(m);
+            const u32 mv = __shfl(wm, (int)f, 64);
+            const u32 mpos = wbase + f;
+            u32 mlen = mv & 0xFFFF;
+            const u32 d = mv >> 16;
+            if (mlen == LE_MCAP) {  // measured to the cap: extend 64 bytes per step
+                const u32 lim = S - LE_LASTLIT;  // block-relative match end limit
+                u32 e2 = mpos + mlen;
                 for (;;) {
-                    const u32 room = mpos - lo < mref ? mpos - lo : mref;
-                    const bool ok = lane < room && L.win[mpos - 1 - lane] == L.win[mref - 1 - lane];
+                    const u32 x = e2 + lane;
+                    const bool ok = x < lim && src_byte(src, b0 + x, t) == src_byte(src, b0 + x - d, t);
                     const unsigned long long bm = __ballot(!ok);
                     const u32 run = bm ? (u32)__builtin_ctzll(bm) : 64u;
-                    mpos -= run;
-                    mref -= run;
+                    e2 += run;
                     if (run < 64) break;
                 }
+                mlen = e2 - mpos;
             }
-            // forward extension from the verified 4 bytes
-            const u32 orig = ip + f;
-            u32 e2 = orig + 4;
-            const u32 d = orig - (u32)__shfl((int)ref, (int)f, 64);  // offset (unchanged by back-ext)
-            for (;;) {
-                const u32 x = e2 + lane;
-                const bool ok = x < mlim && L.win[x] == L.win[x - d];
-                const unsigned long long bm = __ballot(!ok);
-                const u32 run = bm ? (u32)__builtin_ctzll(bm) : 64u;
-                e2 += run;
-                if (run < 64) break;
-            }
-            if (e2 < orig + 4) e2 = orig + 4;  // (cannot happen: the 4 bytes verified, mlim >= orig+4)
-            const u32 mlen = e2 - mpos;
-            // ---- emit the sequence: literals [anchor, wb+mpos), match (d, mlen) ----
-            const u32 lit = (u32)(wb + mpos - anchor);
+            // ---- emit the sequence: literals [anchor, mpos), match (d, mlen) ----
+            const u32 lit = (u32)(mpos - anchor);
             const u64 sz = 1 + len_bytes(lit) + lit + 2 + len_bytes(mlen - 4);
             if (op + sz + 1 + LE_LASTLIT >= S) { stored = true; break; }
             if (lane == 0) out[op] = (u8)(((lit < 15 ? lit : 15) << 4) | ((mlen - 4) < 15 ? (mlen - 4) : 15));
             u64 o = op + 1;
             if (lit >= 15) { put_len(out, o, lit); o += len_bytes(lit); }
-            put_literals(out, o, src, b0 + anchor, lit, L.win, g0, wl, t);
+            put_literals(out, o, src, b0 + anchor, lit, nullptr, 0, 0, t);
             o += lit;
             if (lane == 0) { out[o] = (u8)(d & 0xFF); out[o + 1] = (u8)(d >> 8); }
             o += 2;
             if (mlen - 4 >= 15) { put_len(out, o, mlen - 4); o += len_bytes(mlen - 4); }
             op = o;
-            anchor = wb + e2;
-            ip = e2;
+            anchor = mpos + mlen;
+            ip = mpos + mlen;
         }
-        __syncthreads();  // the window is restaged next
     }
     if (!stored) {  // last literals
         const u32 lit = (u32)(S - anchor);
@@ -188,8 +149,7 @@ __global__ __launch_bounds__(64) void lz4_block_compress(const zcg_chunk* __rest
             if (lane == 0) out[op] = (u8)((lit < 15 ? lit : 15) << 4);
             u64 o = op + 1;
             if (lit >= 15) { put_len(out, o, lit); o += len_bytes(lit); }
-            const u32 wl_last = (S - (S - 1) / LE_WIN * LE_WIN);
-            put_literals(out, o, src, b0 + anchor, lit, L.win, b0 + (S - 1) / LE_WIN * LE_WIN, wl_last, t);
+            put_literals(out, o, src, b0 + anchor, lit, nullptr, 0, 0, t);
             op = o + lit;
         }
     }
@@ -314,10 +274,131 @@ __global__ __launch_bounds__(64) void lz4_content_xxh32(const zcg_chunk* __restr
     o[0] = (u8)h; o[1] = (u8)(h >> 8); o[2] = (u8)(h >> 16); o[3] = (u8)(h >> 24);
 }
 
+namespace {
+
+constexpr u32 LZ_DEPTH = 4;                 // chain candidates per position
+constexpr u32 LZ_CAP = LE_MCAP;             // bytes measured per candidate
+constexpr u32 LZ_KEYBITS = 20;
+constexpr u64 LZ_SUB_BYTES = 128ull << 20;  // input bytes per match-finder sub-batch
+constexpr u64 LZ_SUPER_BYTES = 1ull << 30;  // input bytes per block-compress launch
+
+struct LzLayout {
+    u32 m, sm;
+    u64 tot, cub_bytes;
+    u64 off_ka, off_kb, off_va, off_vb, off_prev, off_match, off_cub, total;
+};
+
+LzLayout lz_layout(u64 D, u32 nbpc, u32 n) {
+    LzLayout y{};
+    u64 m = D ? LZ_SUB_BYTES / D : n;
+    if (m < 1) m = 1;
+    if (m > n) m = n;
+    while (m > 1 && m * nbpc > 4096) m--;  // block id + 20 hash bits fit 32
+    y.m = (u32)m;
+    y.tot = m * D;
+    u64 sm = D ? LZ_SUPER_BYTES / D : n;
+    sm = sm / m * m;
+    if (sm < m) sm = m;
+    if (sm > n) sm = n;
+    y.sm = (u32)sm;
+    size_t cb = 0;
+    hipcub::DoubleBuffer<u32> kk(nullptr, nullptr), v(nullptr, nullptr);
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, cb, kk, v, (int)(y.tot ? y.tot : 1), 0, 32);
+    y.cub_bytes = (cb + 511) & ~255ull;
+    u64 p = 0;
+    auto take = [&](u64 bytes) { const u64 o = p; p = (p + bytes + 255) & ~255ull; return o; };
+    y.off_ka = take(4 * y.tot);
+    y.off_kb = take(4 * y.tot);
+    y.off_va = take(4 * y.tot);
+    y.off_vb = take(4 * y.tot);
+    y.off_prev = take(4 * y.tot);
+    y.off_match = take(4 * (u64)y.sm * D);
+    y.off_cub = take(y.cub_bytes);
+    y.total = p;
+    return y;
+}
+
+__device__ __forceinline__ u32 lz_ser4(const u8* src, u64 x, const DType& t) {  // bytes x..x+3, LE
+    if (!t.swap && !t.isbool) return ld32(src + x);
+    return (u32)src_byte(src, x, t) | ((u32)src_byte(src, x + 1, t) << 8) | ((u32)src_byte(src, x + 2, t) << 16) |
+           ((u32)src_byte(src, x + 3, t) << 24);
+}
+
+__global__ void lz_keys(const zcg_chunk* __restrict__ chunks, u32 c0, u64 D, u32 B, u32 nbpc, u64 tot, DType t,
+                        u32* __restrict__ keys, u32* __restrict__ vals) {
+    const u64 g = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= tot) return;
+    const u32 cl = (u32)(g / D);
+    const u64 p = g - (u64)cl * D;
+    const u32 blk = (u32)(p / B);
+    const u64 bend = ((u64)blk + 1) * B < D ? ((u64)blk + 1) * B : D;
+    u32 h = 0;
+    if (p + 4 <= bend) h = (lz_ser4((const u8*)chunks[c0 + cl].src, p, t) * 2654435761u) >> (32 - LZ_KEYBITS);
+    keys[g] = ((cl * nbpc + blk) << LZ_KEYBITS) | h;
+    vals[g] = (u32)g;
+}
+
+__global__ void lz_chain(u64 tot, const u32* __restrict__ keys, const u32* __restrict__ vals,
+                         u32* __restrict__ prev) {
+    const u64 j = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= tot) return;
+    prev[vals[j]] = (j > 0 && keys[j] == keys[j - 1]) ? vals[j - 1] : 0xFFFFFFFFu;
+}
+
+// match[g] = len | offset << 16 (len 0: none); the match starts before the
+// block's MFLIMIT and ends at or before its last LASTLIT bytes
+__global__ void lz_best(const zcg_chunk* __restrict__ chunks, u32 c0, u64 D, u32 B, u64 tot, DType t,
+                        const u32* __restrict__ prev, u32* __restrict__ match) {
+    const u64 g = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= tot) return;
+    const u32 cl = (u32)(g / D);
+    const u64 p = g - (u64)cl * D;
+    const u64 bs = p / B * B;
+    const u64 bend = bs + B < D ? bs + B : D;
+    u32 best = 0, bd = 0;
+    if (p + LE_MFLIMIT < bend) {
+        const u8* src = (const u8*)chunks[c0 + cl].src;
+        const u64 cbase = (u64)cl * D;
+        u32 mx = (u32)(bend - LE_LASTLIT - p);  // bytes the match may cover
+        if (mx > LZ_CAP) mx = LZ_CAP;           // longer matches are extended by lz4_block_compress
+        const u32 v0 = lz_ser4(src, p, t);
+        u32 q = prev[g];
+        for (u32 dep = 0; dep < LZ_DEPTH && q != 0xFFFFFFFFu; dep++) {
+            const u64 qp = q - cbase;
+            if (p - qp > 65535) break;
+            if (lz_ser4(src, qp, t) == v0) {
+                u32 k = 4;
+                bool diff = false;
+                while (k + 4 <= mx) {
+                    const u32 x = lz_ser4(src, p + k, t) ^ lz_ser4(src, qp + k, t);
+                    if (x) { k += (u32)__builtin_ctz(x) >> 3; diff = true; break; }
+                    k += 4;
+                }
+                if (!diff)
+                    while (k < mx && src_byte(src, p + k, t) == src_byte(src, qp + k, t)) k++;
+                if (k > mx) k = mx;
+                if (k > best) { best = k; bd = (u32)(p - qp); }
+            }
+            q = prev[q];
+        }
+    }
+    match[g] = best >= 4 ? (best | (bd << 16)) : 0u;
+}
+
+}  // namespace
+
+uint64_t lz4_encode_ws_bytes(const zcg_array* a, uint32_t n) {
+    const DType t = make_dtype(a->dtype);
+    const u64 D = a->chunk_num_elements * (u64)t.es;
+    const u32 B = (u32)zcg_effective_lz4_block_size(a->compression.lz4_block_size);
+    const u32 nbpc = (u32)((D + B - 1) / B);
+    if (n == 0 || nbpc == 0) return 0;
+    return lz_layout(D, nbpc, n).total;
+}
+
 hipError_t launch_lz4_encode(const zcg_array* a, const zcg_chunk* d_chunks, uint32_t n,
                              uint64_t* d_out_len, int32_t* d_status, void* ws, uint64_t ws_bytes,
                              hipStream_t s) {
-    (void)ws; (void)ws_bytes;
     if (n == 0) return hipSuccess;
     const DType t = make_dtype(a->dtype);
     const u64 D = a->chunk_num_elements * (u64)t.es;
@@ -325,18 +406,36 @@ hipError_t launch_lz4_encode(const zcg_array* a, const zcg_chunk* d_chunks, uint
     const u32 nbpc = (u32)((D + B - 1) / B);
     const u64 bound = zcg_encode_bound(&a->compression, D);
     if (nbpc) {
-        static bool attr = false;
-        if (!attr) {
-            hipError_t e = hipFuncSetAttribute((const void*)lz4_block_compress,
-                                               hipFuncAttributeMaxDynamicSharedMemorySize,
-                                               (int)sizeof(LzEncLds));
-            if (e != hipSuccess) return e;
-            attr = true;
+        if (nbpc > 4096) return hipErrorInvalidValue;
+        const LzLayout y = lz_layout(D, nbpc, n);
+        if (ws_bytes < y.total || y.tot >= (1ull << 31)) return hipErrorInvalidValue;
+        u8* w = (u8*)ws;
+        for (u32 s0 = 0; s0 < n; s0 += y.sm) {
+            const u32 scnt = (n - s0) < y.sm ? (n - s0) : y.sm;
+            for (u32 c0 = s0; c0 < s0 + scnt; c0 += y.m) {
+                const u32 cnt = (s0 + scnt - c0) < y.m ? (s0 + scnt - c0) : y.m;
+                const u64 tot = (u64)cnt * D;
+                u32 *ka = (u32*)(w + y.off_ka), *kb = (u32*)(w + y.off_kb);
+                u32 *va = (u32*)(w + y.off_va), *vb = (u32*)(w + y.off_vb);
+                const u32 G = (u32)((tot + 255) / 256);
+                u32 bbits = 0;
+                while ((1u << bbits) < cnt * nbpc) bbits++;
+                hipLaunchKernelGGL(lz_keys, dim3(G), dim3(256), 0, s, d_chunks, c0, D, B, nbpc, tot, t, ka, va);
+                hipcub::DoubleBuffer<u32> dk(ka, kb), dv(va, vb);
+                size_t cb = y.cub_bytes;
+                hipError_t e = hipcub::DeviceRadixSort::SortPairs(w + y.off_cub, cb, dk, dv, (int)tot, 0,
+                                                                  (int)(LZ_KEYBITS + bbits), s);
+                if (e != hipSuccess) return e;
+                hipLaunchKernelGGL(lz_chain, dim3(G), dim3(256), 0, s, tot, dk.Current(), dv.Current(),
+                                   (u32*)(w + y.off_prev));
+                hipLaunchKernelGGL(lz_best, dim3(G), dim3(256), 0, s, d_chunks, c0, D, B, tot, t,
+                                   (const u32*)(w + y.off_prev), (u32*)(w + y.off_match) + (u64)(c0 - s0) * D);
+            }
+            const u64 nb = (u64)scnt * nbpc;
+            if (nb > 0x7FFFFFFFull) return hipErrorInvalidValue;
+            hipLaunchKernelGGL(lz4_block_compress, dim3((u32)nb), dim3(64), 0, s, d_chunks, s0, scnt, D, B, nbpc,
+                               bound, t, (const u32*)(w + y.off_match));
         }
-        const u64 nb = (u64)n * nbpc;
-        if (nb > 0x7FFFFFFFull) return hipErrorInvalidValue;
-        hipLaunchKernelGGL(lz4_block_compress, dim3((u32)nb), dim3(64), sizeof(LzEncLds), s, d_chunks,
-                           n, D, B, nbpc, bound, t);
     }
     hipLaunchKernelGGL(lz4_frame_finalize, dim3(n), dim3(256), 0, s, d_chunks, n, D, B, nbpc, bound,
                        (u64*)d_out_len, d_status);
