@@ -202,6 +202,17 @@ uint64_t zcg_region_grid(const zcg_region* r, uint64_t* grid_lo, uint64_t* grid_
 int zcg_read_region(zcg_ctx* ctx, const zcg_region* r, const void* const* d_chunk_table,
                     void* d_out, void* stream);
 
+/* The inverse scatter of ZarrNdarrayWriter::write_ndarray (ndarray.rs:276-385):
+ * the box (d_in, a strided view of bbox_shape) is written into the chunk
+ * slots of d_chunk_table (same grid range and order as zcg_read_region; every
+ * element of the box that falls in a non-NULL chunk is written, at its
+ * chunk-local position in the chunk memory order).  The caller pre-fills
+ * slots of partially covered chunks with the existing chunk (or fill value)
+ * and encodes the slots afterwards (zcg_encode_batch).  fill_missing is
+ * ignored.  Asynchronous on `stream`. */
+int zcg_write_region(zcg_ctx* ctx, const zcg_region* r, void* const* d_chunk_table,
+                     const void* d_in, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

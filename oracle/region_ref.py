@@ -57,3 +57,24 @@ def read_ndarray(shape, chunk_shape, order, bbox_off, bbox_shape, get_chunk, dty
     arr = np.full(tuple(bbox_shape), fill, dtype=dtype, order=order)
     read_ndarray_into(shape, chunk_shape, order, bbox_off, bbox_shape, get_chunk, arr)
     return arr
+
+
+def write_ndarray(shape, chunk_shape, order, offset, array, chunks, fill=0):
+    """ZarrNdarrayWriter::write_ndarray (ndarray.rs:276-385) on a dict
+    coord -> flat chunk elements (the store): fully covered chunks are
+    replaced, partly covered ones are read (or start as fill) and overlaid."""
+    bshape = list(array.shape)
+    for coord in bounded_coord_iter(shape, chunk_shape, offset, bshape):
+        nom = [c * cs for c, cs in zip(coord, chunk_shape)]
+        w_off, w_shp = intersect(nom, chunk_shape, offset, bshape)
+        a_sl = tuple(slice(o - b, o - b + s) for o, b, s in zip(w_off, offset, w_shp))
+        if w_off == nom and w_shp == list(chunk_shape):
+            data = np.asarray(array[a_sl]).flatten(order=order)
+        else:
+            ex = chunks.get(coord)
+            ch = (np.asarray(ex).reshape(tuple(chunk_shape), order=order).copy() if ex is not None
+                  else np.full(tuple(chunk_shape), fill, dtype=array.dtype))
+            c_sl = tuple(slice(o - n, o - n + s) for o, n, s in zip(w_off, nom, w_shp))
+            ch[c_sl] = array[a_sl]
+            data = ch.flatten(order=order)
+        chunks[coord] = data

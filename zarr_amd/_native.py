@@ -29,7 +29,7 @@ EXPORTED_SYMBOLS = (
     "zcg_effective_gzip_level", "zcg_effective_lz4_block_size", "zcg_codec_on_gpu",
     "zcg_decode_batch", "zcg_encode_batch", "zcg_encode_bound", "zcg_workspace_bytes",
     "zcg_read_chunk", "zcg_write_chunk", "zcg_read_chunks_host",
-    "zcg_region_grid", "zcg_read_region",
+    "zcg_region_grid", "zcg_read_region", "zcg_write_region",
 )
 
 
@@ -124,6 +124,9 @@ def load_library(path: str = LIB_PATH):
         L.zcg_read_region.argtypes = [ctypes.c_void_p, ctypes.POINTER(Region), ctypes.c_void_p,
                                       ctypes.c_void_p, ctypes.c_void_p]
         L.zcg_read_region.restype = ctypes.c_int
+        L.zcg_write_region.argtypes = [ctypes.c_void_p, ctypes.POINTER(Region), ctypes.c_void_p,
+                                       ctypes.c_void_p, ctypes.c_void_p]
+        L.zcg_write_region.restype = ctypes.c_int
         _lib = L
         return L
 

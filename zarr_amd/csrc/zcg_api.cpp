@@ -374,8 +374,21 @@ uint64_t zcg_region_grid(const zcg_region* r, uint64_t* grid_lo, uint64_t* grid_
     return cnt;
 }
 
+static int region_call(zcg_ctx* ctx, const zcg_region* r, const void* const* d_chunk_table, void* d_box,
+                       void* stream, uint32_t dir);
+
 int zcg_read_region(zcg_ctx* ctx, const zcg_region* r, const void* const* d_chunk_table, void* d_out,
                     void* stream) {
+    return region_call(ctx, r, d_chunk_table, d_out, stream, 0);
+}
+
+int zcg_write_region(zcg_ctx* ctx, const zcg_region* r, void* const* d_chunk_table, const void* d_in,
+                     void* stream) {
+    return region_call(ctx, r, (const void* const*)d_chunk_table, (void*)d_in, stream, 1);
+}
+
+static int region_call(zcg_ctx* ctx, const zcg_region* r, const void* const* d_chunk_table, void* d_out,
+                       void* stream, uint32_t dir) {
     if (!ctx || !r || r->ndim < 1 || r->ndim > ZCG_MAX_DIMS) return ZCG_ERR_INVALID_INPUT;
     const uint32_t es = r->elem_size;
     if (es != 1 && es != 2 && es != 4 && es != 8) return ZCG_ERR_INVALID_INPUT;
@@ -385,7 +398,8 @@ int zcg_read_region(zcg_ctx* ctx, const zcg_region* r, const void* const* d_chun
     RegionArgs a{};
     a.nd = nd;
     a.es = es;
-    a.fill = r->fill_missing ? 1u : 0u;
+    a.fill = (r->fill_missing && !dir) ? 1u : 0u;
+    a.dir = dir;
     a.V = 16 / es;
     a.fillv = r->fill_value;
     uint64_t tstr_arr[ZCG_MAX_DIMS];

@@ -219,6 +219,7 @@ static __constant__ u32 g_crc32_table[256] = {
 // Region assembly arguments (zcg_region.hip), built by zcg_read_region.
 struct RegionArgs {
     u32 nd, es, fill, V;       // dims, element bytes, fill flag, elements per thread (16/es)
+    u32 dir, pad;              // 0: chunks -> box (read_ndarray), 1: box -> chunks (write_ndarray)
     u64 total;                 // elements in the box
     u64 fillv;                 // fill element, replicated to 16 bytes below
     // per dim, fast-first order (the chunks' memory order)

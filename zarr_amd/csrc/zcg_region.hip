@@ -121,7 +121,8 @@ __global__ __launch_bounds__(RG_T) void region_kernel(RegionArgs a, const u8* co
         const u8* src = region_src(a, p, table, &run);
         if (rem == a.V && run >= a.V && a.ostr[0] == 1) {  // one 16-byte piece, both sides contiguous
             u8* d = out + region_dst(a, p) * (i64)a.es;
-            if (src) st16(d, ld16(src));
+            if (a.dir) { if (src) st16((u8*)src, ld16(d)); }
+            else if (src) st16(d, ld16(src));
             else if (a.fill) st16(d, fill16);
             continue;
         }
@@ -130,7 +131,8 @@ __global__ __launch_bounds__(RG_T) void region_kernel(RegionArgs a, const u8* co
             u8* d = out + region_dst(a, p) * (i64)a.es;
             const i64 ds = a.ostr[0] * (i64)a.es;
             for (u32 j = 0; j < k; j++) {
-                if (src) copy_elem(d + j * ds, src + (u64)j * a.es, a.es);
+                if (a.dir) { if (src) copy_elem((u8*)src + (u64)j * a.es, d + j * ds, a.es); }
+                else if (src) copy_elem(d + j * ds, src + (u64)j * a.es, a.es);
                 else if (a.fill) fill_elem(d + j * ds, fv, a.es);
             }
             rem -= k;
@@ -194,7 +196,9 @@ __global__ __launch_bounds__(RG_T) void region_rows_kernel(RegionArgs a, u64 nro
                 const bool here = ok && (u64)q < a.gn[0];
                 const u8* base = here ? table[ti + (u64)q * a.tstr[0]] : nullptr;
                 if (!(bs0 - x0 >= V && w0 + V <= cs0 && a.ostr[0] == 1)) { mode[u] = 3; continue; }
-                if (base) { v[u] = ld16(base + (wi + w0) * (u64)es); mode[u] = 1; }
+                if (a.dir) {  // write_ndarray: box -> chunk
+                    if (base) { v[u] = ld16(dp[u]); dp[u] = (u8*)base + (wi + w0) * (u64)es; mode[u] = 1; }
+                } else if (base) { v[u] = ld16(base + (wi + w0) * (u64)es); mode[u] = 1; }
                 else if (a.fill) { v[u] = fill16; mode[u] = 2; }
             }
 #pragma unroll
@@ -212,7 +216,8 @@ __global__ __launch_bounds__(RG_T) void region_rows_kernel(RegionArgs a, u64 nro
                     const bool hj = ok && (u64)qj < a.gn[0];
                     const u8* bj = hj ? table[ti + (u64)qj * a.tstr[0]] : nullptr;
                     u8* dj = drow_p + (i64)(x0 + j) * a.ostr[0] * es;
-                    if (bj) copy_elem(dj, bj + (wi + (rj - qj * cs0)) * (u64)es, a.es);
+                    if (a.dir) { if (bj) copy_elem((u8*)bj + (wi + (rj - qj * cs0)) * (u64)es, dj, a.es); }
+                    else if (bj) copy_elem(dj, bj + (wi + (rj - qj * cs0)) * (u64)es, a.es);
                     else if (a.fill) fill_elem(dj, fv, a.es);
                 }
             }

@@ -10,6 +10,7 @@ from __future__ import annotations
 
 import ctypes
 import itertools
+import os
 from typing import List, Sequence
 
 import numpy as np
@@ -195,3 +196,78 @@ def read_ndarray_into(hier, path_name: str, meta: ArrayMetadata, bbox: BoundingB
     torch.cuda.synchronize(device)
     if staged.size:
         np.copyto(arr, out.cpu().numpy().view(dt).reshape(staged.shape))
+
+
+def write_ndarray(hier, path_name: str, meta: ArrayMetadata, offset: Sequence[int], array: np.ndarray,
+                  device: int = 0) -> None:
+    """ZarrNdarrayWriter::write_ndarray (ndarray.rs:276-385) on the GPU: the
+    chunks the box touches are read and decoded when only partly covered
+    (absent ones start as fill value), the box is scattered into them by
+    zcg_write_region, and all of them are encoded in one batch and written."""
+    import torch
+    from .batch import make_encode_batch
+    if array.ndim != meta.get_ndim():
+        raise ZarrIOError("InvalidData", "Wrong number of dimensions")
+    dt = array.dtype.newbyteorder("=")
+    check_array_type(dt, meta)
+    es = dt.itemsize
+    bbox = BoundingBox(offset, list(array.shape))
+    lo, n = region_grid(meta, bbox)
+    coords = list(itertools.product(*[range(l, l + k) for l, k in zip(lo, n)]))  # C order
+    if not coords or bbox.is_empty():
+        return
+    cs = meta.get_chunk_shape()
+    N = meta.get_chunk_num_elements()
+    D = N * es
+    dev = torch.device("cuda", device)
+    slots = torch.empty(len(coords) * D, dtype=torch.uint8, device=dev)
+    partial_bufs, partial_idx, absent_idx = [], [], []
+    for i, c in enumerate(coords):
+        assert meta.in_bounds(c)  # storage.rs:217
+        nom = BoundingBox([ci * s for ci, s in zip(c, cs)], cs)
+        wb = BoundingBox(nom.offset, nom.shape)
+        wb.intersect(bbox)
+        if wb == nom:
+            continue  # fully overwritten: no read (ndarray.rs:328-337)
+        p = hier.chunk_path(path_name, meta, c)
+        try:
+            with open(p, "rb") as f:
+                partial_bufs.append(f.read())
+            partial_idx.append(i)
+        except FileNotFoundError:
+            absent_idx.append(i)  # starts as fill value (ndarray.rs:357-368)
+    if partial_bufs:
+        packed = PackedStreams(partial_bufs, D, dev)
+        BatchCodec(device).decode(meta, packed)
+        st = packed.status.cpu().numpy()
+        for k, i in enumerate(partial_idx):
+            if st[k] != 0:
+                raise ZarrIOError(_native.STATUS_NAMES.get(int(st[k]), str(st[k])), f"chunk {list(coords[i])}")
+            slots[i * D:(i + 1) * D].copy_(packed.dst[k * D:(k + 1) * D])
+    if absent_idx:
+        fill = np.full(N, 0 if meta.fill_value is None else meta.fill_value, dtype=dt)
+        ft = torch.from_numpy(fill.view(np.uint8)).to(dev)
+        for i in absent_idx:
+            slots[i * D:(i + 1) * D].copy_(ft)
+    table = torch.tensor([slots.data_ptr() + i * D for i in range(len(coords))], dtype=torch.int64, device=dev)
+    box = torch.from_numpy(np.ascontiguousarray(array, dtype=dt).reshape(-1).view(np.uint8).copy()).to(dev)
+    ctx = _native.context(device)
+    r = _region(meta, bbox, es, False, 0, _strides(bbox.shape, "C"))
+    h = torch.cuda.current_stream(device).cuda_stream
+    _raise_status(ctx.lib.zcg_write_region(ctx.handle, ctypes.byref(r), table.data_ptr(), box.data_ptr(), h),
+                  ctx, "write_region")
+    codec = BatchCodec(device)
+    cap = codec.encode_bound(meta, D)
+    desc, dst, out_len, status = make_encode_batch(slots, len(coords), cap, dev)
+    codec.encode(meta, desc, len(coords), out_len, status)
+    torch.cuda.synchronize(device)
+    st = status.cpu().numpy()
+    ol = out_len.cpu().numpy()
+    host = dst.cpu().numpy()
+    for i, c in enumerate(coords):
+        if st[i] != 0:
+            raise ZarrIOError(_native.STATUS_NAMES.get(int(st[i]), str(st[i])), f"chunk {list(c)}")
+        p = hier.chunk_path(path_name, meta, c)
+        os.makedirs(os.path.dirname(p), exist_ok=True)
+        with open(p, "wb") as f:
+            f.write(host[i * cap:i * cap + int(ol[i])].tobytes())
