@@ -328,16 +328,51 @@ def test_xz_encode_dtypes(dt):
     assert np.array_equal(back, data)
 
 
-def test_xz_encode_doc_spec_decodes():
-    """tests.rs:147-159 pins xz's doc-spec bytes for liblzma's preset-6
-    encoder; a different LZMA parse is a different (valid) stream, so the GPU
-    stream must decode to the same values through the reference decoder."""
+def test_xz_encode_doc_spec_exact():
+    """tests.rs:147-159 + xz.rs:52-75,84-90: byte-identical to the reference
+    vector (one LZMA2 uncompressed chunk `01 00 0b` + the 12 bytes)."""
     from zarr_amd.compression import Xz
     d = doc_spec()
     meta = ArrayMetadata.new([5, 6, 7], [1, 2, 3], ">i2", Xz(6))
     out = DefaultChunk.write_chunk(meta, SliceDataChunk([0, 0, 0], np.array(d["expected_values"], np.int16)))
+    assert out.hex() == d["encode_expected"]["xz"]
     st, dec = zref.decode(zref.XZ, out, 12, 2, True)
     assert st == zref.OK and np.frombuffer(dec, "<i2").tolist() == d["expected_values"]
+
+
+@pytest.mark.parametrize("nbytes", [1, 7, 12, 40, 1000])
+def test_xz_encode_small_matches_liblzma(nbytes):
+    """Inputs too small to compress: liblzma emits one uncompressed LZMA2
+    chunk, so the whole .xz stream is determined; the GPU stream must be the
+    same bytes (lzma_easy_encoder(6, CRC64) = Python lzma preset 6)."""
+    import lzma
+    from zarr_amd.compression import Xz
+    rng = np.random.default_rng(nbytes)
+    a = rng.integers(0, 256, nbytes, dtype=np.uint8)
+    meta = ArrayMetadata.new([nbytes], [nbytes], "u1", Xz(6))
+    st, outs = encode_batch(meta, [a])
+    assert st[0] == 0
+    ref = lzma.compress(a.tobytes(), format=lzma.FORMAT_XZ, check=lzma.CHECK_CRC64, preset=6)
+    assert outs[0].hex() == ref.hex()
+
+
+def test_xz_encode_incompressible_no_expansion():
+    """Uniform bytes: every LZMA2 chunk falls back to an uncompressed one, as
+    liblzma's do, so the stream is no longer than liblzma's (plus chunk-header
+    slack), and mixed data (compressible / incompressible 64 KiB runs) round
+    trips through uncompressed chunks followed by state-reset LZMA chunks."""
+    import lzma
+    from zarr_amd.compression import Xz
+    D = 1 << 20
+    arrays = [_data("uniform", D, 11), _data("mixed", D, 12)]
+    meta = ArrayMetadata.new([2 * D], [D], "u1", Xz(6))
+    st, outs = encode_batch(meta, arrays)
+    assert (st == 0).all()
+    for a, s in zip(arrays, outs):
+        check_xz_stream(s, a.tobytes(), 6)
+    ref = lzma.compress(arrays[0].tobytes(), format=lzma.FORMAT_XZ, check=lzma.CHECK_CRC64, preset=6)
+    assert len(outs[0]) <= len(ref) + 64, (len(outs[0]), len(ref))
+    assert len(outs[0]) < D + D // 1000
 
 
 # ---- Bzip2 (bzip.rs:36-45: bzip2-rs BzEncoder = libbz2 BZ2_bzCompressInit(block_size)) ----
@@ -462,3 +497,73 @@ def test_bzip2_encode_bad_level():
     with pytest.raises(ZarrIOError) as e:
         DefaultChunk.write_chunk(meta, SliceDataChunk([0], np.zeros(100, np.uint8)))
     assert e.value.kind == "InvalidInput"
+
+
+# ---- descriptor edge cases and the encoders' internal sub-batch splits ----------
+def _codec(name, level=None):
+    from zarr_amd.compression import Bzip2, Raw, Xz
+    return {"raw": lambda: Raw(), "gzip": lambda: Gzip(6), "lz4": lambda: Lz4(65536),
+            "xz": lambda: Xz(6), "bzip2": lambda: Bzip2(9)}[name]()
+
+
+@pytest.mark.parametrize("codec", ["raw", "gzip", "lz4", "xz", "bzip2"])
+def test_encode_short_src_is_invalid_data(codec):
+    """A chunk whose src holds fewer than N*size bytes is write_chunk's
+    element-count error (chunk.rs:309-318): INVALID_DATA for that chunk only,
+    no out-of-bounds read, and the other chunks of the batch still encode."""
+    import torch
+    from zarr_amd.batch import BatchCodec, make_encode_batch
+    D = 200000
+    arrays = [_data("text", D, 1), _data("randwalk", D, 2), _data("uniform", D, 3)]
+    meta = ArrayMetadata.new([3 * D], [D], "u1", _codec(codec))
+    bc = BatchCodec(0)
+    elems = torch.from_numpy(np.concatenate(arrays)).to("cuda:0")
+    cap = bc.encode_bound(meta, D)
+    desc, dst, out_len, status = make_encode_batch(elems, 3, cap, "cuda:0")
+    d = desc.cpu().numpy().view(np.uint64).reshape(3, 4).copy()
+    d[1, 1] = 3  # src_len < D (shorter than one match-finder key)
+    desc = torch.from_numpy(d.view(np.int64)).to("cuda:0")
+    bc.encode(meta, desc, 3, out_len, status)
+    torch.cuda.synchronize()
+    st = status.cpu().numpy()
+    assert st.tolist() == [0, 2, 0]
+    ol = out_len.cpu().numpy()
+    buf = dst.cpu().numpy().reshape(3, cap)
+    cid = {"raw": zref.RAW, "gzip": zref.GZIP, "lz4": zref.LZ4, "xz": zref.XZ, "bzip2": zref.BZIP2}[codec]
+    for i in (0, 2):
+        rst, dec = zref.decode(cid, buf[i, :ol[i]].tobytes(), D, 1, False, False)
+        assert rst == zref.OK and dec == arrays[i].tobytes()
+
+
+@pytest.mark.parametrize("codec", ["lz4", "gzip", "xz"])
+def test_encode_sub_batch_splits_roundtrip(codec):
+    """1 100 distinct 1 MiB chunks: more than one 128 MiB match-finder
+    sub-batch and more than one 1 GiB coder launch (the m / sm splits of
+    lz_layout / df_layout / xe_layout).  Every stream must decode with the
+    reference libraries to its own chunk."""
+    import torch
+    from zarr_amd.batch import BatchCodec, make_encode_batch
+    D, n = 1 << 20, 1100
+    rng = np.random.default_rng(21)
+    base = np.cumsum(rng.integers(-3, 4, (64 << 20) // 2 + D)).astype("<i2").view(np.uint8)
+    offs = [(i * 40009) & ~1 for i in range(n)]  # distinct, overlapping windows of one walk
+    meta = ArrayMetadata.new([n * D], [D], "u1", _codec(codec))
+    bc = BatchCodec(0)
+    elems = torch.empty(n * D, dtype=torch.uint8, device="cuda:0")
+    for i, o in enumerate(offs):
+        elems[i * D:(i + 1) * D].copy_(torch.from_numpy(base[o:o + D]))
+    cap = bc.encode_bound(meta, D)
+    desc, dst, out_len, status = make_encode_batch(elems, n, cap, "cuda:0")
+    bc.encode(meta, desc, n, out_len, status)
+    torch.cuda.synchronize()
+    assert (status.cpu().numpy() == 0).all()
+    ol = out_len.cpu().numpy()
+    del elems
+    host = dst.view(n, cap).cpu().numpy()
+    del dst
+    cid = {"gzip": zref.GZIP, "lz4": zref.LZ4, "xz": zref.XZ}[codec]
+    srcs = [np.ascontiguousarray(host[i, :ol[i]]) for i in range(n)]
+    st, outs = zref.decode_batch(cid, srcs, D, threads=16)
+    assert (st == 0).all()
+    bad = [i for i in range(n) if not np.array_equal(outs[i], base[offs[i]:offs[i] + D])]
+    assert not bad, bad[:10]

@@ -1,22 +1,23 @@
 #!/bin/bash
-# HBM traffic per decode launch for every codec's bench leg (GPU box).
+# HBM traffic per launch of every bench leg (GPU box), measured on the SAME
+# bench code, streams and batch sizes that bench.py reports.
 # One rocprofv3 --pmc pass per counter (FETCH_SIZE takes 3 of the 4 TCC
 # slots, WRITE_SIZE 2, so they cannot share a pass), each under its own
 # time limit; the first failure ends the script.
-#   usage: tools/pmc_traffic.sh OUTDIR [codec ...]
+#   usage: tools/pmc_traffic.sh OUTDIR [leg ...]   (legs: gzip lz4 raw xz bzip2 gzip_encode ...)
 set -o pipefail
 out=$1; shift
-codecs=${*:-gzip lz4 raw xz bzip2}
+legs=${*:-gzip lz4 raw xz bzip2 gzip_encode}
 root="${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p "$out"
 cd /tmp && export TMPDIR=/tmp
-for c in $codecs; do
+for c in $legs; do
   case $c in
-    lz4) b=4096;; xz|bzip2) b=2048;; raw) b=1024;; *) b=4096;;
+    *_encode) args="--codec raw --batch 1 --steps 2 --warmup 1 --legs $c --no-cpu-baseline";;
+    *) args="--codec $c --steps 2 --warmup 1 --no-extra --no-cpu-baseline";;
   esac
   for k in FETCH_SIZE WRITE_SIZE; do
-    timeout -s KILL 150 rocprofv3 --pmc $k --output-format csv -d "$out/$c.$k" -o pmc -- \
-      python3 "$root/bench.py" --codec $c --batch $b --steps 2 --warmup 1 --no-extra --no-cpu-baseline \
-      > "$out/$c.$k.log" 2>&1 || exit $?
+    timeout -s KILL 300 rocprofv3 --pmc $k --output-format csv -d "$out/$c.$k" -o pmc -- \
+      python3 "$root/bench.py" $args > "$out/$c.$k.log" 2>&1 || exit $?
   done
 done

@@ -202,11 +202,12 @@ __device__ __forceinline__ u64 wave_max_u64(u64 x) {
 // piece (q == 254, next byte differs, or end of input) with q >= 3.  Blocks are
 // cut only between pieces, so "4 bytes + count" never straddles two blocks.
 __global__ __launch_bounds__(64) void bze_rle1(const zcg_chunk* __restrict__ chunks, u32 c0, u32 cnt,
-                                               u64 D, DType t, BzeLayout y, u8* __restrict__ ws) {
+                                               u64 D0, DType t, BzeLayout y, u8* __restrict__ ws) {
     const u32 ci = blockIdx.x;
     if (ci >= cnt) return;
     const int lane = lane_id();
     const zcg_chunk ch = chunks[c0 + ci];
+    const u64 D = ch.src_len >= D0 ? D0 : 0;  // a short src reads nothing (INVALID_DATA in bze_assemble)
     const gu8* src = (const gu8*)ch.src;
     gu8* out = (gu8*)(ws + y.off_rle + (u64)ci * y.R);
     BzeLocalBlk* lb = (BzeLocalBlk*)(ws + y.off_lblk) + (u64)ci * y.maxb;
@@ -937,6 +938,10 @@ __global__ __launch_bounds__(BZE_T) void bze_assemble(const zcg_chunk* __restric
     __threadfence_block();
     __syncthreads();
     const u64 total = total_s, F = ftr_s;
+    if (ch.src_len < y.D) {  // fewer serialised bytes than the chunk holds (chunk.rs:309-318)
+        if (tid == 0) { out_len[c0 + c] = 0; status[c0 + c] = ZCG_ERR_INVALID_DATA; }
+        return;
+    }
     if (bad_s) {
         if (tid == 0) { out_len[c0 + c] = 0; status[c0 + c] = ZCG_ERR_RUNTIME; }
         return;

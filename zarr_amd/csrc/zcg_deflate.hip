@@ -675,9 +675,10 @@ __global__ void df_keys(const zcg_chunk* __restrict__ chunks, u32 c0, u64 D, u64
     if (g >= tot) return;
     const u32 cl = (u32)(g / D);
     const u64 p = g - (u64)cl * D;
-    const u8* src = (const u8*)chunks[c0 + cl].src;
+    const zcg_chunk ch = chunks[c0 + cl];
+    const u8* src = (const u8*)ch.src;
     u32 v = 0;
-    if (p + 3 <= D) v = df_ser1(src, p, t) | (df_ser1(src, p + 1, t) << 8) | (df_ser1(src, p + 2, t) << 16);
+    if (p + 3 <= D && ch.src_len >= D) v = df_ser1(src, p, t) | (df_ser1(src, p + 1, t) << 8) | (df_ser1(src, p + 2, t) << 16);
     keys[g] = (cl << 24) | v;
     vals[g] = (u32)g;
 }
@@ -697,7 +698,7 @@ __global__ void df_best(const zcg_chunk* __restrict__ chunks, u32 c0, u64 D, u64
     const u32 cl = (u32)(g / D);
     const u64 p = g - (u64)cl * D;
     u32 best = 0, bd = 0;
-    if (p + 3 <= D) {
+    if (p + 3 <= D && chunks[c0 + cl].src_len >= D) {  // a short src is INVALID_DATA (deflate_finalize)
         const u8* src = (const u8*)chunks[c0 + cl].src;
         const u64 cbase = (u64)cl * D;
         const u32 mx = (D - p) < 258 ? (u32)(D - p) : 258u;

@@ -333,7 +333,7 @@ __global__ void lz_keys(const zcg_chunk* __restrict__ chunks, u32 c0, u64 D, u32
     const u32 blk = (u32)(p / B);
     const u64 bend = ((u64)blk + 1) * B < D ? ((u64)blk + 1) * B : D;
     u32 h = 0;
-    if (p + 4 <= bend) h = (lz_ser4((const u8*)chunks[c0 + cl].src, p, t) * 2654435761u) >> (32 - LZ_KEYBITS);
+    if (p + 4 <= bend && chunks[c0 + cl].src_len >= D) h = (lz_ser4((const u8*)chunks[c0 + cl].src, p, t) * 2654435761u) >> (32 - LZ_KEYBITS);
     keys[g] = ((cl * nbpc + blk) << LZ_KEYBITS) | h;
     vals[g] = (u32)g;
 }
@@ -356,7 +356,7 @@ __global__ void lz_best(const zcg_chunk* __restrict__ chunks, u32 c0, u64 D, u32
     const u64 bs = p / B * B;
     const u64 bend = bs + B < D ? bs + B : D;
     u32 best = 0, bd = 0;
-    if (p + LE_MFLIMIT < bend) {
+    if (p + LE_MFLIMIT < bend && chunks[c0 + cl].src_len >= D) {  // short src: INVALID_DATA in finalize
         const u8* src = (const u8*)chunks[c0 + cl].src;
         const u64 cbase = (u64)cl * D;
         u32 mx = (u32)(bend - LE_LASTLIT - p);  // bytes the match may cover

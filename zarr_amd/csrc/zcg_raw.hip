@@ -32,7 +32,8 @@ __global__ __launch_bounds__(RAW_THREADS) void raw_kernel(const zcg_chunk* __res
     if (!encode) {
         if (ch.src_len < nbytes) st = ZCG_ERR_UNEXPECTED_EOF;  // read_exact short
     } else {
-        if (ch.dst_cap < nbytes) st = ZCG_ERR_OUTPUT_TOO_SMALL;
+        if (ch.src_len < nbytes) st = ZCG_ERR_INVALID_DATA;  // element count (chunk.rs:309-318)
+        else if (ch.dst_cap < nbytes) st = ZCG_ERR_OUTPUT_TOO_SMALL;
     }
     if (tile == 0 && threadIdx.x == 0) {
         status[c] = st;

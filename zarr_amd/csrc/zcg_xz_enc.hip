@@ -92,6 +92,36 @@ struct XeEnc {
         const u64 e = pos < cap ? pos : cap;
         if (g + lane < e) dst[g + lane] = (u8)lbuf;
     }
+    // Move the output position back to `at` (<= pos): bytes before `at` stay.
+    // If `at`'s 64-byte group was already stored, reload it into the staging
+    // registers (each lane reads back the byte it stored, except header bytes
+    // that patch() stored from lane 0 — hence the fence).
+    __device__ __forceinline__ void rewind(u64 at) {
+        if ((at >> 6) != (pos >> 6)) {
+            __threadfence_block();
+            const u64 g = at & ~63ull;
+            if (g + lane < cap) lbuf = dst[g + lane];
+        }
+        pos = at;
+    }
+    // Append `len` serialised input bytes starting at q0, 64 per step: lane j
+    // of the wave takes byte (j - pos) mod 64 of the step (one rotation).
+    __device__ __forceinline__ void out_run(u64 q0, u64 len) {
+        for (u64 k = 0; k < len; k += 64) {
+            const u32 cnt = (len - k) < 64 ? (u32)(len - k) : 64u;
+            const u32 o = (u32)(pos & 63);
+            const u32 v = ((u32)lane < cnt) ? sb(q0 + k + lane) : 0u;
+            const u32 rot = (u32)__shfl((int)v, (lane - (int)o) & 63);
+            if ((u32)lane >= o && (u32)lane < o + cnt) lbuf = rot;
+            if (o + cnt >= 64) {
+                const u64 g = pos & ~63ull;
+                if (g + lane < cap) dst[g + lane] = (u8)lbuf;
+                if ((u32)lane < o + cnt - 64) lbuf = rot;
+            }
+            if (pos + cnt > cap) over = true;
+            pos += cnt;
+        }
+    }
     // byte `at` < pos, possibly still in the staging group
     __device__ __forceinline__ void patch(u64 at, u32 b) {
         if (at >= cap) return;
@@ -224,6 +254,10 @@ __global__ __launch_bounds__(64) void xz_encode_kernel(const zcg_chunk* __restri
     const u32* bdist = g_bdist + (u64)blockIdx.x * D;  // its distance (p - q)
     const int lane = lane_id();
     const zcg_chunk ch = chunks[c];
+    if (ch.src_len < D) {  // fewer serialised bytes than the chunk holds (chunk.rs:309-318)
+        if (lane == 0) { out_len[c] = 0; status[c] = ZCG_ERR_INVALID_DATA; }
+        return;
+    }
     XeEnc e;
     e.src = (const gu8*)ch.src;
     e.n = D;
@@ -258,9 +292,11 @@ __global__ __launch_bounds__(64) void xz_encode_kernel(const zcg_chunk* __restri
         for (int k = 0; k < 4; k++) e.out((hc >> (8 * k)) & 0xFF);
         const u64 cdata0 = e.pos;
 
-        for (u32 i = lane; i < XE_PROBS; i += 64) probs[i] = 1024;
         u32 state = 0, rep0 = 0;
-        bool first = true;
+        // liblzma's LZMA2 chunk flags (lzma2_encoder.c): a dictionary reset
+        // and the properties go with the first chunk of their kind; an
+        // uncompressed chunk leaves a state reset pending for the next LZMA one.
+        bool need_dict = true, need_props = true, need_state = true;
         // Per-lane window of 64 consecutive positions: the serialised byte, the
         // byte rep0 + 1 back, and the precomputed best match, so literal runs
         // need no dependent memory access per position.
@@ -280,7 +316,15 @@ __global__ __launch_bounds__(64) void xz_encode_kernel(const zcg_chunk* __restri
         while (p < n) {
             // ---- one LZMA2 chunk ----
             const u64 hdr = e.pos;
-            const u32 hlen = first ? 6 : 5;
+            const bool over0 = e.over;
+            const u32 hlen = need_props ? 6 : 5;
+            if (need_state) {  // LZMA state reset: probabilities, state, reps
+                __syncthreads();
+                for (u32 i = lane; i < XE_PROBS; i += 64) probs[i] = 1024;
+                __syncthreads();
+                state = 0;
+                rep0 = 0;
+            }
             for (u32 k = 0; k < hlen; k++) e.out(0);
             const u64 data0 = e.pos;
             const u64 u0 = p;
@@ -349,15 +393,33 @@ __global__ __launch_bounds__(64) void xz_encode_kernel(const zcg_chunk* __restri
                 }
             }
             for (int k = 0; k < 5; k++) e.shift_low();  // range coder flush
+            if (e.pos - data0 >= p - u0) {
+                // liblzma's rule: an LZMA chunk that is not smaller than its
+                // input is replaced by an uncompressed chunk (control 1 with a
+                // dictionary reset, else 2; then size-1 big-endian, the bytes).
+                // The input stays in the dictionary; the next LZMA chunk
+                // starts with a state reset.  (usz <= XE_CMAX < 64 KiB.)
+                const u32 usz = (u32)(p - u0) - 1;
+                e.rewind(hdr);
+                e.over = over0;
+                e.out(need_dict ? 0x01u : 0x02u);
+                e.out((usz >> 8) & 0xFF);
+                e.out(usz & 0xFF);
+                e.out_run(u0, p - u0);
+                need_dict = false;
+                need_state = true;
+                continue;
+            }
             const u32 usz = (u32)(p - u0) - 1;
             const u32 csz = (u32)(e.pos - data0) - 1;
-            e.patch(hdr, (first ? 0xE0u : 0x80u) | (usz >> 16));
+            const u32 ctl = need_props ? (need_dict ? 0xE0u : 0xC0u) : (need_state ? 0xA0u : 0x80u);
+            e.patch(hdr, ctl | (usz >> 16));
             e.patch(hdr + 1, (usz >> 8) & 0xFF);
             e.patch(hdr + 2, usz & 0xFF);
             e.patch(hdr + 3, (csz >> 8) & 0xFF);
             e.patch(hdr + 4, csz & 0xFF);
-            if (first) e.patch(hdr + 5, (XE_PB * 5 + 0) * 9 + XE_LC);
-            first = false;
+            if (need_props) e.patch(hdr + 5, (XE_PB * 5 + 0) * 9 + XE_LC);
+            need_dict = need_props = need_state = false;
         }
         e.out(0x00);  // end of LZMA2 data
         const u64 csize = e.pos - cdata0;
@@ -473,7 +535,7 @@ __global__ void xe_keys(const zcg_chunk* __restrict__ chunks, u32 c0, u64 D, u64
     const u32 cl = (u32)(g / D);
     const u64 p = g - (u64)cl * D;
     u32 h = 0;
-    if (p + 4 <= D) h = (xe_ser4((const u8*)chunks[c0 + cl].src, p, t) * 2654435761u) >> (32 - XE_KEYBITS);
+    if (p + 4 <= D && chunks[c0 + cl].src_len >= D) h = (xe_ser4((const u8*)chunks[c0 + cl].src, p, t) * 2654435761u) >> (32 - XE_KEYBITS);
     keys[g] = (cl << cshift) | h;
     vals[g] = (u32)g;
 }
@@ -492,7 +554,7 @@ __global__ void xe_best(const zcg_chunk* __restrict__ chunks, u32 c0, u64 D, u64
     const u32 cl = (u32)(g / D);
     const u64 p = g - (u64)cl * D;
     u32 best = 0, bd = 0;
-    if (p + 4 <= D) {
+    if (p + 4 <= D && chunks[c0 + cl].src_len >= D) {  // short src: INVALID_DATA in the coder
         const u8* src = (const u8*)chunks[c0 + cl].src;
         const u64 cbase = (u64)cl * D;
         const u32 mx = (D - p) < 273 ? (u32)(D - p) : 273u;
