@@ -164,7 +164,7 @@ uint64_t zcg_workspace_bytes(const zcg_array* a, uint32_t n, int encode) {
         return encode ? bzip2_encode_ws_bytes(a, n) : bzip2_decode_ws_bytes(a, n);
     if (a->compression.codec == ZCG_CODEC_XZ && encode) return xz_encode_ws_bytes(a, n);
     if (a->compression.codec == ZCG_CODEC_GZIP && encode) return deflate_ws_bytes(a, n);
-    if (a->compression.codec == ZCG_CODEC_LZ4 && encode) return lz4_encode_ws_bytes(a, n);
+    if (a->compression.codec == ZCG_CODEC_LZ4) return encode ? lz4_encode_ws_bytes(a, n) : lz4_decode_ws_bytes(a, n);
     return 0;
 }
 
@@ -178,7 +178,13 @@ int zcg_decode_batch(zcg_ctx* ctx, const zcg_array* a, const zcg_chunk* d_chunks
     hipError_t e;
     switch (a->compression.codec) {
     case ZCG_CODEC_RAW: e = launch_raw(a, d_chunks, n, d_status, nullptr, 0, s); break;
-    case ZCG_CODEC_LZ4: e = launch_lz4_decode(a, d_chunks, n, d_status, s); break;
+    case ZCG_CODEC_LZ4: {
+        zcg_ctx::Ws* w = nullptr;
+        const int r = stream_ws(ctx, stream, lz4_decode_ws_bytes(a, n), &w);
+        if (r != ZCG_OK) return r;
+        e = launch_lz4_decode(a, d_chunks, n, d_status, w->p, w->bytes, s);
+        break;
+    }
     case ZCG_CODEC_GZIP:
         e = (a->compression.flags & ZCG_FLAG_SERIAL_INFLATE)
                 ? launch_inflate(a, d_chunks, n, d_status, s)

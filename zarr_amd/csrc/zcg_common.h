@@ -241,7 +241,8 @@ struct Workspace;  // defined in zcg_api.cpp
 hipError_t launch_raw(const zcg_array* a, const zcg_chunk* d_chunks, uint32_t n, int32_t* d_status,
                       uint64_t* d_out_len, int encode, hipStream_t s);
 hipError_t launch_lz4_decode(const zcg_array* a, const zcg_chunk* d_chunks, uint32_t n,
-                             int32_t* d_status, hipStream_t s);
+                             int32_t* d_status, void* ws, uint64_t ws_bytes, hipStream_t s);
+uint64_t lz4_decode_ws_bytes(const zcg_array* a, uint32_t n);
 hipError_t launch_lz4_encode(const zcg_array* a, const zcg_chunk* d_chunks, uint32_t n,
                              uint64_t* d_out_len, int32_t* d_status, void* ws, uint64_t ws_bytes,
                              hipStream_t s);

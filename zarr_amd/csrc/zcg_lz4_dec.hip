@@ -1,22 +1,27 @@
 // zcg_lz4_dec.hip — Lz4Compression decode (src/compression/lz.rs:81-83,
 // lz4-rs Decoder = LZ4F_decompress of liblz4 1.9.x) on gfx950.
 //
-// Layout / parallelism (one wave = one workgroup of 64 lanes):
-//   * a wave owns G consecutive chunks (G = 64 / slots-per-chunk), lanes
-//     0..G-1 parse the frame headers and walk the block headers of "their"
-//     chunk into an LDS slot table (one slot per 64 KiB-or-larger block);
-//   * every lane then decodes WHOLE BLOCKS, one block per lane (SIMT across
-//     independent blocks): the LZ4 sequence parse is serial inside a block,
-//     so the parallelism is across blocks, not inside one.  A 1 MiB chunk
-//     written by the reference encoder (lz.rs:85-92: Independent 64 KiB
-//     blocks) gives 16 blocks, so one wave decodes 4 chunks at a time;
-//   * literal and match copies move 16 B per lane per access; matches with
-//     offset < 16 expand their period in registers first;
-//   * block k is placed at k*blockMax (LZ4F emits full blocks except the
-//     last); a block that decodes short before the frame end, a linked-block
-//     frame, or a frame needing more slots is re-decoded by one lane serially
-//     with exact offsets (same code, exact placement) — correctness never
-//     depends on the guess.
+// Three launches per batch (workspace: a 16-byte record per chunk and per
+// block slot):
+//   1. lz4_frames_kernel — one lane per chunk parses the frame header and
+//      walks the block headers into the slot table (block k of a frame is
+//      placed at k*blockMax: LZ4F emits full blocks except the last);
+//   2. lz4_blocks_kernel — ONE WAVE PER BLOCK (lz4-rs writes independent
+//      blocks, lz.rs:88).  The block is decoded in steps over 64-byte windows
+//      of the compressed stream: every lane parses a sequence speculatively at
+//      its own byte (token, length bytes, offset; the window is one 16-byte
+//      load per lane), a scalar walk through the lanes' "next sequence"
+//      offsets (one v_readlane per sequence) marks the true sequence starts,
+//      a wave prefix sum places their output, and each start lane copies its
+//      literals and match (byte-exact ranges, no over-writes, sources read
+//      from the block's own output, L1/L2-hot).  Matches whose source lies in
+//      this step's own output, and long sequences, are copied afterwards in
+//      order by the whole wave (byte k of a match = byte o - d + (k mod d)).
+//      Stored blocks are a coalesced 16 B/lane copy;
+//   3. lz4_finish_kernel — one wave per chunk: per-chunk verdict from the
+//      slots, LZ4F's look-ahead at the next block header, the exact serial
+//      fallback (linked-block frames, a short block mid-frame, frames that
+//      end before N), and the element transform ('>' types, bool).
 // Algorithmic bytes per chunk: C (compressed bytes read once) + D (decoded
 // bytes written once).
 //
@@ -286,172 +291,457 @@ __device__ int lz4_frame_serial(const u8* s, u64 n, u8* dst, u64 D, u32 vflags) 
     return ZCG_OK;
 }
 
-__global__ __launch_bounds__(64) void lz4_decode_kernel(const zcg_chunk* __restrict__ chunks,
-                                                        u32 n, u64 D, DType t, u32 vflags, u32 G,
-                                                        u32 S, i32* __restrict__ status) {
-    extern __shared__ __attribute__((aligned(16))) u8 smem[];
-    // LDS carve: per slot 4 words, per chunk 4 words
-    u32* slot_src = (u32*)smem;                  // [G*S] block data offset in src
-    u32* slot_cs = slot_src + G * S;             // [G*S] raw block size word
-    u32* slot_dec = slot_cs + G * S;             // [G*S] decoded size
-    i32* slot_st = (i32*)(slot_dec + G * S);     // [G*S] block status
-    u32* c_nslot = (u32*)(slot_st + G * S);      // [G]
-    u32* c_bmax = c_nslot + G;                   // [G]
-    u32* c_flags = c_bmax + G;                   // [G]
-    i32* c_st = (i32*)(c_flags + G);             // [G] -1 = needs serial
-    u32* c_jobbase = (u32*)(c_st + G);           // [G+1]
 
-    const int lane = lane_id();
-    const u32 c0 = blockIdx.x * G;
+// ---- slot table (workspace) -------------------------------------------
+struct Lz4ChunkInfo {
+    i32 st;      // header status; -1 = needs the serial path
+    u32 nslot;   // blocks walked into the slot table
+    u32 bmax;    // block maximum size
+    u32 flags;   // F_*
+};
+struct Lz4Slot {
+    u32 src_off;  // block data offset in the stream
+    u32 bs;       // raw block size word (MSB = stored)
+    u32 got;      // decoded bytes
+    i32 st;       // block status
+};
 
-    // ---- phase 1: frame headers + block walk (lane j -> chunk c0+j) ------
-    if ((u32)lane < G) {
-        const u32 j = lane;
-        const u32 c = c0 + j;
-        u32 ns = 0, bmax = 0, fl = 0;
-        int st = ZCG_OK;
-        if (c < n && D > 0) {
-            const zcg_chunk ch = chunks[c];
-            const u8* s = (const u8*)ch.src;
-            Lz4Hdr h = lz4_parse_header(s, ch.src_len);
-            st = h.st;
-            bmax = h.bmax;
-            fl = h.flags;
-            if (st == ZCG_OK && (fl & F_LINKED)) {
-                st = -1;  // serial
-            } else if (st == ZCG_OK) {
-                u64 pos = h.hdr_len;
-                while ((u64)ns * bmax < D) {
-                    if (ns == S) { st = -1; break; }
-                    if (pos + 4 > ch.src_len) { fl |= F_TRUNC; break; }
-                    const u32 bs = ld32(s + pos);
-                    if (bs == 0) { fl |= F_FRAME_END; break; }
-                    const u32 cs = bs & 0x7FFFFFFFu;
-                    if (cs > bmax) { st = ZCG_ERR_INVALID_DATA; break; }
-                    const u64 need = (u64)cs + ((fl & F_BLOCK_CKSUM) ? 4 : 0);
-                    if (pos + 4 + need > ch.src_len) { fl |= F_TRUNC; break; }
-                    slot_src[j * S + ns] = (u32)(pos + 4);
-                    slot_cs[j * S + ns] = bs;
-                    ns++;
-                    pos += 4 + need;
-                }
-                // peek at the header after the last walked block
-                if (st == ZCG_OK && !(fl & (F_TRUNC | F_FRAME_END))) {
-                    if (pos + 4 <= ch.src_len && ld32(s + pos) == 0) fl |= F_FRAME_END;
-                }
-            }
-        } else if (c < n) {
-            st = ZCG_OK;  // N == 0: read_exact of nothing
-        }
-        c_nslot[j] = (st == ZCG_OK) ? ns : 0;
-        c_bmax[j] = bmax;
-        c_flags[j] = fl;
-        c_st[j] = st;
-    }
-    __syncthreads();
-    if (lane == 0) {
-        u32 acc = 0;
-        for (u32 j = 0; j < G; j++) { c_jobbase[j] = acc; acc += c_nslot[j]; }
-        c_jobbase[G] = acc;
-    }
-    __syncthreads();
-
-    // ---- phase 2: one block per lane --------------------------------------
-    const u32 njobs = c_jobbase[G];
-    for (u32 job = lane; job < njobs; job += 64) {
-        u32 j = 0;
-        while (c_jobbase[j + 1] <= job) j++;
-        const u32 k = job - c_jobbase[j];
-        const zcg_chunk ch = chunks[c0 + j];
+// 1. frame header + block walk, one lane per chunk
+__global__ __launch_bounds__(256) void lz4_frames_kernel(const zcg_chunk* __restrict__ chunks, u32 n, u64 D,
+                                                         u32 S, Lz4ChunkInfo* __restrict__ info,
+                                                         Lz4Slot* __restrict__ slots) {
+    const u32 c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= n) return;
+    u32 ns = 0, bmax = 0, fl = 0;
+    int st = ZCG_OK;
+    if (D > 0) {
+        const zcg_chunk ch = chunks[c];
         const u8* s = (const u8*)ch.src;
-        const u32 bmax = c_bmax[j];
-        const u32 bs = slot_cs[j * S + k];
-        const u32 cs = bs & 0x7FFFFFFFu;
-        const u64 so = slot_src[j * S + k];
-        const u64 op0 = (u64)k * bmax;
-        u8* dst = (u8*)ch.dst;
-        int st = ZCG_OK;
-        u32 got = 0;
-        if ((c_flags[j] & F_BLOCK_CKSUM) && !(vflags & ZCG_FLAG_SKIP_LZ4_BLOCK_CHECKSUM)) {
-            if (xxh32(s + so, cs, 0) != ld32(s + so + cs)) st = ZCG_ERR_INVALID_DATA;
-        }
-        if (st == ZCG_OK) {
-            if (bs & 0x80000000u) {
-                const u64 lim = D - op0 < cs ? D - op0 : cs;
-                for (u64 i = 0; i < lim; i += 16) {
-                    if (i + 16 <= lim) st16(dst + op0 + i, ld16(s + so + i));
-                    else for (u64 q = i; q < lim; q++) dst[op0 + q] = s[so + q];
-                }
-                got = cs;
-            } else {
-                st = lz4_block(s + so, cs, ch.src_len - so, dst, op0, bmax, D, op0, &got);
+        const Lz4Hdr h = lz4_parse_header(s, ch.src_len);
+        st = h.st;
+        bmax = h.bmax;
+        fl = h.flags;
+        if (st == ZCG_OK && (fl & F_LINKED)) {
+            st = -1;  // serial
+        } else if (st == ZCG_OK) {
+            u64 pos = h.hdr_len;
+            Lz4Slot* sl = slots + (u64)c * S;
+            while ((u64)ns * bmax < D) {
+                if (ns == S) { st = -1; break; }
+                if (pos + 4 > ch.src_len) { fl |= F_TRUNC; break; }
+                const u32 bs = ld32(s + pos);
+                if (bs == 0) { fl |= F_FRAME_END; break; }
+                const u32 cs = bs & 0x7FFFFFFFu;
+                if (cs > bmax) { st = ZCG_ERR_INVALID_DATA; break; }
+                const u64 need = (u64)cs + ((fl & F_BLOCK_CKSUM) ? 4 : 0);
+                if (pos + 4 + need > ch.src_len) { fl |= F_TRUNC; break; }
+                sl[ns].src_off = (u32)(pos + 4);
+                sl[ns].bs = bs;
+                ns++;
+                pos += 4 + need;
+            }
+            // peek at the header after the last walked block
+            if (st == ZCG_OK && !(fl & (F_TRUNC | F_FRAME_END))) {
+                if (pos + 4 <= ch.src_len && ld32(s + pos) == 0) fl |= F_FRAME_END;
             }
         }
-        slot_dec[j * S + k] = got;
-        slot_st[j * S + k] = st;
     }
-    __syncthreads();
+    info[c] = Lz4ChunkInfo{st, st == ZCG_OK ? ns : 0u, bmax, fl};
+}
 
-    // ---- phase 3: per-chunk verdict; phase 4: serial fallback -------------
-    if ((u32)lane < G && c0 + lane < n) {
-        const u32 j = lane;
-        int st = c_st[j];
+// ---- 2. one wave per block ----------------------------------------------
+// LZ4_decompress_safe of one independent block by one wave, in steps over
+// 64-byte windows of the compressed stream:
+//   * every lane parses a sequence speculatively at its own window byte
+//     (token, length bytes and offset from one 16-byte load), giving the
+//     offset of the next sequence;
+//   * the true chain through the window (it starts at the window's first
+//     byte) comes from pointer doubling over those offsets: lane k finds the
+//     chain's k-th sequence with five ds_bpermute lookups, no serial walk;
+//   * a wave prefix sum (DPP) places the sequences' output; LZ4's output-side
+//     checks run per sequence;
+//   * the step's output bytes are produced byte-parallel into a per-wave LDS
+//     ring of 16-bit entries (a byte, or a pointer to an earlier byte of the
+//     same step), the pointers are resolved (they point strictly backward),
+//     and the bytes are stored to HBM with dword stores.  Match sources older
+//     than the ring come from the block's HBM output behind a workgroup fence.
+// Long sequences (> LZ_LIGHT bytes) go one at a time, LZ_ROUND bytes per round.
+// Positions are block-relative.
+enum : u32 { K_NORMAL = 0, K_LAST = 1, K_ERR = 2 };
+constexpr u32 LZ_LIGHT = 32;
+constexpr u32 LZ_RING = 2048;  // 16-bit entries per wave
+constexpr u32 LZ_RMASK = LZ_RING - 1;
+constexpr u32 LZ_ROUND = 1024;
+constexpr u32 LZ_PTR = 0x8000u;
+
+__device__ __forceinline__ u32x4 gwin_load(const gu8* __restrict__ src, u32 q, u64 avail) {
+    if (q + 16 <= avail) return *(const gu32x4_ua*)(src + q);
+    u64 lo = 0, hi = 0;
+    for (u32 k = 0; k < 16; k++) {
+        const u64 b = (q + k < avail) ? (u64)src[q + k] : 0ull;
+        if (k < 8) lo |= b << (8 * k);
+        else hi |= b << (8 * (k - 8));
+    }
+    return u32x4{(u32)lo, (u32)(lo >> 32), (u32)hi, (u32)(hi >> 32)};
+}
+
+// One LZ4 sequence parsed at block offset x (LZ4_decompress_safe's input-side
+// rules; the output-side rules need the output position and are applied
+// after the prefix sum).  Speculative: x need not be a true sequence start.
+struct LzSeq {
+    u32 kind;  // K_NORMAL, K_LAST (literals up to the block end), K_ERR
+    u32 adv;   // bytes to the next sequence (K_NORMAL)
+    u32 lit, lo, off, ml;  // literal count, literal start - x, offset, match length
+};
+
+__device__ __forceinline__ LzSeq lz4_seq_at(const gu8* __restrict__ s, u32 iend, u64 avail, u32 x) {
+    LzSeq q{K_ERR, 0, 0, 0, 0, 0};
+    if (x >= iend) return q;  // no token left: LZ4_decompress_safe's `ip >= iend` error
+    const u32x4 w = gwin_load(s, x, avail);
+    auto B = [&](u32 p) -> u32 {
+        const u32 d = p - x;
+        return d < 16 ? win_byte(w, d) : (u32)s[p];
+    };
+    const u32 tok = win_byte(w, 0);
+    u32 lit = tok >> 4;
+    u32 ip = x + 1;
+    const int ie = (int)iend;
+    if (lit == 15) {
+        if ((int)ip >= ie - 15) return q;
+        u32 b;
+        do {
+            b = B(ip++);
+            lit += b;
+        } while (b == 255 && (int)ip < ie - 15);
+    }
+    q.lit = lit;
+    q.lo = ip - x;
+    if ((i64)ip + lit > (i64)ie - 8) {  // must be the last sequence: consume the input exactly
+        q.kind = ((u64)ip + lit == iend) ? K_LAST : K_ERR;
+        return q;
+    }
+    ip += lit;
+    q.off = B(ip) | (B(ip + 1) << 8);
+    ip += 2;
+    u32 ml = tok & 15;
+    if (ml == 15) {
+        u32 b;
+        do {
+            b = B(ip++);
+            ml += b;
+            if ((int)ip >= ie - 4) return q;
+        } while (b == 255);
+    }
+    q.ml = ml + 4;
+    q.kind = K_NORMAL;
+    q.adv = ip - x;
+    return q;
+}
+
+// inclusive prefix sum over the wave
+__device__ __forceinline__ u32 wave_incl_scan(u32 v) {
+    const u32 lane = (u32)lane_id();
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const u32 t = (u32)__shfl_up((int)v, d);
+        if (lane >= (u32)d) v += t;
+    }
+    return v;
+}
+
+struct LzRing {
+    u16* r;           // this wave's ring (LDS)
+    const gu8* s;     // compressed block
+    gu8* dst;         // the block's output
+    u32 lim;          // stored bytes of the block (N*size clips the last block)
+    u32 fenced;       // HBM output below this position is visible to the wave's loads
+
+    // entry of output byte j of a sequence at o (lit literals from the stream
+    // at lsrc, then match bytes at distance off), in a round [rb, rb+rn)
+    __device__ __forceinline__ u32 entry(u32 o, u32 lsrc, u32 lit, u32 off, u32 j, u32 rb, u32 rn) const {
+        if (j < lit) return s[lsrc + j];
+        if (off == 0) return 0;  // lz4 1.9.3 decodes offset 0 to zeros
+        u32 m = j - lit;
+        if (m >= off) m %= off;
+        const u32 src = o + lit - off + m;  // < the byte itself
+        if (src >= rb) return LZ_PTR | (src & LZ_RMASK);
+        if (src + LZ_RING >= rb + rn) return r[src & LZ_RMASK];
+        return dst[src];
+    }
+    // resolve [rb, rb+rn) (4 bytes per lane per pass) and store it to HBM
+    __device__ __forceinline__ void finish(u32 rb, u32 rn) {
+        const u32 lane = (u32)lane_id();
+        for (u32 i0 = lane * 4; i0 < rn; i0 += 256) {
+            u32 v[4];
+#pragma unroll
+            for (u32 t = 0; t < 4; t++) v[t] = i0 + t < rn ? r[(rb + i0 + t) & LZ_RMASK] : 0u;
+            u32 wasp = 0;
+#pragma unroll
+            for (u32 t = 0; t < 4; t++) {
+                if (v[t] & LZ_PTR) {
+                    wasp |= 1u << t;
+                    do { v[t] = r[v[t] & LZ_RMASK]; } while (v[t] & LZ_PTR);
+                }
+            }
+            if (wasp) {
+#pragma unroll
+                for (u32 t = 0; t < 4; t++)
+                    if (wasp & (1u << t)) r[(rb + i0 + t) & LZ_RMASK] = (u16)v[t];
+            }
+            const u32 wv = v[0] | (v[1] << 8) | (v[2] << 16) | (v[3] << 24);
+            const u32 p = rb + i0;
+            if (i0 + 4 <= rn && p + 4 <= lim) {
+                *(gu32*)(dst + p) = wv;  // unaligned dword store (gfx950 allows it)
+            } else {
+                for (u32 t = 0; t < 4 && i0 + t < rn; t++)
+                    if (p + t < lim) dst[p + t] = (u8)(wv >> (8 * t));
+            }
+        }
+    }
+    // make HBM output below `need` visible before a round reads it
+    __device__ __forceinline__ void need_visible(u32 need, u32 op) {
+        if (need > fenced) {
+            __threadfence_block();
+            fenced = op;
+        }
+    }
+};
+
+//   s/iend: the compressed block; avail: readable bytes from s
+//   dst: the block's output; cap: blockMax; lim: bytes of the block below N*size
+__device__ void lz4_block_wave(const gu8* __restrict__ s, u32 iend, u64 avail, gu8* dst, u32 cap, u32 lim,
+                               u16* ring, u32* got_out, int* st_out) {
+    const u32 lane = (u32)lane_id();
+    LzRing R{ring, s, dst, lim, 0};
+    u32 e = 0;   // block offset of the window's first (true) sequence
+    u32 op = 0;  // output position
+    int st = ZCG_OK;
+    for (;;) {
+        const LzSeq q = lz4_seq_at(s, iend, avail, e + lane);
+        // chain by pointer doubling: J^(2^b)(x) for x < 64; values >= 64 are
+        // exits (a next sequence beyond the window), 255 a terminal sequence
+        const u32 nx = q.kind == K_NORMAL ? lane + q.adv : 0xFFFFFFFFu;  // next sequence (window offset)
+        const u32 j1 = nx < 64 ? nx : (nx == 0xFFFFFFFFu ? 255u : 64u);
+        u32 jt[5];
+        jt[0] = j1;
+#pragma unroll
+        for (int b = 1; b < 5; b++) {
+            const u32 y = (u32)__shfl((int)jt[b - 1], (int)(jt[b - 1] & 63));
+            jt[b] = jt[b - 1] < 64 ? y : jt[b - 1];
+        }
+        u32 pos = 0;  // lane k: the chain's k-th sequence (k < 32)
+#pragma unroll
+        for (int b = 0; b < 5; b++) {
+            const u32 y = (u32)__shfl((int)jt[b], (int)(pos & 63));
+            if (((lane >> b) & 1) && pos < 64) pos = y;
+        }
+        const bool valid = lane < 32 && pos < 64;
+        const u32 nseq = (u32)__builtin_popcountll(__ballot(valid));
+        // the sequence after the last one in the window: an exit offset, or 255
+        const u32 last_next = (u32)__builtin_amdgcn_readlane((int)__shfl((int)nx, (int)(pos & 63)), (int)(nseq - 1));
+        const bool term = last_next == 0xFFFFFFFFu;
+        // gather the k-th sequence's fields
+        const u32 sp = pos & 63;
+        // (every shuffle runs on all lanes: a bpermute reads 0 from lanes outside EXEC)
+        const u32 gkind = (u32)__shfl((int)q.kind, (int)sp);
+        const u32 kkind = valid ? gkind : (u32)K_NORMAL;
+        const u32 klit = (u32)__shfl((int)q.lit, (int)sp);
+        const u32 kml = (u32)__shfl((int)q.ml, (int)sp);
+        const u32 koff = (u32)__shfl((int)q.off, (int)sp);
+        const u32 klo = (u32)__shfl((int)q.lo, (int)sp);
+        const bool norm = valid && kkind == K_NORMAL;
+        const u32 len = valid && kkind != K_ERR ? klit + (norm ? kml : 0u) : 0u;
+        const u32 incl = wave_incl_scan(len);
+        const u32 total = (u32)__builtin_amdgcn_readlane((int)incl, 63);
+        const u32 excl = incl - len;
+        const u32 o = op + excl;
+        // the output-side rules of LZ4_decompress_safe (u64: lengths may be huge on corrupt input)
+        bool err = false;
+        if (valid) {
+            const u64 cpy = (u64)o + klit;
+            if (kkind == K_ERR) err = true;
+            else if (kkind == K_LAST) err = cpy > cap;
+            else err = (cpy + 12 > cap) || (cpy < koff) || (cpy + kml + 5 > cap);
+        }
+        if (__ballot(err)) { st = ZCG_ERR_INVALID_DATA; break; }
+        const u32 koffn = norm ? koff : 0u;
+        const u32 klsrc = e + sp + klo;
+        const bool heavy = __ballot(valid && len > LZ_LIGHT) != 0;
+        if (!heavy && total <= LZ_ROUND) {
+            // one round, byte-parallel: byte i belongs to the last k with excl_k <= i
+            const u32 pk = klit | ((klsrc - e) << 6) | (koffn << 16);  // lit <= 32, klsrc - e <= 66
+            R.need_visible(op + total > LZ_RING ? op + total - LZ_RING : 0, op);
+            for (u32 i0 = 0; i0 < total; i0 += 64) {  // wave-uniform: every lane takes part in the shuffles
+                const u32 i = i0 + lane;
+                u32 r = 0;
+#pragma unroll
+                for (u32 stp = 16; stp; stp >>= 1) {
+                    const u32 c = r + stp;
+                    const u32 oc = (u32)__shfl((int)excl, (int)(c & 63));
+                    if (c < nseq && oc <= i) r = c;
+                }
+                const u32 ro = (u32)__shfl((int)excl, (int)r);
+                const u32 rp = (u32)__shfl((int)pk, (int)r);
+                if (i < total)
+                    ring[(op + i) & LZ_RMASK] = (u16)R.entry(op + ro, e + ((rp >> 6) & 127), rp & 63, rp >> 16,
+                                                             i - ro, op, total);
+            }
+            R.finish(op, total);
+        } else {
+            // long sequences: one at a time, LZ_ROUND bytes per round, the
+            // bytes spread over the lanes
+            for (u32 k = 0; k < nseq; k++) {
+                const u32 kl = (u32)__builtin_amdgcn_readlane((int)klit, (int)k);
+                const u32 ks = (u32)__builtin_amdgcn_readlane((int)klsrc, (int)k);
+                const u32 ko = (u32)__builtin_amdgcn_readlane((int)koffn, (int)k);
+                const u32 kn = (u32)__builtin_amdgcn_readlane((int)len, (int)k);
+                const u32 kpos = op + (u32)__builtin_amdgcn_readlane((int)excl, (int)k);
+                for (u32 r0 = 0; r0 < kn; r0 += LZ_ROUND) {
+                    const u32 rn = kn - r0 < LZ_ROUND ? kn - r0 : LZ_ROUND;
+                    const u32 rb = kpos + r0;
+                    R.need_visible(rb + rn > LZ_RING ? rb + rn - LZ_RING : 0, rb);
+                    for (u32 j = lane; j < rn; j += 64)
+                        ring[(rb + j) & LZ_RMASK] = (u16)R.entry(kpos, ks, kl, ko, r0 + j, rb, rn);
+                    R.finish(rb, rn);
+                }
+            }
+        }
+        op += total;
+        if (term) break;
+        e += last_next;
+    }
+    *got_out = op;
+    *st_out = st;
+}
+
+__global__ __launch_bounds__(256) void lz4_blocks_kernel(const zcg_chunk* __restrict__ chunks, u32 n, u64 D,
+                                                         u32 S, u32 vflags, const Lz4ChunkInfo* __restrict__ info,
+                                                         Lz4Slot* __restrict__ slots) {
+    __shared__ u16 rings[4][LZ_RING];
+    // the wave index is wave-uniform: readfirstlane lets the compiler keep the
+    // whole block walk in scalar registers and scalar branches
+    const u32 wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const u64 w = (u64)blockIdx.x * 4 + wv;
+    u16* ring = rings[wv];
+    const u32 c = (u32)(w / S);
+    const u32 k = (u32)(w - (u64)c * S);
+    if (c >= n) return;
+    const Lz4ChunkInfo ci = info[c];
+    if (ci.st != ZCG_OK || k >= ci.nslot) return;
+    const int lane = lane_id();
+    const zcg_chunk ch = chunks[c];
+    Lz4Slot* sl = slots + (u64)c * S + k;
+    const u32 bs = sl->bs;
+    const u32 cs = bs & 0x7FFFFFFFu;
+    const u64 so = sl->src_off;
+    const gu8* s = (const gu8*)ch.src + so;
+    gu8* dst = (gu8*)ch.dst;
+    const u64 op0 = (u64)k * ci.bmax;
+    int st = ZCG_OK;
+    u32 got = 0;
+    if ((ci.flags & F_BLOCK_CKSUM) && !(vflags & ZCG_FLAG_SKIP_LZ4_BLOCK_CHECKSUM)) {
+        u32 bad = 0;
+        if (lane == 0) bad = xxh32((const u8*)s, cs, 0) != ld32((const u8*)s + cs);
+        if (__builtin_amdgcn_readfirstlane(bad)) st = ZCG_ERR_INVALID_DATA;
+    }
+    if (st == ZCG_OK) {
+        if (bs & 0x80000000u) {  // stored block: coalesced copy
+            const u64 lim = D - op0 < cs ? D - op0 : cs;
+            for (u64 i = (u64)lane * 16; i < lim; i += 1024) {
+                if (i + 16 <= lim) *(gu32x4_ua*)(dst + op0 + i) = *(const gu32x4_ua*)(s + i);
+                else for (u64 q = i; q < lim; q++) dst[op0 + q] = s[q];
+            }
+            got = cs;
+        } else {
+            const u64 lb = D - op0 < ci.bmax ? D - op0 : ci.bmax;
+            lz4_block_wave(s, cs, ch.src_len - so, dst + op0, ci.bmax, (u32)lb, ring, &got, &st);
+        }
+    }
+    if (lane == 0) {
+        sl->got = got;
+        sl->st = st;
+    }
+}
+
+// ---- 3. per-chunk verdict, serial fallback, element transform -----------
+__global__ __launch_bounds__(64) void lz4_finish_kernel(const zcg_chunk* __restrict__ chunks, u32 n, u64 D,
+                                                        DType t, u32 vflags, u32 S,
+                                                        const Lz4ChunkInfo* __restrict__ info,
+                                                        const Lz4Slot* __restrict__ slots,
+                                                        i32* __restrict__ status) {
+    const u32 c = blockIdx.x;
+    if (c >= n) return;
+    const int lane = lane_id();
+    __shared__ int st_s;
+    if (lane == 0) {
+        const Lz4ChunkInfo ci = info[c];
+        const Lz4Slot* sl = slots + (u64)c * S;
+        int st = ci.st;
         if (st == ZCG_OK && D > 0) {
-            const u32 ns = c_nslot[j];
-            const u32 bmax = c_bmax[j];
+            const u32 ns = ci.nslot, bmax = ci.bmax;
             u64 total = 0;
             for (u32 k = 0; k < ns; k++) {
-                if (slot_st[j * S + k] != ZCG_OK) { st = slot_st[j * S + k]; break; }
-                const u32 got = slot_dec[j * S + k];
+                if (sl[k].st != ZCG_OK) { st = sl[k].st; break; }
+                const u32 got = sl[k].got;
                 total = (u64)k * bmax + got;
                 if (got != bmax && k + 1 < ns) { st = -1; break; }  // short block mid-frame
             }
             if (st == ZCG_OK && total == D && ns > 0) {  // last block ended exactly at N
-                const zcg_chunk ch = chunks[c0 + j];
-                const u32 k = ns - 1;
-                const u64 pos = (u64)slot_src[j * S + k] + (slot_cs[j * S + k] & 0x7FFFFFFFu) +
-                                ((c_flags[j] & F_BLOCK_CKSUM) ? 4 : 0);
+                const zcg_chunk ch = chunks[c];
+                const u64 pos = (u64)sl[ns - 1].src_off + (sl[ns - 1].bs & 0x7FFFFFFFu) +
+                                ((ci.flags & F_BLOCK_CKSUM) ? 4 : 0);
                 st = lz4_next_header_check((const u8*)ch.src, ch.src_len, pos, bmax);
             }
             if (st == ZCG_OK && total < D) {
                 // frame ended / input ran out before N bytes; a short last
-                // block followed by more blocks means the guess failed.
-                if (c_flags[j] & F_TRUNC) st = ZCG_ERR_UNEXPECTED_EOF;
-                else if (c_flags[j] & F_FRAME_END)  // suffix checks: exact serial path
-                    st = (c_flags[j] & (F_CONTENT_CKSUM | F_CONTENT_SIZE)) ? -1 : ZCG_ERR_UNEXPECTED_EOF;
+                // block followed by more blocks means the placement guess failed
+                if (ci.flags & F_TRUNC) st = ZCG_ERR_UNEXPECTED_EOF;
+                else if (ci.flags & F_FRAME_END)  // suffix checks: exact serial path
+                    st = (ci.flags & (F_CONTENT_CKSUM | F_CONTENT_SIZE)) ? -1 : ZCG_ERR_UNEXPECTED_EOF;
                 else st = -1;
             }
         }
         if (st == -1) {
-            const zcg_chunk ch = chunks[c0 + j];
+            const zcg_chunk ch = chunks[c];
             st = lz4_frame_serial((const u8*)ch.src, ch.src_len, (u8*)ch.dst, D, vflags);
         }
-        c_st[j] = st;
-        status[c0 + j] = st;
+        status[c] = st;
+        st_s = st;
     }
     __syncthreads();
-
-    // ---- phase 5: element transform ('>' types, bool) ---------------------
-    if (t.swap || t.isbool) {
+    if ((t.swap || t.isbool) && st_s == ZCG_OK) {
         __threadfence_block();
-        for (u32 j = 0; j < G && c0 + j < n; j++)
-            if (c_st[j] == ZCG_OK) wave_transform((u8*)chunks[c0 + j].dst, D, t);
+        wave_transform((u8*)chunks[c].dst, D, t);
     }
 }
 
-hipError_t launch_lz4_decode(const zcg_array* a, const zcg_chunk* d_chunks, uint32_t n,
-                             int32_t* d_status, hipStream_t s) {
+uint64_t lz4_decode_ws_bytes(const zcg_array* a, uint32_t n) {
+    const DType t = make_dtype(a->dtype);
+    const u64 D = a->chunk_num_elements * (u64)t.es;
+    u64 S = (D + LZ4_MIN_BMAX - 1) / LZ4_MIN_BMAX;
+    if (S < 1) S = 1;
+    return ((u64)n * sizeof(Lz4ChunkInfo) + 255) / 256 * 256 + (u64)n * S * sizeof(Lz4Slot);
+}
+
+hipError_t launch_lz4_decode(const zcg_array* a, const zcg_chunk* d_chunks, uint32_t n, int32_t* d_status,
+                             void* ws, uint64_t ws_bytes, hipStream_t s) {
     if (n == 0) return hipSuccess;
     const DType t = make_dtype(a->dtype);
     const u64 D = a->chunk_num_elements * (u64)t.es;
     u64 S = (D + LZ4_MIN_BMAX - 1) / LZ4_MIN_BMAX;
     if (S < 1) S = 1;
-    if (S > 8192) return hipErrorInvalidValue;  // > 512 MiB chunks: not supported
-    const u32 G = S >= 64 ? 1u : (u32)(64 / S);
-    const size_t lds = (size_t)G * S * 16 + (size_t)G * 16 + (G + 1) * 4 + 16;
-    const u32 grid = (n + G - 1) / G;
-    hipLaunchKernelGGL(lz4_decode_kernel, dim3(grid), dim3(64), lds, s, d_chunks, n, D, t,
-                       a->compression.flags, G, (u32)S, d_status);
+    if (S > 65536 || ws_bytes < lz4_decode_ws_bytes(a, n)) return hipErrorInvalidValue;
+    Lz4ChunkInfo* info = (Lz4ChunkInfo*)ws;
+    Lz4Slot* slots = (Lz4Slot*)((u8*)ws + ((u64)n * sizeof(Lz4ChunkInfo) + 255) / 256 * 256);
+    hipLaunchKernelGGL(lz4_frames_kernel, dim3((n + 255) / 256), dim3(256), 0, s, d_chunks, n, D, (u32)S, info,
+                       slots);
+    const u64 waves = (u64)n * S;
+    if ((waves + 3) / 4 > 0x7FFFFFFFull) return hipErrorInvalidValue;
+    if (D > 0)
+        hipLaunchKernelGGL(lz4_blocks_kernel, dim3((u32)((waves + 3) / 4)), dim3(256), 0, s, d_chunks, n, D,
+                           (u32)S, a->compression.flags, (const Lz4ChunkInfo*)info, slots);
+    hipLaunchKernelGGL(lz4_finish_kernel, dim3(n), dim3(64), 0, s, d_chunks, n, D, t, a->compression.flags,
+                       (u32)S, (const Lz4ChunkInfo*)info, (const Lz4Slot*)slots, d_status);
     return hipGetLastError();
 }
 
