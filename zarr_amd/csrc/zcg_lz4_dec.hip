@@ -373,6 +373,9 @@ constexpr u32 LZ_RING = 2048;  // 16-bit entries per wave
 constexpr u32 LZ_RMASK = LZ_RING - 1;
 constexpr u32 LZ_ROUND = 1024;
 constexpr u32 LZ_PTR = 0x8000u;
+#ifndef LZ_PREFETCH
+#define LZ_PREFETCH 1
+#endif
 
 __device__ __forceinline__ u32x4 gwin_load(const gu8* __restrict__ src, u32 q, u64 avail) {
     if (q + 16 <= avail) return *(const gu32x4_ua*)(src + q);
@@ -394,10 +397,17 @@ struct LzSeq {
     u32 lit, lo, off, ml;  // literal count, literal start - x, offset, match length
 };
 
-__device__ __forceinline__ LzSeq lz4_seq_at(const gu8* __restrict__ s, u32 iend, u64 avail, u32 x) {
+// the 16 stream bytes at e + lane for every lane of the wave (wave-uniform bounds test)
+__device__ __forceinline__ u32x4 gwin_wave(const gu8* __restrict__ src, u32 e, u64 avail) {
+    const u32 lane = (u32)lane_id();
+    if ((u64)e + 80 <= avail) return *(const gu32x4_ua*)(src + e + lane);
+    return gwin_load(src, e + lane, avail);
+}
+
+// w: the 16 stream bytes at x
+__device__ __forceinline__ LzSeq lz4_seq_at(const gu8* __restrict__ s, u32 iend, const u32x4& w, u32 x) {
     LzSeq q{K_ERR, 0, 0, 0, 0, 0};
     if (x >= iend) return q;  // no token left: LZ4_decompress_safe's `ip >= iend` error
-    const u32x4 w = gwin_load(s, x, avail);
     auto B = [&](u32 p) -> u32 {
         const u32 d = p - x;
         return d < 16 ? win_byte(w, d) : (u32)s[p];
@@ -438,15 +448,18 @@ __device__ __forceinline__ LzSeq lz4_seq_at(const gu8* __restrict__ s, u32 iend,
     return q;
 }
 
-// inclusive prefix sum over the wave
+// inclusive prefix sum over the wave: DPP row shifts within each 16-lane row,
+// then the three row totals (v_readlane) added to the rows above them
 __device__ __forceinline__ u32 wave_incl_scan(u32 v) {
+    v += (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
+    v += (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
+    v += (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
+    v += (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
+    const u32 t0 = (u32)__builtin_amdgcn_readlane((int)v, 15);
+    const u32 t1 = t0 + (u32)__builtin_amdgcn_readlane((int)v, 31);
+    const u32 t2 = t1 + (u32)__builtin_amdgcn_readlane((int)v, 47);
     const u32 lane = (u32)lane_id();
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const u32 t = (u32)__shfl_up((int)v, d);
-        if (lane >= (u32)d) v += t;
-    }
-    return v;
+    return v + (lane < 16 ? 0u : (lane < 32 ? t0 : (lane < 48 ? t1 : t2)));
 }
 
 struct LzRing {
@@ -507,17 +520,41 @@ struct LzRing {
     }
 };
 
+// Debug counters (flag ZCG_FLAG_DEBUG_COUNTERS), summed over all blocks:
+// steps, heavy steps, bytes, cycles of parse / chain / entries / finish / total.
+__device__ unsigned long long g_lz_dbg[16];
+extern "C" int zcg__debug_lz4_counters(unsigned long long* out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_lz_dbg), sizeof(unsigned long long) * 16) != hipSuccess) return -1;
+    if (reset) {
+        unsigned long long z[16] = {0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_lz_dbg), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+
 //   s/iend: the compressed block; avail: readable bytes from s
 //   dst: the block's output; cap: blockMax; lim: bytes of the block below N*size
 __device__ void lz4_block_wave(const gu8* __restrict__ s, u32 iend, u64 avail, gu8* dst, u32 cap, u32 lim,
-                               u16* ring, u32* got_out, int* st_out) {
+                               u16* ring, bool dbg, u32* got_out, int* st_out) {
     const u32 lane = (u32)lane_id();
+    u64 dc[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // steps, heavy, -, parse, chain, entries, finish, total
+    u64 tp = dbg ? __builtin_readcyclecounter() : 0;
+    const u64 tstart = tp;
+#define LZ_T(slot)                                              \
+    if (dbg) {                                                  \
+        const u64 _t = __builtin_readcyclecounter();            \
+        dc[slot] += _t - tp;                                    \
+        tp = _t;                                                \
+    }
     LzRing R{ring, s, dst, lim, 0};
     u32 e = 0;   // block offset of the window's first (true) sequence
     u32 op = 0;  // output position
     int st = ZCG_OK;
+    u32x4 w = gwin_wave(s, 0, avail);  // this window's stream bytes (lane l: e + l ..)
     for (;;) {
-        const LzSeq q = lz4_seq_at(s, iend, avail, e + lane);
+        const LzSeq q = lz4_seq_at(s, iend, w, e + lane);
+        dc[0]++;
+        LZ_T(3)
         // chain by pointer doubling: J^(2^b)(x) for x < 64; values >= 64 are
         // exits (a next sequence beyond the window), 255 a terminal sequence
         const u32 nx = q.kind == K_NORMAL ? lane + q.adv : 0xFFFFFFFFu;  // next sequence (window offset)
@@ -540,6 +577,9 @@ __device__ void lz4_block_wave(const gu8* __restrict__ s, u32 iend, u64 avail, g
         // the sequence after the last one in the window: an exit offset, or 255
         const u32 last_next = (u32)__builtin_amdgcn_readlane((int)__shfl((int)nx, (int)(pos & 63)), (int)(nseq - 1));
         const bool term = last_next == 0xFFFFFFFFu;
+#if LZ_PREFETCH
+        const u32x4 wn = gwin_wave(s, term ? e : e + last_next, avail);  // next window, in flight during the copies
+#endif
         // gather the k-th sequence's fields
         const u32 sp = pos & 63;
         // (every shuffle runs on all lanes: a bpermute reads 0 from lanes outside EXEC)
@@ -567,6 +607,7 @@ __device__ void lz4_block_wave(const gu8* __restrict__ s, u32 iend, u64 avail, g
         const u32 koffn = norm ? koff : 0u;
         const u32 klsrc = e + sp + klo;
         const bool heavy = __ballot(valid && len > LZ_LIGHT) != 0;
+        LZ_T(4)
         if (!heavy && total <= LZ_ROUND) {
             // one round, byte-parallel: byte i belongs to the last k with excl_k <= i
             const u32 pk = klit | ((klsrc - e) << 6) | (koffn << 16);  // lit <= 32, klsrc - e <= 66
@@ -582,12 +623,27 @@ __device__ void lz4_block_wave(const gu8* __restrict__ s, u32 iend, u64 avail, g
                 }
                 const u32 ro = (u32)__shfl((int)excl, (int)r);
                 const u32 rp = (u32)__shfl((int)pk, (int)r);
-                if (i < total)
-                    ring[(op + i) & LZ_RMASK] = (u16)R.entry(op + ro, e + ((rp >> 6) & 127), rp & 63, rp >> 16,
-                                                             i - ro, op, total);
+                const u32 rlit = rp & 63, rsrc = (rp >> 6) & 127;  // literal start, window-relative
+                const u32 c = rsrc + (i - ro);                    // this byte's stream byte if a literal
+                const u32 wlit = (u32)__shfl((int)w.x, (int)(c & 63)) & 0xFF;
+                if (i < total) {
+                    const u32 ix = (op + i) & LZ_RMASK;
+                    u32 v;
+                    if (i - ro < rlit) v = c < 64 ? wlit : (u32)s[e + c];
+                    else v = R.entry(op + ro + rlit, 0, 0, rp >> 16, i - ro - rlit, op, total);  // the match part
+                    ring[ix] = (u16)v;
+                    // every byte of this pass is in the ring now (LDS operations of a
+                    // wave complete in order): resolve, write back, store to HBM
+                    if (v & LZ_PTR) {
+                        do { v = ring[v & LZ_RMASK]; } while (v & LZ_PTR);
+                        ring[ix] = (u16)v;
+                    }
+                    if (op + i < lim) dst[op + i] = (u8)v;
+                }
             }
-            R.finish(op, total);
+            LZ_T(5)
         } else {
+            dc[1]++;
             // long sequences: one at a time, LZ_ROUND bytes per round, the
             // bytes spread over the lanes
             for (u32 k = 0; k < nseq; k++) {
@@ -609,7 +665,23 @@ __device__ void lz4_block_wave(const gu8* __restrict__ s, u32 iend, u64 avail, g
         op += total;
         if (term) break;
         e += last_next;
+#if LZ_PREFETCH
+        w = wn;
+#else
+        w = gwin_wave(s, e, avail);
+#endif
     }
+    if (dbg) {
+        dc[7] = __builtin_readcyclecounter() - tstart;
+        dc[2] = op;
+        if (lane < 8) {
+            u64 v = 0;
+#pragma unroll
+            for (u32 k = 0; k < 8; k++) v = lane == k ? dc[k] : v;
+            atomicAdd(&g_lz_dbg[lane], (unsigned long long)v);
+        }
+    }
+#undef LZ_T
     *got_out = op;
     *st_out = st;
 }
@@ -654,7 +726,8 @@ __global__ __launch_bounds__(256) void lz4_blocks_kernel(const zcg_chunk* __rest
             got = cs;
         } else {
             const u64 lb = D - op0 < ci.bmax ? D - op0 : ci.bmax;
-            lz4_block_wave(s, cs, ch.src_len - so, dst + op0, ci.bmax, (u32)lb, ring, &got, &st);
+            lz4_block_wave(s, cs, ch.src_len - so, dst + op0, ci.bmax, (u32)lb, ring,
+                           (vflags & ZCG_FLAG_DEBUG_COUNTERS) != 0, &got, &st);
         }
     }
     if (lane == 0) {
