@@ -259,3 +259,80 @@ def test_write_ndarray_random_vs_oracle(tmp_path, seed):
         got = h.read_chunk("a", meta, list(c), npdt)
         assert got is not None, c
         assert np.array_equal(got.get_data(), np.asarray(want, npdt)), c
+
+
+@pytest.mark.parametrize("es,order,istride_c,unaligned", [(1, "F", False, True), (2, "F", False, True),
+                                                          (4, "F", True, False), (8, "F", False, True),
+                                                          (2, "C", True, True)])
+def test_write_region_device_long_rows(es, order, istride_c, unaligned):
+    """zcg_write_region's row-per-wave path (box rows of >= 32*16/es elements
+    along the fast dimension): rows that start at unaligned offsets inside a
+    chunk, absent (NULL) chunks that must stay untouched, and a strided input
+    view; compared with region_ref.write_ndarray's element placement."""
+    import torch
+    from zarr_amd.region import region_grid, scatter_region, _strides
+    dt = {1: np.uint8, 2: np.int16, 4: np.int32, 8: np.int64}[es]
+    ts = {1: "u1", 2: "<i2", 4: "<i4", 8: "<i8"}[es]
+    if order == "C":
+        meta = ArrayMetadata.new([9, 50, 900], [4, 7, 301], ts)
+        off, shp = ([1, 3, 13] if unaligned else [0, 0, 0]), [8, 40, 880]
+    else:
+        meta = ArrayMetadata.new([900, 50, 9], [301, 7, 4], ts)
+        off, shp = ([13, 3, 1] if unaligned else [0, 0, 0]), [880, 40, 8]
+    meta.chunk_memory_layout = order
+    bbox = BoundingBox(off, shp)
+    lo, n = region_grid(meta, bbox)
+    coords = list(itertools.product(*[range(a, a + k) for a, k in zip(lo, n)]))
+    cs = meta.chunk_shape
+    N = int(np.prod(cs))
+    rng = np.random.default_rng(40 + es)
+    chunks = {c: rng.integers(0, 100, N).astype(dt) for c in coords}
+    absent = set(c for c in coords if rng.random() < 0.2)
+    box = rng.integers(0, 100, shp).astype(dt)
+    # expected: the oracle's write_ndarray placement on the present chunks
+    want = {c: v.copy() for c, v in chunks.items() if c not in absent}
+    region_ref.write_ndarray(meta.shape, cs, order, off, box, want, 0)
+    dev = torch.device("cuda", 0)
+    host = np.stack([chunks[c] for c in coords]).reshape(-1)
+    slots = torch.from_numpy(host.view(np.uint8).copy()).to(dev)
+    table = torch.tensor([0 if c in absent else slots.data_ptr() + i * N * es for i, c in enumerate(coords)],
+                         dtype=torch.int64, device=dev)
+    st = _strides(shp, "C" if istride_c else order)
+    flat = np.empty(int(np.prod(shp)), dt)
+    view = np.ndarray(tuple(shp), dtype=dt, buffer=flat, strides=tuple(s * es for s in st))
+    view[...] = box
+    boxd = torch.from_numpy(flat.view(np.uint8).copy()).to(dev)
+    scatter_region(meta, bbox, es, table, boxd, st)
+    torch.cuda.synchronize()
+    got = slots.cpu().numpy().view(dt).reshape(len(coords), N)
+    for i, c in enumerate(coords):
+        exp = chunks[c] if c in absent else want[c]
+        assert np.array_equal(got[i], exp), c
+
+
+def test_write_ndarray_sub_batches(tmp_path, monkeypatch):
+    """write_ndarray split into several sub-batches (a small byte budget):
+    chunks outside a sub-batch are NULL in that region call, and every chunk
+    still ends up equal to the oracle's."""
+    import zarr_amd.region as R
+    from zarr_amd.region import write_ndarray
+    monkeypatch.setattr(R, "WRITE_BATCH_BYTES", 3 * 1024)
+    rng = np.random.default_rng(77)
+    shape, cs = [30, 20, 10], [4, 3, 5]
+    meta = ArrayMetadata.new(shape, cs, "<i4", Gzip(1))
+    h = FilesystemHierarchy.open_or_create(str(tmp_path))
+    h.create_array("a", meta)
+    chunks = {}
+    n_el = int(np.prod(cs))
+    for c in itertools.product(*[range((s + k - 1) // k) for s, k in zip(shape, cs)]):
+        if rng.random() < 0.5:
+            d = rng.integers(0, 1000, n_el).astype(np.int32)
+            chunks[c] = d
+            h.write_chunk("a", meta, SliceDataChunk(list(c), d))
+    off, shp = [3, 2, 1], [21, 15, 8]
+    box = rng.integers(0, 1000, shp).astype(np.int32)
+    region_ref.write_ndarray(shape, cs, meta.chunk_memory_layout, off, box, chunks, 0)
+    write_ndarray(h, "a", meta, off, box)
+    for c, want in chunks.items():
+        got = h.read_chunk("a", meta, list(c), np.int32)
+        assert got is not None and np.array_equal(got.get_data(), want), c

@@ -118,6 +118,26 @@ def assemble_region(meta: ArrayMetadata, bbox: BoundingBox, es: int, table, out,
     _raise_status(st, ctx, "read_region")
 
 
+def scatter_region(meta: ArrayMetadata, bbox: BoundingBox, es: int, table, box, box_strides, device: int = 0,
+                   stream=None) -> None:
+    """Device-level inverse of assemble_region (zcg_write_region): the box
+    (`box` = device tensor whose data_ptr() is element (0, ..., 0) of a view
+    with `box_strides`) is written into the chunk slots of `table`."""
+    import torch
+    ctx = _native.context(device)
+    r = _region(meta, bbox, es, False, 0, box_strides)
+    s = stream if stream is not None else torch.cuda.current_stream(device)
+    h = s.cuda_stream if hasattr(s, "cuda_stream") else int(s)
+    st = ctx.lib.zcg_write_region(ctx.handle, ctypes.byref(r), table.data_ptr() if table is not None else None,
+                                  box.data_ptr(), h)
+    _raise_status(st, ctx, "write_region")
+
+
+# write_ndarray works through the touched chunks in sub-batches of at most this
+# many bytes of decoded slots plus encode capacity (device memory bound)
+WRITE_BATCH_BYTES = 1 << 30
+
+
 def _decode_visited(hier, path_name: str, meta: ArrayMetadata, bbox: BoundingBox, device: int):
     """Read + batch-decode the chunks bounded_coord_iter visits; returns
     (table tensor, keep-alive objects)."""
@@ -220,9 +240,29 @@ def write_ndarray(hier, path_name: str, meta: ArrayMetadata, offset: Sequence[in
     N = meta.get_chunk_num_elements()
     D = N * es
     dev = torch.device("cuda", device)
-    slots = torch.empty(len(coords) * D, dtype=torch.uint8, device=dev)
+    codec = BatchCodec(device)
+    cap = codec.encode_bound(meta, D)
+    box = torch.from_numpy(np.ascontiguousarray(array, dtype=dt).reshape(-1).view(np.uint8).copy()).to(dev)
+    ctx = _native.context(device)
+    r = _region(meta, bbox, es, False, 0, _strides(bbox.shape, "C"))
+    h = torch.cuda.current_stream(device).cuda_stream
+    per = max(1, WRITE_BATCH_BYTES // max(D + cap, 1))
+    for b0 in range(0, len(coords), per):
+        _write_sub_batch(hier, path_name, meta, bbox, coords, b0, min(len(coords), b0 + per), dt, D, N, cap,
+                         box, ctx, r, h, codec, dev)
+
+
+def _write_sub_batch(hier, path_name, meta, bbox, coords, b0, b1, dt, D, N, cap, box, ctx, r, h, codec, dev):
+    """write_ndarray for coords[b0:b1]: read/decode the partly covered chunks,
+    scatter the box into all of them, encode, write each chunk's bytes."""
+    import torch
+    from .batch import make_encode_batch
+    cs = meta.get_chunk_shape()
+    m = b1 - b0
+    slots = torch.empty(m * D, dtype=torch.uint8, device=dev)
     partial_bufs, partial_idx, absent_idx = [], [], []
-    for i, c in enumerate(coords):
+    for i in range(m):
+        c = coords[b0 + i]
         assert meta.in_bounds(c)  # storage.rs:217
         nom = BoundingBox([ci * s for ci, s in zip(c, cs)], cs)
         wb = BoundingBox(nom.offset, nom.shape)
@@ -238,36 +278,39 @@ def write_ndarray(hier, path_name: str, meta: ArrayMetadata, offset: Sequence[in
             absent_idx.append(i)  # starts as fill value (ndarray.rs:357-368)
     if partial_bufs:
         packed = PackedStreams(partial_bufs, D, dev)
-        BatchCodec(device).decode(meta, packed)
+        codec.decode(meta, packed)
         st = packed.status.cpu().numpy()
         for k, i in enumerate(partial_idx):
             if st[k] != 0:
-                raise ZarrIOError(_native.STATUS_NAMES.get(int(st[k]), str(st[k])), f"chunk {list(coords[i])}")
+                raise ZarrIOError(_native.STATUS_NAMES.get(int(st[k]), str(st[k])), f"chunk {list(coords[b0 + i])}")
             slots[i * D:(i + 1) * D].copy_(packed.dst[k * D:(k + 1) * D])
+        del packed
     if absent_idx:
         fill = np.full(N, 0 if meta.fill_value is None else meta.fill_value, dtype=dt)
         ft = torch.from_numpy(fill.view(np.uint8)).to(dev)
         for i in absent_idx:
             slots[i * D:(i + 1) * D].copy_(ft)
-    table = torch.tensor([slots.data_ptr() + i * D for i in range(len(coords))], dtype=torch.int64, device=dev)
-    box = torch.from_numpy(np.ascontiguousarray(array, dtype=dt).reshape(-1).view(np.uint8).copy()).to(dev)
-    ctx = _native.context(device)
-    r = _region(meta, bbox, es, False, 0, _strides(bbox.shape, "C"))
-    h = torch.cuda.current_stream(device).cuda_stream
+    # the region call covers the whole grid range: chunks outside this
+    # sub-batch get NULL slots and are skipped
+    table_h = np.zeros(len(coords), np.int64)
+    table_h[b0:b1] = slots.data_ptr() + np.arange(m, dtype=np.int64) * D
+    table = torch.from_numpy(table_h).to(dev)
     _raise_status(ctx.lib.zcg_write_region(ctx.handle, ctypes.byref(r), table.data_ptr(), box.data_ptr(), h),
                   ctx, "write_region")
-    codec = BatchCodec(device)
-    cap = codec.encode_bound(meta, D)
-    desc, dst, out_len, status = make_encode_batch(slots, len(coords), cap, dev)
-    codec.encode(meta, desc, len(coords), out_len, status)
-    torch.cuda.synchronize(device)
+    desc, dst, out_len, status = make_encode_batch(slots, m, cap, dev)
+    codec.encode(meta, desc, m, out_len, status)
+    torch.cuda.synchronize(dev)
     st = status.cpu().numpy()
-    ol = out_len.cpu().numpy()
-    host = dst.cpu().numpy()
-    for i, c in enumerate(coords):
-        if st[i] != 0:
-            raise ZarrIOError(_native.STATUS_NAMES.get(int(st[i]), str(st[i])), f"chunk {list(c)}")
-        p = hier.chunk_path(path_name, meta, c)
+    ol = out_len.cpu().numpy().astype(np.int64)
+    bad = np.nonzero(st != 0)[0]
+    if len(bad):
+        i = int(bad[0])
+        raise ZarrIOError(_native.STATUS_NAMES.get(int(st[i]), str(st[i])), f"chunk {list(coords[b0 + i])}")
+    # only each chunk's encoded bytes cross to the host, compacted on the device
+    packed_out = torch.cat([dst[i * cap:i * cap + int(ol[i])] for i in range(m)]).cpu().numpy()
+    starts = np.concatenate([[0], np.cumsum(ol)])
+    for i in range(m):
+        p = hier.chunk_path(path_name, meta, coords[b0 + i])
         os.makedirs(os.path.dirname(p), exist_ok=True)
         with open(p, "wb") as f:
-            f.write(host[i * cap:i * cap + int(ol[i])].tobytes())
+            f.write(packed_out[starts[i]:starts[i + 1]].tobytes())
