@@ -62,6 +62,8 @@ enum zcg_status {
     ZCG_ERR_INVALID_INPUT = 3,  /* dtype mismatch (chunk.rs:261-264), bad args */
     ZCG_ERR_UNSUPPORTED = 4,    /* e.g. LZ4 dictionary frames                  */
     ZCG_ERR_OUTPUT_TOO_SMALL = 5, /* encode: dst capacity below the stream size */
+    ZCG_ABSENT = 6,             /* store: no chunk file (get() -> Ok(None), read_chunk -> None) */
+    ZCG_ERR_IO = 7,             /* store: a filesystem error (open/lock/read/write)  */
     ZCG_ERR_RUNTIME = 100       /* HIP runtime failure (see zcg_last_error)     */
 };
 
@@ -212,6 +214,72 @@ int zcg_read_region(zcg_ctx* ctx, const zcg_region* r, const void* const* d_chun
  * ignored.  Asynchronous on `stream`. */
 int zcg_write_region(zcg_ctx* ctx, const zcg_region* r, void* const* d_chunk_table,
                      const void* d_in, void* stream);
+
+/* ---- FilesystemHierarchy chunk files ---------------
+ * The e2e path's two ends: chunk files read into pinned staging by a pool of
+ * `io_threads` host threads (open + shared flock + read, as ReadableStore::get,
+ * src/store/filesystem.rs:201-210), H2D, zcg_decode_batch, D2H into `dsts`
+ * (N*elem_size bytes each), pipelined over two streams in sub-batches of
+ * <= 256 MiB; status[i] = ZCG_ABSENT for a missing chunk (read_chunk -> None,
+ * src/storage.rs:226-234), ZCG_ERR_IO for a filesystem error, else the decode
+ * status.  The write direction encodes `elems` (N*elem_size host bytes each)
+ * on the GPU and writes each file as WriteableStore::set (filesystem.rs:260-280):
+ * create_dir_all(parent), open, exclusive flock, truncate, write.  Paths come
+ * from the caller (get_chunk_key, storage.rs:109-127).  Blocking. */
+int zcg_store_read_chunks(zcg_ctx* ctx, const zcg_array* array, uint32_t n, const char* const* paths,
+                          void* const* dsts, int32_t* status, uint32_t io_threads);
+int zcg_store_write_chunks(zcg_ctx* ctx, const zcg_array* array, uint32_t n, const char* const* paths,
+                           const void* const* elems, int32_t* status, uint32_t io_threads);
+
+/* ---- several GPUs in one process -------------------------
+ * Chunk i goes to devices[i mod n_devices]; one host thread and one context
+ * per device, no collective (chunks are independent, chunk.rs:282,297); the
+ * per-chunk status arrays are merged.  Same arguments as the single-context
+ * calls; returns the first failing device's return code. */
+typedef struct zcg_multi zcg_multi;
+zcg_multi* zcg_multi_create(const int* devices, uint32_t n_devices);
+void zcg_multi_destroy(zcg_multi* multi);
+const char* zcg_multi_last_error(const zcg_multi* multi);
+uint32_t zcg_multi_device_count(const zcg_multi* multi);
+int zcg_multi_read_chunks_host(zcg_multi* multi, const zcg_array* array, uint32_t n, const void* const* srcs,
+                               const uint64_t* src_lens, void* const* dsts, int32_t* status);
+int zcg_multi_store_read_chunks(zcg_multi* multi, const zcg_array* array, uint32_t n,
+                                const char* const* paths, void* const* dsts, int32_t* status,
+                                uint32_t io_threads);
+int zcg_multi_store_write_chunks(zcg_multi* multi, const zcg_array* array, uint32_t n,
+                                 const char* const* paths, const void* const* elems, int32_t* status,
+                                 uint32_t io_threads);
+
+/* ---- array metadata JSON -------------------------
+ * The Zarr v3.0-dev array document (ArrayMetadata's serde form, lib.rs:382-402;
+ * DataType strings data_type.rs:165-240; ExtensibleDataType fallback
+ * data_type.rs:282-310; CompressionType {"codec", "configuration"} with the
+ * codecs' serde defaults, compression/mod.rs:36-51) parsed into the batch
+ * API's descriptor, so a C or Rust caller can drive zcg_decode_batch from a
+ * real hierarchy.  Returns ZCG_OK; ZCG_ERR_INVALID_DATA for a malformed
+ * document (serde's io::ErrorKind::InvalidData); ZCG_ERR_UNSUPPORTED where the
+ * reference panics (unknown endian/size character, an extended type without
+ * fallback) or rejects the document (a must_understand extension,
+ * storage.rs:172-176).  `err` (optional) receives a message. */
+enum zcg_dtype_kind { ZCG_DT_BOOL = 0, ZCG_DT_INT = 1, ZCG_DT_UINT = 2, ZCG_DT_FLOAT = 3, ZCG_DT_RAW = 4 };
+typedef struct zcg_array_meta {
+    zcg_array array;            /* codec + configuration, effective dtype,
+                                   chunk_num_elements = product(chunk_shape) (lib.rs:474-480) */
+    uint32_t ndim;              /* len(shape) */
+    uint32_t chunk_ndim;        /* len(chunk_shape) */
+    uint32_t chunk_order;       /* chunk_memory_layout: 0 = "C" (RowMajor), 1 = "F" (ColumnMajor) */
+    uint32_t dtype_kind;        /* enum zcg_dtype_kind of the effective type */
+    uint32_t extended_type;     /* 1: data_type was an extension object (its fallback is used) */
+    uint32_t has_fill_value;    /* fill_value present, not null, and convertible to the type */
+    int32_t fill_value_status;  /* ZCG_OK, or why fill_value does not convert (get_effective_fill_value) */
+    uint32_t reserved;
+    uint64_t fill_value;        /* element bytes of the effective fill value, host order (0 = T::default()) */
+    uint64_t shape[ZCG_MAX_DIMS];
+    uint64_t chunk_shape[ZCG_MAX_DIMS];
+    char separator[8];          /* chunk_grid.separator (get_chunk_key, storage.rs:109-127) */
+} zcg_array_meta;
+
+int zcg_array_meta_from_json(const char* json, uint64_t len, zcg_array_meta* out, char* err, uint64_t err_cap);
 
 #ifdef __cplusplus
 }

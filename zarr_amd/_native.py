@@ -13,6 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libzchunk_gpu.so")
 
 OK, UNEXPECTED_EOF, INVALID_DATA, INVALID_INPUT, UNSUPPORTED, OUTPUT_TOO_SMALL = 0, 1, 2, 3, 4, 5
+ABSENT, IO = 6, 7  # store: no chunk file (read_chunk -> None); filesystem error
 RUNTIME = 100
 
 FLAG_VERIFY_GZIP_CRC = 0x1
@@ -22,7 +23,7 @@ FLAG_SERIAL_INFLATE = 0x100
 
 STATUS_NAMES = {OK: "Ok", UNEXPECTED_EOF: "UnexpectedEof", INVALID_DATA: "InvalidData",
                 INVALID_INPUT: "InvalidInput", UNSUPPORTED: "Unsupported",
-                OUTPUT_TOO_SMALL: "OutputTooSmall", RUNTIME: "Runtime"}
+                OUTPUT_TOO_SMALL: "OutputTooSmall", ABSENT: "NotFound", IO: "Other", RUNTIME: "Runtime"}
 
 EXPORTED_SYMBOLS = (
     "zcg_abi_version", "zcg_create", "zcg_destroy", "zcg_last_error",
@@ -30,6 +31,10 @@ EXPORTED_SYMBOLS = (
     "zcg_decode_batch", "zcg_encode_batch", "zcg_encode_bound", "zcg_workspace_bytes",
     "zcg_read_chunk", "zcg_write_chunk", "zcg_read_chunks_host",
     "zcg_region_grid", "zcg_read_region", "zcg_write_region",
+    "zcg_store_read_chunks", "zcg_store_write_chunks",
+    "zcg_multi_create", "zcg_multi_destroy", "zcg_multi_last_error", "zcg_multi_device_count",
+    "zcg_multi_read_chunks_host", "zcg_multi_store_read_chunks", "zcg_multi_store_write_chunks",
+    "zcg_array_meta_from_json",
 )
 
 
@@ -67,6 +72,15 @@ class Region(ctypes.Structure):
                 ("array_shape", ctypes.c_uint64 * MAX_DIMS), ("chunk_shape", ctypes.c_uint64 * MAX_DIMS),
                 ("bbox_offset", ctypes.c_uint64 * MAX_DIMS), ("bbox_shape", ctypes.c_uint64 * MAX_DIMS),
                 ("out_strides", ctypes.c_int64 * MAX_DIMS), ("fill_value", ctypes.c_uint64)]
+
+
+class ArrayMeta(ctypes.Structure):
+    _fields_ = [("array", Array), ("ndim", ctypes.c_uint32), ("chunk_ndim", ctypes.c_uint32),
+                ("chunk_order", ctypes.c_uint32), ("dtype_kind", ctypes.c_uint32),
+                ("extended_type", ctypes.c_uint32), ("has_fill_value", ctypes.c_uint32),
+                ("fill_value_status", ctypes.c_int32), ("reserved", ctypes.c_uint32),
+                ("fill_value", ctypes.c_uint64), ("shape", ctypes.c_uint64 * MAX_DIMS),
+                ("chunk_shape", ctypes.c_uint64 * MAX_DIMS), ("separator", ctypes.c_char * 8)]
 
 
 assert ctypes.sizeof(Region) == 16 + 5 * 8 * MAX_DIMS + 8
@@ -127,6 +141,25 @@ def load_library(path: str = LIB_PATH):
         L.zcg_write_region.argtypes = [ctypes.c_void_p, ctypes.POINTER(Region), ctypes.c_void_p,
                                        ctypes.c_void_p, ctypes.c_void_p]
         L.zcg_write_region.restype = ctypes.c_int
+        L.zcg_store_read_chunks.argtypes = [vp, ctypes.POINTER(Array), u32, vp, vp, vp, u32]
+        L.zcg_store_read_chunks.restype = ctypes.c_int
+        L.zcg_store_write_chunks.argtypes = [vp, ctypes.POINTER(Array), u32, vp, vp, vp, u32]
+        L.zcg_store_write_chunks.restype = ctypes.c_int
+        L.zcg_multi_create.argtypes = [vp, u32]
+        L.zcg_multi_create.restype = vp
+        L.zcg_multi_destroy.argtypes = [vp]
+        L.zcg_multi_last_error.argtypes = [vp]
+        L.zcg_multi_last_error.restype = ctypes.c_char_p
+        L.zcg_multi_device_count.argtypes = [vp]
+        L.zcg_multi_device_count.restype = u32
+        L.zcg_multi_read_chunks_host.argtypes = [vp, ctypes.POINTER(Array), u32, vp, vp, vp, vp]
+        L.zcg_multi_read_chunks_host.restype = ctypes.c_int
+        L.zcg_multi_store_read_chunks.argtypes = [vp, ctypes.POINTER(Array), u32, vp, vp, vp, u32]
+        L.zcg_multi_store_read_chunks.restype = ctypes.c_int
+        L.zcg_multi_store_write_chunks.argtypes = [vp, ctypes.POINTER(Array), u32, vp, vp, vp, u32]
+        L.zcg_multi_store_write_chunks.restype = ctypes.c_int
+        L.zcg_array_meta_from_json.argtypes = [ctypes.c_char_p, u64, ctypes.POINTER(ArrayMeta), vp, u64]
+        L.zcg_array_meta_from_json.restype = ctypes.c_int
         _lib = L
         return L
 
@@ -167,3 +200,13 @@ def context(device: int = 0) -> Context:
         with _lock:
             _contexts[device] = ctx
     return ctx
+
+
+def array_meta_from_json(text) -> "tuple[int, ArrayMeta, str]":
+    """zcg_array_meta_from_json (host code, no GPU): (status, ArrayMeta, message)."""
+    L = load_library()
+    b = text.encode() if isinstance(text, str) else bytes(text)
+    m = ArrayMeta()
+    err = ctypes.create_string_buffer(256)
+    st = L.zcg_array_meta_from_json(b, len(b), ctypes.byref(m), ctypes.addressof(err), 256)
+    return st, m, err.value.decode(errors="replace")

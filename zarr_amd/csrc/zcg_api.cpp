@@ -16,6 +16,8 @@
 
 using namespace zcg;
 
+struct zcg_store_slots;
+
 struct zcg_ctx {
     int device = 0;
     hipStream_t stream = nullptr;  // internal stream of the host conveniences
@@ -33,7 +35,23 @@ struct zcg_ctx {
     size_t d_buf_bytes = 0;
     void* h_pin = nullptr;
     size_t h_pin_bytes = 0;
+    // store pipeline slots (zcg_store.cpp), created on first use
+    zcg_store_slots* store = nullptr;
 };
+
+namespace zcg {
+int ctx_device(zcg_ctx* ctx) { return ctx->device; }
+void ctx_set_error(zcg_ctx* ctx, const std::string& e) { ctx->err = e; }
+zcg_store_slots* store_slots_new(int device);
+void store_slots_free(zcg_store_slots* p);
+zcg_store_slots* ctx_store_slots(zcg_ctx* ctx) {
+    if (!ctx->store) {
+        ctx->store = store_slots_new(ctx->device);
+        if (!ctx->store) ctx->err = "store: stream/event creation failed";
+    }
+    return ctx->store;
+}
+}  // namespace zcg
 
 namespace {
 
@@ -113,6 +131,7 @@ void zcg_destroy(zcg_ctx* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->store) store_slots_free(ctx->store);
     for (auto& w : ctx->ws)
         if (w.p) (void)hipFree(w.p);
     if (ctx->d_buf) (void)hipFree(ctx->d_buf);

@@ -7,16 +7,23 @@ array metadata keys ``/meta/root/<path>.array.json`` (lib.rs:194-201),
 chunk keys ``/data/root/<path>/c<i>/<j>/…`` (``get_chunk_key``,
 storage.rs:109-127), ``read_chunk`` with a missing chunk -> ``None``
 (storage.rs:206-235), ``read_chunk_into`` (237-267), ``write_chunk``
-(456-470) and ``delete_chunk``.  Groups/attributes/listing and the flock
-concurrency protocol are out of scope.
+(456-470) and ``delete_chunk``.  Chunk files go through the native store
+path (zcg_store.cpp): shared flock on read, exclusive flock + truncate on
+write (filesystem.rs:201-210,260-280), read into pinned staging on a host
+thread pool and pipelined with the GPU.  Groups/attributes/listing are out
+of scope.
 """
 from __future__ import annotations
 
+import ctypes
 import json
 import os
 from typing import List, Optional, Sequence
 
-from .chunk import DefaultChunk, SliceDataChunk, ZarrIOError, read_chunks_host
+import numpy as np
+
+from . import _native
+from .chunk import DefaultChunk, SliceDataChunk, ZarrIOError, abi_array, check_array_type
 from .metadata import ArrayMetadata
 
 ENTRY_POINT_KEY = "zarr.json"
@@ -95,54 +102,63 @@ class FilesystemHierarchy:
     # ---- chunks (the path) ---------------------------------------------------------
     def read_chunk(self, path_name: str, array_meta: ArrayMetadata, grid_position, t,
                    device: int = 0) -> Optional[SliceDataChunk]:
-        assert array_meta.in_bounds(grid_position)  # storage.rs:217 (a panic there)
-        p = self.chunk_path(path_name, array_meta, grid_position)
-        if not os.path.isfile(p):
-            return None
-        with open(p, "rb") as f:
-            buf = f.read()
-        return DefaultChunk.read_chunk(buf, array_meta, grid_position, t, device=device)
+        """storage.rs:206-235: get() under a shared flock; None if absent."""
+        return self.read_chunks(path_name, array_meta, [grid_position], t, device=device, io_threads=1)[0]
 
     def read_chunk_into(self, path_name: str, array_meta: ArrayMetadata, grid_position,
                         chunk: SliceDataChunk, t, device: int = 0) -> Optional[bool]:
-        assert array_meta.in_bounds(grid_position)
-        p = self.chunk_path(path_name, array_meta, grid_position)
-        if not os.path.isfile(p):
+        """storage.rs:237-267: None if absent, else the chunk reinitialised
+        (ReinitDataChunk::reinitialize, chunk.rs:91-94) with the decoded data."""
+        got = self.read_chunk(path_name, array_meta, grid_position, t, device=device)
+        if got is None:
             return None
-        with open(p, "rb") as f:
-            buf = f.read()
-        DefaultChunk.read_chunk_into(buf, array_meta, grid_position, chunk, t, device=device)
+        chunk.grid_position = list(grid_position)
+        chunk.data = got.get_data()
         return True
 
     def read_chunks(self, path_name: str, array_meta: ArrayMetadata, grid_positions, t,
-                    device: int = 0) -> List[Optional[SliceDataChunk]]:
-        """Batched read_chunk: all present chunks are decoded in one launch."""
-        bufs, idx = [], []
-        out: List[Optional[SliceDataChunk]] = [None] * len(grid_positions)
-        for i, g in enumerate(grid_positions):
-            assert array_meta.in_bounds(g)
-            p = self.chunk_path(path_name, array_meta, g)
-            if os.path.isfile(p):
-                with open(p, "rb") as f:
-                    bufs.append(f.read())
-                idx.append(i)
-        if bufs:
-            status, arrs = read_chunks_host(array_meta, bufs, t, device=device)
-            for k, i in enumerate(idx):
-                if status[k] != 0:
-                    from ._native import STATUS_NAMES
-                    raise ZarrIOError(STATUS_NAMES.get(int(status[k]), str(status[k])),
-                                      f"chunk {list(grid_positions[i])}")
-                out[i] = SliceDataChunk(list(grid_positions[i]), arrs[k])
+                    device: int = 0, io_threads: int = 8) -> List[Optional[SliceDataChunk]]:
+        """Batched read_chunk through the native store path
+        (zcg_store_read_chunks): files read under a shared flock into pinned
+        staging by `io_threads` host threads, pipelined with H2D, the batch
+        decode and D2H on two streams.  A missing chunk is None."""
+        for g in grid_positions:
+            assert array_meta.in_bounds(g)  # storage.rs:217 (a panic there)
+        paths = [self.chunk_path(path_name, array_meta, g) for g in grid_positions]
+        arrs, status = store_read(array_meta, paths, t, device=device, io_threads=io_threads)
+        out: List[Optional[SliceDataChunk]] = []
+        for g, a, st in zip(grid_positions, arrs, status):
+            if st == _native.ABSENT:
+                out.append(None)
+                continue
+            if st != _native.OK:
+                raise ZarrIOError(_native.STATUS_NAMES.get(int(st), str(st)), f"chunk {list(g)}")
+            out.append(SliceDataChunk(list(g), a))
         return out
+
+    def write_chunks(self, path_name: str, array_meta: ArrayMetadata, chunks: Sequence[SliceDataChunk],
+                     device: int = 0, io_threads: int = 8) -> None:
+        """Batched write_chunk (zcg_store_write_chunks): GPU encode, then each
+        file written under an exclusive flock, truncated after locking
+        (filesystem.rs:260-280)."""
+        paths = [self.chunk_path(path_name, array_meta, c.get_grid_position()) for c in chunks]
+        status = store_write(array_meta, paths, [c.get_data() for c in chunks], device=device,
+                             io_threads=io_threads)
+        for c, st in zip(chunks, status):
+            if st != _native.OK:
+                raise ZarrIOError(_native.STATUS_NAMES.get(int(st), str(st)), f"chunk {c.get_grid_position()}")
 
     def write_chunk(self, path_name: str, array_meta: ArrayMetadata, chunk: SliceDataChunk,
                     device: int = 0) -> None:
-        data = DefaultChunk.write_chunk(array_meta, chunk, device=device)
-        p = self.chunk_path(path_name, array_meta, chunk.get_grid_position())
-        os.makedirs(os.path.dirname(p), exist_ok=True)
-        with open(p, "wb") as f:  # set(): truncate + write (filesystem.rs:260-280)
-            f.write(data)
+        """storage.rs:456-470 + DefaultChunk::write_chunk (chunk.rs:306-323),
+        stored by set() under an exclusive flock (filesystem.rs:260-280)."""
+        data = np.asarray(chunk.get_data())
+        check_array_type(data.dtype, array_meta)
+        if data.size != array_meta.get_chunk_num_elements():  # chunk.rs:309-318
+            raise ZarrIOError("InvalidData",
+                              f"Can not write chunk with too few elements. Expected "
+                              f"{array_meta.get_chunk_num_elements()} given {data.size}")
+        self.write_chunks(path_name, array_meta, [chunk], device=device, io_threads=1)
 
     def delete_chunk(self, path_name: str, array_meta: ArrayMetadata, grid_position) -> bool:
         p = self.chunk_path(path_name, array_meta, grid_position)
@@ -152,3 +168,53 @@ class FilesystemHierarchy:
 
     def exists_chunk(self, path_name: str, array_meta: ArrayMetadata, grid_position) -> bool:
         return os.path.isfile(self.chunk_path(path_name, array_meta, grid_position))
+
+
+def _cstrs(paths):
+    enc = [os.fsencode(p) for p in paths]
+    arr = (ctypes.c_char_p * max(len(enc), 1))(*enc)
+    return arr, enc
+
+
+def store_read(array_meta: ArrayMetadata, paths: Sequence[str], t, device: int = 0, io_threads: int = 8):
+    """zcg_store_read_chunks: (list of element arrays, status array)."""
+    check_array_type(t, array_meta)
+    ctx = _native.context(device)
+    n = len(paths)
+    dt = np.dtype(t).newbyteorder("=")
+    N = array_meta.get_chunk_num_elements()
+    arrs = [np.empty(N, dt) for _ in range(n)]
+    dp = (ctypes.c_void_p * max(n, 1))(*[a.ctypes.data for a in arrs])
+    cp, keep = _cstrs(paths)
+    st = np.zeros(max(n, 1), np.int32)
+    arr = abi_array(array_meta)
+    r = ctx.lib.zcg_store_read_chunks(ctx.handle, ctypes.byref(arr), n, ctypes.addressof(cp),
+                                      ctypes.addressof(dp), st.ctypes.data, io_threads)
+    if r != _native.OK:
+        raise ZarrIOError(_native.STATUS_NAMES.get(r, str(r)), f"store_read_chunks: {ctx.last_error()}")
+    return arrs, st[:n]
+
+
+def store_write(array_meta: ArrayMetadata, paths: Sequence[str], datas, device: int = 0, io_threads: int = 8):
+    """zcg_store_write_chunks: status array.  Each element array must hold
+    exactly get_chunk_num_elements() elements (chunk.rs:309-318)."""
+    ctx = _native.context(device)
+    n = len(paths)
+    N = array_meta.get_chunk_num_elements()
+    t = array_meta.effective_type()
+    datas = [np.ascontiguousarray(d) for d in datas]
+    for d in datas:
+        check_array_type(d.dtype, array_meta)
+        if d.size != N:
+            raise ZarrIOError("InvalidData", "Wrong number of elements")
+    if t.kind == "bool":
+        datas = [d.astype(np.uint8) for d in datas]
+    ep = (ctypes.c_void_p * max(n, 1))(*[d.ctypes.data for d in datas])
+    cp, keep = _cstrs(paths)
+    st = np.zeros(max(n, 1), np.int32)
+    arr = abi_array(array_meta)
+    r = ctx.lib.zcg_store_write_chunks(ctx.handle, ctypes.byref(arr), n, ctypes.addressof(cp),
+                                       ctypes.addressof(ep), st.ctypes.data, io_threads)
+    if r != _native.OK:
+        raise ZarrIOError(_native.STATUS_NAMES.get(r, str(r)), f"store_write_chunks: {ctx.last_error()}")
+    return st[:n]
