@@ -139,7 +139,10 @@ int zcg_decode_batch(zcg_ctx* ctx, const zcg_array* array, const zcg_chunk* d_ch
                      uint32_t n, int32_t* d_status, void* stream);
 
 /* Replaces N calls of DefaultChunk::write_chunk (chunk.rs:306-323).
- * d_out_len[i] receives the encoded stream length of chunk i. */
+ * d_out_len[i] receives the encoded stream length of chunk i.  LZ4 encode
+ * accepts at most 4096 LZ4 blocks per chunk (256 MiB at the 64 KiB default
+ * block size); beyond that it returns ZCG_ERR_UNSUPPORTED (zcg_last_error
+ * says why) and launches nothing. */
 int zcg_encode_batch(zcg_ctx* ctx, const zcg_array* array, const zcg_chunk* d_chunks,
                      uint32_t n, uint64_t* d_out_len, int32_t* d_status, void* stream);
 

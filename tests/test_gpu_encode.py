@@ -567,3 +567,22 @@ def test_encode_sub_batch_splits_roundtrip(codec):
     assert (st == 0).all()
     bad = [i for i in range(n) if not np.array_equal(outs[i], base[offs[i]:offs[i] + D])]
     assert not bad, bad[:10]
+
+
+def test_lz4_encode_block_count_limit():
+    """More than 4096 LZ4 blocks per chunk is refused up front with
+    ZCG_ERR_UNSUPPORTED and a message; nothing is launched (the chunk table
+    below points at 1-byte buffers and is never read)."""
+    import ctypes
+    import torch
+    from zarr_amd import _native
+    from zarr_amd.chunk import abi_array
+    ctx = _native.context(0)
+    meta = ArrayMetadata.new([(4097 << 16)], [(4097 << 16)], "u1", Lz4(65536))
+    dummy = torch.zeros(64, dtype=torch.uint8, device="cuda:0")
+    st = torch.zeros(1, dtype=torch.int32, device="cuda:0")
+    ol = torch.zeros(1, dtype=torch.int64, device="cuda:0")
+    arr = abi_array(meta)
+    r = ctx.lib.zcg_encode_batch(ctx.handle, ctypes.byref(arr), ctypes.c_void_p(dummy.data_ptr()), 1,
+                                 ctypes.c_void_p(ol.data_ptr()), ctypes.c_void_p(st.data_ptr()), None)
+    assert r == _native.UNSUPPORTED and "4096" in ctx.last_error()

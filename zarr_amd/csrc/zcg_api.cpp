@@ -182,7 +182,9 @@ uint64_t zcg_workspace_bytes(const zcg_array* a, uint32_t n, int encode) {
     if (a->compression.codec == ZCG_CODEC_BZIP2)
         return encode ? bzip2_encode_ws_bytes(a, n) : bzip2_decode_ws_bytes(a, n);
     if (a->compression.codec == ZCG_CODEC_XZ && encode) return xz_encode_ws_bytes(a, n);
-    if (a->compression.codec == ZCG_CODEC_GZIP && encode) return deflate_ws_bytes(a, n);
+    if (a->compression.codec == ZCG_CODEC_GZIP)
+        return encode ? deflate_ws_bytes(a, n)
+                      : ((a->compression.flags & ZCG_FLAG_SERIAL_INFLATE) ? 0 : inflate_par_ws_bytes(a, n));
     if (a->compression.codec == ZCG_CODEC_LZ4) return encode ? lz4_encode_ws_bytes(a, n) : lz4_decode_ws_bytes(a, n);
     return 0;
 }
@@ -204,11 +206,17 @@ int zcg_decode_batch(zcg_ctx* ctx, const zcg_array* a, const zcg_chunk* d_chunks
         e = launch_lz4_decode(a, d_chunks, n, d_status, w->p, w->bytes, s);
         break;
     }
-    case ZCG_CODEC_GZIP:
-        e = (a->compression.flags & ZCG_FLAG_SERIAL_INFLATE)
-                ? launch_inflate(a, d_chunks, n, d_status, s)
-                : launch_inflate_par(a, d_chunks, n, d_status, s);
+    case ZCG_CODEC_GZIP: {
+        if (a->compression.flags & ZCG_FLAG_SERIAL_INFLATE) {
+            e = launch_inflate(a, d_chunks, n, d_status, s);
+            break;
+        }
+        zcg_ctx::Ws* w = nullptr;
+        const int r = stream_ws(ctx, stream, inflate_par_ws_bytes(a, n), &w);
+        if (r != ZCG_OK) return r;
+        e = launch_inflate_par(a, d_chunks, n, d_status, w->p, w->bytes, s);
         break;
+    }
     case ZCG_CODEC_XZ: e = launch_xz_decode(a, d_chunks, n, d_status, nullptr, 0, s); break;
     case ZCG_CODEC_BZIP2: {
         zcg_ctx::Ws* w = nullptr;
@@ -234,6 +242,15 @@ int zcg_encode_batch(zcg_ctx* ctx, const zcg_array* a, const zcg_chunk* d_chunks
     switch (a->compression.codec) {
     case ZCG_CODEC_RAW: e = launch_raw(a, d_chunks, n, d_status, d_out_len, 1, s); break;
     case ZCG_CODEC_LZ4: {
+        // The match-finder sort key holds (chunk, block) in 12 bits: at most
+        // 4096 LZ4 blocks per chunk (256 MiB chunks at the 64 KiB default).
+        const uint64_t B = (uint64_t)zcg_effective_lz4_block_size(a->compression.lz4_block_size);
+        const uint64_t D = a->chunk_num_elements * (uint64_t)a->dtype.elem_size;
+        if ((D + B - 1) / B > 4096) {
+            ctx->err = "LZ4 encode supports at most 4096 blocks per chunk (" + std::to_string((D + B - 1) / B) +
+                       " requested); use a larger block size or smaller chunks";
+            return ZCG_ERR_UNSUPPORTED;
+        }
         zcg_ctx::Ws* w = nullptr;
         const int r = stream_ws(ctx, stream, lz4_encode_ws_bytes(a, n), &w);
         if (r != ZCG_OK) return r;

@@ -38,12 +38,9 @@ namespace zcg {
 
 constexpr u32 PI_NL = 256;       // lanes per chunk (4 waves)
 constexpr u32 PI_SEG = 256;      // bits per lane segment
-constexpr u32 PI_BLK = 16;       // tokens per pool block
-constexpr u32 PI_LBLK = 5;       // pool blocks per lane -> up to 80 tokens per lane
-constexpr u32 PI_TMAX = PI_BLK * PI_LBLK;
-constexpr u32 PI_NBLK = 864;     // pool blocks per round: 2 per lane static + 352 on demand
+constexpr u32 PI_TMAX = 96;      // tokens per lane per round (the lane stops with N_CAP)
 constexpr u32 PI_STAGE = 16384;  // output bytes per round (power of 2)
-constexpr u32 PI_WIN = 32768;    // LZ77 window ring
+constexpr u32 PI_WIN = 32768;    // LZ77 window (read back from the chunk's committed output)
 constexpr u32 PI_SEGW = PI_SEG / 32;
 constexpr u32 PI_IN_VEC = (PI_NL * PI_SEG + 1024) / 128 + 2;  // staged 16-B vectors
 constexpr u32 PI_IN_WORDS = PI_IN_VEC * 4;
@@ -89,12 +86,21 @@ __device__ __forceinline__ u32 tok_dist(u32 t) { return (t & 0x7FFF) + 1; }
 // stream bits of a literal/match token (bits 24..29; <= 48)
 __device__ __forceinline__ u32 tok_bits(u32 t) { return (t >> 24) & 63; }
 
+// Round-stage entries (u16): E_VAL|byte is a final byte value; a value below
+// PI_STAGE points at an earlier byte of the same round (offset from the round
+// start); E_FAR + k - 1 stands for the byte k (1..32768) positions before the
+// round start, read back from the chunk's committed output.
+constexpr u32 E_VAL = 0xFF00u;
+constexpr u32 E_FAR = 0x4000u;
+static_assert(PI_STAGE <= E_FAR && E_FAR + PI_WIN <= E_VAL, "stage entry encoding");
+__device__ __forceinline__ bool e_val(u32 v) { return v >= E_VAL; }
+
+// 69 KiB: two chunks' workgroups per CU (8 waves).  The token lists live in a
+// per-workgroup slot of the HBM workspace (coalesced [token][lane] layout,
+// L2-resident while the chunk decodes), not in LDS.
 struct ParLds {
-    u8 win[PI_WIN];                  // LZ77 window ring (absolute pos & 32767)
-    u16 ptr[PI_STAGE];               // round bytes: 0x8000|value, or an earlier round offset
-    u32 in[PI_IN_PAD];               // staged stream words (padded: in[padw(w)])
-    u32 pool[PI_NBLK * PI_BLK];      // token pool: lanes take 16-token blocks
-    u16 blk[PI_NL * PI_LBLK];        // each lane's pool blocks
+    u16 ptr[PI_STAGE];               // round bytes (E_VAL / pointer / E_FAR entries); header scratch
+    u32 in[PI_IN_PAD];               // staged stream words (padded: in[padw(w)]); header scratch
     u32 mark[PI_NL * (PI_SEGW + 1)]; // token-start bitmap of each lane's segment (+1 pad)
     u32 head[PI_STAGE / 32];         // token-start bitmap over the round's output bytes
     u32 ltab[INF_LTAB];
@@ -107,10 +113,8 @@ struct ParLds {
     u32 give[PI_NL];                 // index of the sync token in the target's list
     u32 sidx[PI_NL];                 // first valid token of the lane
     u32 ntok[PI_NL];
-    u32 base[PI_NL];                 // output offset of the lane's first valid token
     unsigned long long anom[PI_NL / 64];
     u32 seg_s[PI_MAXSEG], seg_e[PI_MAXSEG];  // chain segments [s, e] (lane ranges)
-    u32 pool_top;
     u32 wsum[8];
     u32 ctl[16];
     u32 dbgc[32];                    // debug counters of this chunk (flushed at the end)
@@ -118,7 +122,15 @@ struct ParLds {
 // debug counter add (LDS atomic; flushed to g_inf_dbg once per chunk)
 #define DBG_ADD(slot, v) atomicAdd(&L.dbgc[slot], (u32)(v))
 
-static_assert(sizeof(ParLds) <= 160 * 1024, "ParLds exceeds the 160 KiB LDS of a CU");
+static_assert(sizeof(ParLds) <= 80 * 1024, "ParLds must leave room for two workgroups per CU");
+
+// Per-workgroup token slots in the workspace: slot s holds PI_TMAX x PI_NL
+// token words, token j of lane i at [j * PI_NL + i].  A workgroup takes a
+// free slot when it starts (owner word 0 -> 1) and frees it when it ends; the
+// launcher zeroes the owner words before each launch.
+constexpr u32 PI_NSLOT = 1024;  // > the 512 workgroups two per CU can keep resident
+constexpr u64 PI_SLOT_WORDS = (u64)PI_TMAX * PI_NL;
+constexpr u64 PI_OWNER_BYTES = PI_NSLOT * 4;
 
 // Decode one token from a bit buffer holding >= 48 valid bits: <= 2 LDS
 // lookups for the literal/length code, <= 2 for the distance code.
@@ -171,20 +183,8 @@ __device__ __forceinline__ u32 decode_token_fast(const ParLds& L, u64 v, u32* ad
     return tk;
 }
 
-// Token j of lane i in the pool.
-// Within a block the slots are rotated by the block id so that lanes reading
-// their j-th token at the same time spread over the LDS banks.
-__device__ __forceinline__ u32 pool_slot(u32 b, u32 j) { return b * PI_BLK + ((j + b) % PI_BLK); }
-// Lane i owns pool blocks 2i and 2i+1 (its first 32 tokens) outright; blocks
-// from PI_STATIC_BLK up are taken on demand (L.blk records them).
-constexpr u32 PI_STATIC_TOK = 2 * PI_BLK;
-constexpr u32 PI_STATIC_BLK = 2 * PI_NL;
-__device__ __forceinline__ u32 tok_blk(const ParLds& L, u32 i, u32 j) {
-    return j < PI_STATIC_TOK ? 2 * i + j / PI_BLK : (u32)L.blk[i * PI_LBLK + (j / PI_BLK)];
-}
-__device__ __forceinline__ u32& tok_ref(ParLds& L, u32 i, u32 j) {
-    return L.pool[pool_slot(tok_blk(L, i, j), j)];
-}
+// Token j of lane i in the workgroup's slot.
+__device__ __forceinline__ u32 tok_at(const gu32* gp, u32 i, u32 j) { return gp[j * PI_NL + i]; }
 
 // Register bit buffer over the staged words: a 96-bit window (lo:hi) holding
 // bits [q, q+nb) of the stream; lb_fill keeps nb >= 48 (one token's worst
@@ -229,9 +229,12 @@ __device__ __forceinline__ void lb_drop(LaneBits& s, u32 k) {  // 0 < k <= 48
     s.nb -= k;
 }
 
-// Flush the resolved round bytes [from, to) to dst (transform fused) and
-// append them to the window ring.  ptr[] is indexed by absolute pos & mask.
-__device__ void par_commit(ParLds& L, u8* dst, u64 from, u64 to, const DType& t) {
+// Flush the resolved round bytes [from, to) to dst (byte-order transform
+// fused; bool normalisation is deferred to the end of the chunk because the
+// committed bytes double as the LZ77 window).  ptr[] is indexed by absolute
+// pos & mask.  The trailing barrier makes the bytes visible to the next
+// round's window reads (same workgroup, same CU).
+__device__ void par_commit(ParLds& L, u8* dst, u64 from, u64 to, DType t) {
     const u32 tid = threadIdx.x;
     __syncthreads();
     const u64 a16 = (from + 15) & ~15ull, b16 = to & ~15ull;
@@ -246,22 +249,29 @@ __device__ void par_commit(ParLds& L, u8* dst, u64 from, u64 to, const DType& t)
             };
             const u32x4 v = u32x4{pk(lo.x, lo.y), pk(lo.z, lo.w), pk(hi.x, hi.y), pk(hi.z, hi.w)};
             st16(dst + p, transform16(v, t));
-            *(u32x4*)(L.win + (p & (PI_WIN - 1))) = v;
         }
     }
     const u64 e0 = a16 < b16 ? a16 : to;
-    for (u64 q = from + tid; q < e0; q += PI_NL) {
-        const u8 v = (u8)L.ptr[q & (PI_STAGE - 1)];
-        dst[swap_pos(q, t)] = norm_byte(v, t);
-        L.win[q & (PI_WIN - 1)] = v;
-    }
+    for (u64 q = from + tid; q < e0; q += PI_NL) dst[swap_pos(q, t)] = (u8)L.ptr[q & (PI_STAGE - 1)];
     if (a16 < b16)
-        for (u64 q = b16 + tid; q < to; q += PI_NL) {
-            const u8 v = (u8)L.ptr[q & (PI_STAGE - 1)];
-            dst[swap_pos(q, t)] = norm_byte(v, t);
-            L.win[q & (PI_WIN - 1)] = v;
-        }
+        for (u64 q = b16 + tid; q < to; q += PI_NL) dst[swap_pos(q, t)] = (u8)L.ptr[q & (PI_STAGE - 1)];
     __syncthreads();
+}
+
+// Bool arrays: byte != 0 over the whole decoded chunk, after the last round.
+__device__ void par_bool_norm(u8* dst, u64 D) {
+    __syncthreads();
+    const u32 tid = threadIdx.x;
+    const bool al = (((uintptr_t)dst) & 15) == 0;
+    for (u64 p = (u64)tid * 16; p < D; p += PI_NL * 16) {
+        if (p + 16 <= D) {
+            u32x4 v = al ? *(u32x4*)(dst + p) : ld16(dst + p);
+            v.x = bool_norm32(v.x); v.y = bool_norm32(v.y); v.z = bool_norm32(v.z); v.w = bool_norm32(v.w);
+            if (al) *(u32x4*)(dst + p) = v; else st16(dst + p, v);
+        } else {
+            for (u64 q = p; q < D; q++) dst[q] = dst[q] != 0;
+        }
+    }
 }
 
 // Block-wide exclusive scan over 256 lanes; *total receives the sum.
@@ -296,7 +306,7 @@ __device__ __forceinline__ u32 block_excl_scan(ParLds& L, u32 v, u32* total) {
 constexpr u32 HD_BITS = 4608;            // >= 316 symbols * 14 bits
 constexpr u32 HD_WORDS = HD_BITS / 32 + 8;
 
-__device__ int read_dynamic_par(ParLds& L, BitIn& b, bool dbg) {
+__device__ __attribute__((always_inline)) int read_dynamic_par(ParLds& L, BitIn& b, bool dbg) {
     const u32 tid = threadIdx.x;
     u64 hts = __builtin_readcyclecounter();
     if (!bi_has(b, 14)) return R_EXHAUSTED;
@@ -326,26 +336,26 @@ __device__ int read_dynamic_par(ParLds& L, BitIn& b, bool dbg) {
         bi_seek(b, c0 + 3 * ncode);
     }
     {  // code-length code must be complete ("invalid code lengths set")
-        u32 cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         const u32 lane = tid & 63;
-        for (u32 i = 0; i < 19; i++) {
-            const u32 li = __shfl(mycl, (int)i, 64);
-            if (i < ncode) cnt[li & 7]++;
-        }
         int left = 1;
-        for (int l = 1; l <= 7; l++) { left <<= 1; left -= cnt[l]; if (left < 0) break; }
+        for (u32 l = 1; l <= 7; l++) {
+            const u32 cnt = (u32)__popcll(__ballot(lane < ncode && mycl == l));
+            left <<= 1;
+            left -= (int)cnt;
+            if (left < 0) break;
+        }
         if (left != 0) return R_INVALID;
         __syncthreads();
         if (tid < 19) L.lens[tid] = 0;
         __syncthreads();
         if (tid < ncode) L.lens[c_clen_order[tid]] = (u8)mycl;
-        (void)lane;
     }
-    // stage the region [H0, H0 + HD_BITS) of the stream
+    // stage the region [H0, H0 + HD_BITS) of the stream (header scratch lives
+    // in the round arrays, which are free between rounds)
     const u64 H0 = b.consumed;
     const u64 B0 = H0 >> 3;
     const u32 o = (u32)(H0 & 7);
-    u32* hw = L.in;  // free between rounds
+    u32* hw = L.mark + 512;
     for (u32 w = tid; w < HD_WORDS; w += PI_NL) {
         const u64 q = B0 + 4ull * w;
         u32 v = 0;
@@ -356,37 +366,40 @@ __device__ int read_dynamic_par(ParLds& L, BitIn& b, bool dbg) {
         hw[w] = v;
     }
     build_table(L.lens, 19, &L.lh, L.ltab, 7, false, INF_LTAB);  // barriers inside
-    // one record per bit position: adv | codelen << 4 | sym << 8 | count << 13
-    u32* rec = L.pool;
-    for (u32 r = tid; r < HD_BITS; r += PI_NL) {
+    // one record per bit position: adv | codelen << 4 | sym << 7 (the repeat
+    // count is re-derived from the stream bits by hd_cnt)
+    u16* rec = L.ptr;
+    auto hd_v = [&](u32 r) -> u32 {
         const u32 bit = o + r, w = bit >> 5, sh = bit & 31;
-        const u64 x = (((u64)hw[w + 1] << 32) | hw[w]) >> sh;
-        const u32 v = (u32)x & 0x3FFF;
+        return (u32)((((u64)hw[w + 1] << 32) | hw[w]) >> sh) & 0x3FFF;
+    };
+    auto hd_cnt = [&](u32 r, u32 f) -> u32 {  // f = rec[r]
+        const u32 l = (f >> 4) & 7, sym = f >> 7, x = hd_v(r) >> l;
+        return sym == 16 ? 3 + (x & 3) : sym == 17 ? 3 + (x & 7) : sym == 18 ? 11 + (x & 127) : 1;
+    };
+    for (u32 r = tid; r < HD_BITS; r += PI_NL) {
+        const u32 v = hd_v(r);
         const u32 e = L.ltab[v & 127];
         const u32 l = e >> 28, sym = e & 0x1F;
-        u32 adv = l, cnt = 1;
-        if (sym == 16) { adv = l + 2; cnt = 3 + ((v >> l) & 3); }
-        else if (sym == 17) { adv = l + 3; cnt = 3 + ((v >> l) & 7); }
-        else if (sym == 18) { adv = l + 7; cnt = 11 + ((v >> l) & 127); }
-        rec[r] = adv | (l << 4) | (sym << 8) | (cnt << 13);
+        const u32 adv = sym == 16 ? l + 2 : sym == 17 ? l + 3 : sym == 18 ? l + 7 : l;
+        rec[r] = (u16)(adv | (l << 4) | (sym << 7));
     }
     __syncthreads();
-    // 2- and 4-symbol jumps: pos (13 bits) | summed count << 13
-    u32* rec2 = (u32*)L.ptr;   // free between rounds
-    u32* rec4 = L.pool + HD_BITS;
-    auto rec_at = [&](u32 r) -> u32 { return rec[r < HD_BITS ? r : HD_BITS - 1]; };
+    // 2-symbol jumps (position), then 4-symbol jumps: pos (13 bits) | summed count << 13
+    auto cl = [](u32 r) -> u32 { return r < HD_BITS ? r : HD_BITS - 1; };
+    u16* rec2 = (u16*)L.in;
+    u32* rec4 = (u32*)(L.ptr + HD_BITS);
     for (u32 r = tid; r < HD_BITS; r += PI_NL) {
-        const u32 f0 = rec[r];
-        const u32 r1 = r + (f0 & 15);
-        const u32 f1 = rec_at(r1);
-        rec2[r] = (r1 + (f1 & 15)) | (((f0 >> 13) + (f1 >> 13)) << 13);
+        const u32 r1 = r + (rec[r] & 15);
+        rec2[r] = (u16)(r1 + (rec[cl(r1)] & 15));
     }
     __syncthreads();
     for (u32 r = tid; r < HD_BITS; r += PI_NL) {
-        const u32 g0 = rec2[r];
-        const u32 r2 = g0 & 8191;
-        const u32 g1 = rec2[r2 < HD_BITS ? r2 : HD_BITS - 1];
-        rec4[r] = (g1 & 8191) | (((g0 >> 13) + (g1 >> 13)) << 13);
+        const u32 r1 = cl(r + (rec[r] & 15));
+        const u32 r2 = cl(rec2[r]);
+        const u32 r3 = cl(r2 + (rec[r2] & 15));
+        const u32 c = hd_cnt(r, rec[r]) + hd_cnt(r1, rec[r1]) + hd_cnt(r2, rec[r2]) + hd_cnt(r3, rec[r3]);
+        rec4[r] = (u32)rec2[r2] | (c << 13);
     }
     __syncthreads();
     // the walk over groups of 4 symbols: gpos[g] = start bit | out index << 13
@@ -396,7 +409,7 @@ __device__ int read_dynamic_par(ParLds& L, BitIn& b, bool dbg) {
     if (tid == 0) {
         u32 r = 0, idx = 0, g = 0;
         while (idx < total) {
-            const u32 f = rec4[r < HD_BITS ? r : HD_BITS - 1];
+            const u32 f = rec4[cl(r)];
             gpos[g++] = r | (idx << 13);
             idx += f >> 13;
             r = f & 8191;
@@ -416,8 +429,9 @@ __device__ int read_dynamic_par(ParLds& L, BitIn& b, bool dbg) {
         for (u32 g = tid; g < ng; g += PI_NL) {
             u32 r = gpos[g] & 8191, idx = gpos[g] >> 13;
             for (u32 k = 0; k < 4 && idx < total; k++) {
-                const u32 f = rec_at(r);
-                const u32 adv = f & 15, l = (f >> 4) & 7, sym = (f >> 8) & 31, cnt = f >> 13;
+                const u32 rc = cl(r);
+                const u32 f = rec[rc];
+                const u32 adv = f & 15, l = (f >> 4) & 7, sym = f >> 7, cnt = hd_cnt(rc, f);
                 const u32 i = 4 * g + k;
                 u32 err = 0;  // zlib's checks in order: code bits, repeat at 0, extra bits, overflow
                 if (r + l > lim) err = 1 + R_EXHAUSTED;
@@ -465,7 +479,7 @@ __device__ int read_dynamic_par(ParLds& L, BitIn& b, bool dbg) {
 }
 
 // read_block_header with the block-parallel dynamic header
-__device__ int read_block_header_par(ParLds& L, BitIn& b, bool* last, u32* type, u32* slen, bool dbg) {
+__device__ __attribute__((always_inline)) int read_block_header_par(ParLds& L, BitIn& b, bool* last, u32* type, u32* slen, bool dbg) {
     if (!bi_has(b, 3)) return R_EXHAUSTED;
     const u32 hdr = bi_bits(b, 3);
     *last = hdr & 1;
@@ -486,18 +500,19 @@ __device__ int read_block_header_par(ParLds& L, BitIn& b, bool* last, u32* type,
 
 // Bit position of token `j` of lane `i`: its segment start plus the bit
 // lengths stored in tokens 0..j-1 (never markers).  Called by one full wave.
-__device__ u32 token_pos(const ParLds& L, u32 R0, u32 i, u32 j) {
+__device__ u32 token_pos(const gu32* gp, u32 R0, u32 i, u32 j) {
     const u32 lane = threadIdx.x & 63;
     u32 sum = 0;
-    for (u32 k = lane; k < j; k += 64) sum += tok_bits(L.pool[pool_slot(tok_blk(L, i, k), k)]);
+    for (u32 k = lane; k < j; k += 64) sum += tok_bits(tok_at(gp, i, k));
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) sum += __shfl_xor(sum, d, 64);
     return R0 + i * PI_SEG + sum;
 }
 
-__global__ __launch_bounds__(PI_NL) void inflate_par_kernel(const zcg_chunk* __restrict__ chunks,
-                                                            u32 n, u64 D, DType t, u32 vflags,
-                                                            i32* __restrict__ status) {
+__global__ __launch_bounds__(PI_NL, 2) void inflate_par_kernel(const zcg_chunk* __restrict__ chunks,
+                                                               u32 n, u64 D, DType t, u32 vflags,
+                                                               i32* __restrict__ status,
+                                                               u32* __restrict__ owner, gu32* __restrict__ pools) {
     extern __shared__ __attribute__((aligned(16))) u8 smem_raw[];
     ParLds& L = *(ParLds*)smem_raw;
     const u32 c = blockIdx.x;
@@ -516,6 +531,17 @@ __global__ __launch_bounds__(PI_NL) void inflate_par_kernel(const zcg_chunk* __r
 
     u8* dst = (u8*)ch.dst;
     const u8* ds = s + h;  // deflate stream
+    DType tw = t;  // commit transform: bool waits for the end (the output is the window)
+    tw.isbool = 0;
+    // take a token slot (released at the end; every path below reaches it)
+    if (tid == 0) {
+        u32 sl = c % PI_NSLOT;
+        while (atomicCAS(&owner[sl], 0u, 1u) != 0u) sl = (sl + 1) % PI_NSLOT;
+        L.ctl[15] = sl;
+    }
+    __syncthreads();
+    const u32 slot = L.ctl[15];
+    gu32* const gp = pools + (u64)slot * PI_SLOT_WORDS;
     const u64 n_ds = n_in - h;
     const u32 total_bits = (u32)(n_ds * 8);
     // Every wave runs the wave-uniform header/look-ahead code redundantly on
@@ -553,8 +579,8 @@ __global__ __launch_bounds__(PI_NL) void inflate_par_kernel(const zcg_chunk* __r
                 if ((u64)k > D - P) k = (u32)(D - P);
                 if (in0 + k > n_ds) { r = R_EXHAUSTED; break; }
                 for (u32 i = tid; i < k; i += PI_NL)
-                    L.ptr[(P + i) & (PI_STAGE - 1)] = (u16)(0x8000u | ds[in0 + i]);
-                par_commit(L, dst, P, P + k, t);
+                    L.ptr[(P + i) & (PI_STAGE - 1)] = (u16)(E_VAL | ds[in0 + i]);
+                par_commit(L, dst, P, P + k, tw);
                 P += k; in0 += k; done += k;
             }
             if (r != R_OK) break;
@@ -580,10 +606,13 @@ __global__ __launch_bounds__(PI_NL) void inflate_par_kernel(const zcg_chunk* __r
                     if (vi < PI_IN_VEC) {
                         if (q + 16 <= n_ds) x = ld16(ds + q);
                         else {
-                            u32 w4[4] = {0u, 0u, 0u, 0u};
+                            u64 lo = 0, hi = 0;
                             for (u32 i = 0; i < 16; i++)
-                                if (q + i < n_ds) w4[i >> 2] |= (u32)ds[q + i] << (8 * (i & 3));
-                            x = u32x4{w4[0], w4[1], w4[2], w4[3]};
+                                if (q + i < n_ds) {
+                                    const u64 b8 = (u64)ds[q + i] << (8 * (i & 7));
+                                    if (i < 8) lo |= b8; else hi |= b8;
+                                }
+                            x = u32x4{(u32)lo, (u32)(lo >> 32), (u32)hi, (u32)(hi >> 32)};
                         }
                     }
                     v[k] = x;
@@ -598,7 +627,6 @@ __global__ __launch_bounds__(PI_NL) void inflate_par_kernel(const zcg_chunk* __r
                     }
                 }
             }
-            if (tid == 0) L.pool_top = PI_STATIC_BLK;
             for (u32 k = tid; k < PI_STAGE / 32; k += PI_NL) L.head[k] = 0;
             for (u32 k = tid; k < PI_NL * (PI_SEGW + 1); k += PI_NL) L.mark[k] = 0;
             __syncthreads();
@@ -607,27 +635,15 @@ __global__ __launch_bounds__(PI_NL) void inflate_par_kernel(const zcg_chunk* __r
             // ---- pass 1: decode my own segment, mark token starts ----------------
             const u32 p = R0 + tid * PI_SEG;
             const u32 pend = p + PI_SEG;
-            u16* myblk = L.blk + tid * PI_LBLK;
             u32* mymark = L.mark + tid * (PI_SEGW + 1);
             LaneBits bs;
             lb_init(bs, L.in, p, bit0);
             u32 q = p, nt = 0, olen_all = 0;  // olen_all: output bytes of all stored tokens
             u32 nxt = 0xFFFFFFFFu;
-            u32 curb = 2 * tid;  // current pool block of this lane
             // append a token; false when the lane's token store is full
             auto push = [&](u32 tk) -> bool {
-                if ((nt % PI_BLK) == 0) {
-                    if (nt < PI_STATIC_TOK) {
-                        curb = 2 * tid + nt / PI_BLK;
-                    } else {
-                        if (nt == PI_TMAX) return false;
-                        const u32 bi = atomicAdd(&L.pool_top, 1u);
-                        if (bi >= PI_NBLK) return false;
-                        myblk[nt / PI_BLK] = (u16)bi;
-                        curb = bi;
-                    }
-                }
-                L.pool[pool_slot(curb, nt)] = tk;
+                if (nt == PI_TMAX) return false;
+                gp[nt * PI_NL + tid] = tk;
                 nt++;
                 olen_all += tok_len(tk);
                 return true;
@@ -748,7 +764,7 @@ __global__ __launch_bounds__(PI_NL) void inflate_par_kernel(const zcg_chunk* __r
                 DBG_ADD(DBG_CHAIN, E + 1);
                 const u32 nx = L.next[E];
                 DBG_ADD(nx == N_CAP ? DBG_END_CAP : nx == N_ROUND_END ? DBG_END_ROUND
-                        : (tok_ref(L, E, L.ntok[E] - 1) == T_EOB ? DBG_END_EOB : DBG_END_BAD), 1);
+                        : (tok_at(gp, E, L.ntok[E] - 1) == T_EOB ? DBG_END_EOB : DBG_END_BAD), 1);
                 u32 sk = 0;
                 for (u32 x = 0; x < E; x++) sk += L.next[x] != x + 1;
                 DBG_ADD(DBG_SKIPS, sk);
@@ -757,14 +773,21 @@ __global__ __launch_bounds__(PI_NL) void inflate_par_kernel(const zcg_chunk* __r
             const bool on = (tid <= E) && my_s != 0xFFFFFFFFu;
             u32 vend = nt;
             u32 marker = 0;
-            if (on && tid == E && nxt == N_MARKER) { vend = nt - 1; marker = tok_ref(L, tid, nt - 1); }
+            if (on && tid == E && nxt == N_MARKER) { vend = nt - 1; marker = tok_at(gp, tid, nt - 1); }
             // ---- placement ------------------------------------------------------------------
             // output bytes of my valid tokens [my_s, vend): the running sum minus
             // the tokens before my sync point (few) and a trailing marker
             u32 olen = 0;
             if (on) {
                 olen = olen_all - (vend < nt ? 1u : 0u);
-                for (u32 a = 0; a < my_s; a++) olen -= tok_len(tok_ref(L, tid, a));
+                for (u32 a0 = 0; a0 < my_s; a0 += 4) {
+                    u32 tk4[4];
+#pragma unroll
+                    for (u32 u = 0; u < 4; u++) tk4[u] = a0 + u < my_s ? tok_at(gp, tid, a0 + u) : 0u;
+#pragma unroll
+                    for (u32 u = 0; u < 4; u++)
+                        if (a0 + u < my_s) olen -= tok_len(tk4[u]);
+                }
             }
             u32 total;
             const u32 base = block_excl_scan(L, olen, &total);
@@ -783,14 +806,23 @@ __global__ __launch_bounds__(PI_NL) void inflate_par_kernel(const zcg_chunk* __r
                 // the lane whose output range holds byte `cap`
                 const bool mine = on && olen > 0 && base < cap && base + olen >= cap;
                 if (mine) {
+                    // take tokens while they fit below cap (at N: until cap is reached)
                     u32 acc = base, a = my_s;
-                    if (cap == room) {
-                        while (a < vend && acc < cap) { acc += tok_len(tok_ref(L, tid, a)); a++; }
-                        L.ctl[7] = (acc == cap) ? 1u : 0u;
-                    } else {
-                        while (a < vend && acc + tok_len(tok_ref(L, tid, a)) <= cap) { acc += tok_len(tok_ref(L, tid, a)); a++; }
-                        L.ctl[7] = 0;
+                    bool go = true;
+                    while (go && a < vend) {
+                        u32 tk8[8];
+#pragma unroll
+                        for (u32 u = 0; u < 8; u++) tk8[u] = a + u < vend ? tok_at(gp, tid, a + u) : 0u;
+#pragma unroll
+                        for (u32 u = 0; u < 8; u++) {
+                            if (go && a < vend) {  // while go holds, a == (a at the load) + u
+                                const u32 len = tok_len(tk8[u]);
+                                if (cap == room ? acc >= cap : acc + len > cap) go = false;
+                                else { acc += len; a++; }
+                            }
+                        }
                     }
+                    L.ctl[7] = (cap == room && acc == cap) ? 1u : 0u;
                     L.ctl[8] = acc < cap ? acc : cap;  // a token may cross N: clip there
                     L.ctl[9] = tid;
                     L.ctl[10] = a;
@@ -805,7 +837,7 @@ __global__ __launch_bounds__(PI_NL) void inflate_par_kernel(const zcg_chunk* __r
                 if (tid == cl) take_end = L.ctl[10];
                 if (tid < 64) {  // bit position of the first token not taken
                     const u32 a = L.ctl[10];
-                    const u32 pos = (a < L.ntok[cl]) ? token_pos(L, R0, cl, a) : L.endp[cl];
+                    const u32 pos = (a < L.ntok[cl]) ? token_pos(gp, R0, cl, a) : L.endp[cl];
                     if (tid == 0) L.ctl[11] = pos;
                 }
                 __syncthreads();
@@ -815,42 +847,49 @@ __global__ __launch_bounds__(PI_NL) void inflate_par_kernel(const zcg_chunk* __r
             if (mk == T_BAD) { r = R_INVALID; break; }
             if (mk == T_EXH) { r = R_EXHAUSTED; break; }
             // ---- token heads: one entry per taken token ----------------------------------
-            // literal -> 0x8000|byte (final); match -> dist-1 at its first byte,
+            // literal -> E_VAL|byte (final); match -> dist-1 at its first byte,
             // plus a token-start bit in head[] over the round's output bytes.
             const u64 S = P;
             bool far = false;
             {
                 u32 o = base;
                 u32 hw = 0xFFFFFFFFu, hbits = 0;
-                for (u32 a = my_s; a < take_end; a++) {
-                    const u32 tk = tok_ref(L, tid, a);
-                    u16 v;
-                    u32 len;
-                    if (tk & T_MATCH) {
-                        const u32 d = tok_dist(tk);
-                        if (d > P + o) far = true;  // before the stream start
-                        v = (u16)(d - 1);
-                        len = tok_len(tk);
-                    } else {
-                        v = (u16)(0x8000u | (tk & 0xFF));
-                        len = 1;
+                for (u32 a0 = my_s; a0 < take_end; a0 += 8) {
+                    u32 tk8[8];
+#pragma unroll
+                    for (u32 u = 0; u < 8; u++) tk8[u] = a0 + u < take_end ? tok_at(gp, tid, a0 + u) : 0u;
+#pragma unroll
+                    for (u32 u = 0; u < 8; u++) {
+                        if (a0 + u >= take_end) break;
+                        const u32 tk = tk8[u];
+                        u16 v;
+                        u32 len;
+                        if (tk & T_MATCH) {
+                            const u32 d = tok_dist(tk);
+                            if (d > P + o) far = true;  // before the stream start
+                            v = (u16)(d - 1);
+                            len = tok_len(tk);
+                        } else {
+                            v = (u16)(E_VAL | (tk & 0xFF));
+                            len = 1;
+                        }
+                        L.ptr[(S + o) & (PI_STAGE - 1)] = v;
+                        if ((o >> 5) != hw) {
+                            if (hbits) atomicOr(&L.head[hw], hbits);
+                            hw = o >> 5;
+                            hbits = 0;
+                        }
+                        hbits |= 1u << (o & 31);
+                        o += len;
                     }
-                    L.ptr[(S + o) & (PI_STAGE - 1)] = v;
-                    if ((o >> 5) != hw) {
-                        if (hbits) atomicOr(&L.head[hw], hbits);
-                        hw = o >> 5;
-                        hbits = 0;
-                    }
-                    hbits |= 1u << (o & 31);
-                    o += len;
                 }
                 if (hbits) atomicOr(&L.head[hw], hbits);
             }
             if (__syncthreads_or(far)) { r = R_INVALID; break; }
             TSTAMP(TP_PLACE);
             // ---- LZ77 resolution by pointer jumping ---------------------------------------
-            // Every round byte gets its value (literal, or a byte of the final
-            // window) or a pointer to an EARLIER round byte: byte k of a match
+            // Every round byte gets its value (literal), a pointer to an EARLIER
+            // round byte, or a far code (a byte before the round): byte k of a match
             // (start o, distance d) copies B[o - d + (k mod d)], which lies
             // before the match start.  Thread t expands the contiguous byte
             // range [x0, x1), carrying in the match that covers x0.
@@ -877,7 +916,7 @@ __global__ __launch_bounds__(PI_NL) void inflate_par_kernel(const zcg_chunk* __r
                     const u32 i = (u32)((S + x) & (PI_STAGE - 1));
                     if ((hb >> (x & 31)) & 1u) {
                         const u16 v = L.ptr[i];
-                        if (v & 0x8000u) { in_match = false; continue; }  // literal: final
+                        if (e_val(v)) { in_match = false; continue; }  // literal: final
                         mo = x; md = (u32)v + 1; mj = 0; in_match = true;
                     } else if (!in_match) {
                         continue;  // unreachable for a well-formed round
@@ -886,11 +925,32 @@ __global__ __launch_bounds__(PI_NL) void inflate_par_kernel(const zcg_chunk* __r
                     }
                     const int sp = (int)mo - (int)md + (int)mj;
                     u16 nv;
-                    if (sp < 0) nv = (u16)(0x8000u | L.win[(S + (int64_t)sp) & (PI_WIN - 1)]);
+                    if (sp < 0) nv = (u16)(E_FAR - 1 + (u32)(-sp));
                     else if ((u32)sp >= x0) nv = L.ptr[(S + (u32)sp) & (PI_STAGE - 1)];  // mine, final
                     else nv = (u16)sp;
                     L.ptr[i] = nv;
                 }
+            }
+            __syncthreads();
+            // far codes: read the bytes back from the committed output (the
+            // previous rounds' bytes, L2-hot; 8 loads in flight per thread)
+            for (u32 x = tid; x < emitted; x += 8 * PI_NL) {
+                u32 v[8];
+                u8 bv[8];
+#pragma unroll
+                for (u32 u = 0; u < 8; u++) {
+                    const u32 xx = x + u * PI_NL;
+                    v[u] = xx < emitted ? (u32)L.ptr[(u32)((S + xx) & (PI_STAGE - 1))] : E_VAL;
+                }
+#pragma unroll
+                for (u32 u = 0; u < 8; u++) {
+                    const bool fr = !e_val(v[u]) && v[u] >= E_FAR;
+                    bv[u] = fr ? ((const gu8*)dst)[swap_pos(S - (v[u] - E_FAR + 1), tw)] : (u8)0;
+                }
+#pragma unroll
+                for (u32 u = 0; u < 8; u++)
+                    if (!e_val(v[u]) && v[u] >= E_FAR)
+                        L.ptr[(u32)((S + x + u * PI_NL) & (PI_STAGE - 1))] = (u16)(E_VAL | bv[u]);
             }
             __syncthreads();
             TSTAMP(TP_LIT);
@@ -901,16 +961,16 @@ __global__ __launch_bounds__(PI_NL) void inflate_par_kernel(const zcg_chunk* __r
 #pragma unroll
                     for (u32 u = 0; u < 4; u++) {
                         const u32 xx = x + u * PI_NL;
-                        v[u] = xx < emitted ? L.ptr[(u32)((S + xx) & (PI_STAGE - 1))] : (u16)0x8000u;
+                        v[u] = xx < emitted ? L.ptr[(u32)((S + xx) & (PI_STAGE - 1))] : (u16)E_VAL;
                     }
 #pragma unroll
                     for (u32 u = 0; u < 4; u++)
-                        w[u] = (v[u] & 0x8000u) ? v[u] : L.ptr[(u32)((S + v[u]) & (PI_STAGE - 1))];
+                        w[u] = e_val(v[u]) ? v[u] : L.ptr[(u32)((S + v[u]) & (PI_STAGE - 1))];
 #pragma unroll
                     for (u32 u = 0; u < 4; u++)
-                        if (!(v[u] & 0x8000u)) {
+                        if (!e_val(v[u])) {
                             L.ptr[(u32)((S + x + u * PI_NL) & (PI_STAGE - 1))] = w[u];
-                            pending |= !(w[u] & 0x8000u);
+                            pending |= !e_val(w[u]);
                         }
                 }
                 if (dbg && tid == 0) DBG_ADD(DBG_MRR_IT, 1);
@@ -918,7 +978,7 @@ __global__ __launch_bounds__(PI_NL) void inflate_par_kernel(const zcg_chunk* __r
             }
             TSTAMP(TP_MRR);
             // ---- commit -------------------------------------------------------------------------------
-            par_commit(L, dst, S, S + emitted, t);
+            par_commit(L, dst, S, S + emitted, tw);
             P = S + emitted;
             if (dbg) {
                 if (tid == 0) DBG_ADD(DBG_BYTES, emitted);
@@ -949,12 +1009,17 @@ __global__ __launch_bounds__(PI_NL) void inflate_par_kernel(const zcg_chunk* __r
     }
     if (r == R_INVALID) st = ZCG_ERR_INVALID_DATA;
     else if (r == R_EXHAUSTED || P < D) st = ZCG_ERR_UNEXPECTED_EOF;
+    if (t.isbool) par_bool_norm(dst, P < D ? P : D);
     if (dbg) {
         if (tid == 0) L.dbgc[TP_TOTAL] = (u32)(__builtin_readcyclecounter() - t_start);
         __syncthreads();
         if (tid < 32 && L.dbgc[tid]) atomicAdd(&g_inf_dbg[tid], (unsigned long long)L.dbgc[tid]);
     }
-    if (tid == 0) status[c] = st;
+    __syncthreads();  // every token-slot access of this workgroup is done
+    if (tid == 0) {
+        status[c] = st;
+        atomicExch(&owner[slot], 0u);
+    }
 }
 
 extern "C" int zcg__debug_inflate_counters(unsigned long long* out, int reset) {
@@ -967,9 +1032,16 @@ extern "C" int zcg__debug_inflate_counters(unsigned long long* out, int reset) {
     return 0;
 }
 
+uint64_t inflate_par_ws_bytes(const zcg_array* a, uint32_t n) {
+    (void)a;
+    if (n == 0) return 0;
+    return PI_OWNER_BYTES + (u64)PI_NSLOT * PI_SLOT_WORDS * 4;
+}
+
 hipError_t launch_inflate_par(const zcg_array* a, const zcg_chunk* d_chunks, uint32_t n,
-                              int32_t* d_status, hipStream_t s) {
+                              int32_t* d_status, void* ws, uint64_t ws_bytes, hipStream_t s) {
     if (n == 0) return hipSuccess;
+    if (!ws || ws_bytes < inflate_par_ws_bytes(a, n)) return hipErrorInvalidValue;
     const DType t = make_dtype(a->dtype);
     const u64 D = a->chunk_num_elements * (u64)t.es;
     static bool attr_set = false;
@@ -980,8 +1052,12 @@ hipError_t launch_inflate_par(const zcg_array* a, const zcg_chunk* d_chunks, uin
         if (e != hipSuccess) return e;
         attr_set = true;
     }
+    u32* owner = (u32*)ws;  // the workspace is shared by the stream's codecs: clear the owners
+    hipError_t e = hipMemsetAsync(owner, 0, PI_OWNER_BYTES, s);
+    if (e != hipSuccess) return e;
+    gu32* pools = (gu32*)((u8*)ws + PI_OWNER_BYTES);
     hipLaunchKernelGGL(inflate_par_kernel, dim3(n), dim3(PI_NL), lds, s, d_chunks, n, D, t,
-                       a->compression.flags, d_status);
+                       a->compression.flags, d_status, owner, pools);
     return hipGetLastError();
 }
 
