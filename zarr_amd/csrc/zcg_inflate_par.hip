@@ -697,6 +697,12 @@ __global__ __launch_bounds__(PI_NL, 2) void inflate_par_kernel(const zcg_chunk* 
                 lb_drop(bs, adv);
                 q += adv;
             }
+            // prefetch the lane's first PF tokens into registers: the loads
+            // overlap the chain phase's barriers (placement usually needs no more)
+            constexpr u32 PF = 16;
+            u32 pre[PF];
+#pragma unroll
+            for (u32 u = 0; u < PF; u++) pre[u] = u < nt ? tok_at(gp, tid, u) : 0u;
             L.next[tid] = nxt;
             L.endp[tid] = q;
             L.give[tid] = give;
@@ -780,7 +786,10 @@ __global__ __launch_bounds__(PI_NL, 2) void inflate_par_kernel(const zcg_chunk* 
             u32 olen = 0;
             if (on) {
                 olen = olen_all - (vend < nt ? 1u : 0u);
-                for (u32 a0 = 0; a0 < my_s; a0 += 4) {
+#pragma unroll
+                for (u32 u = 0; u < PF; u++)
+                    if (u < my_s) olen -= tok_len(pre[u]);
+                for (u32 a0 = PF; a0 < my_s; a0 += 4) {
                     u32 tk4[4];
 #pragma unroll
                     for (u32 u = 0; u < 4; u++) tk4[u] = a0 + u < my_s ? tok_at(gp, tid, a0 + u) : 0u;
@@ -854,34 +863,37 @@ __global__ __launch_bounds__(PI_NL, 2) void inflate_par_kernel(const zcg_chunk* 
             {
                 u32 o = base;
                 u32 hw = 0xFFFFFFFFu, hbits = 0;
-                for (u32 a0 = my_s; a0 < take_end; a0 += 8) {
+                auto put = [&](u32 tk) {
+                    u16 v;
+                    u32 len;
+                    if (tk & T_MATCH) {
+                        const u32 d = tok_dist(tk);
+                        if (d > P + o) far = true;  // before the stream start
+                        v = (u16)(d - 1);
+                        len = tok_len(tk);
+                    } else {
+                        v = (u16)(E_VAL | (tk & 0xFF));
+                        len = 1;
+                    }
+                    L.ptr[(S + o) & (PI_STAGE - 1)] = v;
+                    if ((o >> 5) != hw) {
+                        if (hbits) atomicOr(&L.head[hw], hbits);
+                        hw = o >> 5;
+                        hbits = 0;
+                    }
+                    hbits |= 1u << (o & 31);
+                    o += len;
+                };
+#pragma unroll
+                for (u32 u = 0; u < PF; u++)
+                    if (u >= my_s && u < take_end) put(pre[u]);
+                for (u32 a0 = my_s > PF ? my_s : PF; a0 < take_end; a0 += 8) {
                     u32 tk8[8];
 #pragma unroll
                     for (u32 u = 0; u < 8; u++) tk8[u] = a0 + u < take_end ? tok_at(gp, tid, a0 + u) : 0u;
 #pragma unroll
-                    for (u32 u = 0; u < 8; u++) {
-                        if (a0 + u >= take_end) break;
-                        const u32 tk = tk8[u];
-                        u16 v;
-                        u32 len;
-                        if (tk & T_MATCH) {
-                            const u32 d = tok_dist(tk);
-                            if (d > P + o) far = true;  // before the stream start
-                            v = (u16)(d - 1);
-                            len = tok_len(tk);
-                        } else {
-                            v = (u16)(E_VAL | (tk & 0xFF));
-                            len = 1;
-                        }
-                        L.ptr[(S + o) & (PI_STAGE - 1)] = v;
-                        if ((o >> 5) != hw) {
-                            if (hbits) atomicOr(&L.head[hw], hbits);
-                            hw = o >> 5;
-                            hbits = 0;
-                        }
-                        hbits |= 1u << (o & 31);
-                        o += len;
-                    }
+                    for (u32 u = 0; u < 8; u++)
+                        if (a0 + u < take_end) put(tk8[u]);
                 }
                 if (hbits) atomicOr(&L.head[hw], hbits);
             }
@@ -933,22 +945,23 @@ __global__ __launch_bounds__(PI_NL, 2) void inflate_par_kernel(const zcg_chunk* 
             }
             __syncthreads();
             // far codes: read the bytes back from the committed output (the
-            // previous rounds' bytes, L2-hot; 8 loads in flight per thread)
-            for (u32 x = tid; x < emitted; x += 8 * PI_NL) {
-                u32 v[8];
-                u8 bv[8];
+            // previous rounds' bytes, L2-hot; FU loads in flight per thread)
+            constexpr u32 FU = 16;  // loads in flight per thread
+            for (u32 x = tid; x < emitted; x += FU * PI_NL) {
+                u32 v[FU];
+                u8 bv[FU];
 #pragma unroll
-                for (u32 u = 0; u < 8; u++) {
+                for (u32 u = 0; u < FU; u++) {
                     const u32 xx = x + u * PI_NL;
                     v[u] = xx < emitted ? (u32)L.ptr[(u32)((S + xx) & (PI_STAGE - 1))] : E_VAL;
                 }
 #pragma unroll
-                for (u32 u = 0; u < 8; u++) {
+                for (u32 u = 0; u < FU; u++) {
                     const bool fr = !e_val(v[u]) && v[u] >= E_FAR;
                     bv[u] = fr ? ((const gu8*)dst)[swap_pos(S - (v[u] - E_FAR + 1), tw)] : (u8)0;
                 }
 #pragma unroll
-                for (u32 u = 0; u < 8; u++)
+                for (u32 u = 0; u < FU; u++)
                     if (!e_val(v[u]) && v[u] >= E_FAR)
                         L.ptr[(u32)((S + x + u * PI_NL) & (PI_STAGE - 1))] = (u16)(E_VAL | bv[u]);
             }
