@@ -61,7 +61,7 @@ LEG = {"gzip": {"pool": 64, "batch": 4096, "strong": False},
        "lz4": {"pool": 512, "batch": 65536, "strong": True},   # C4: fixed 65 536-chunk job
        "raw": {"pool": 64, "batch": 1024, "strong": False},
        "xz": {"pool": 64, "batch": 2048, "strong": False},
-       "bzip2": {"pool": 64, "batch": 2048, "strong": False}}
+       "bzip2": {"pool": 64, "batch": 4096, "strong": False}}
 # encode legs: chunks per rank, timed steps
 ENCODE_LEG = {"gzip": (512, 2), "lz4": (1024, 3), "xz": (1024, 2), "bzip2": (512, 2)}
 TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r02_pmc_traffic.json")
