@@ -22,7 +22,7 @@
 //      transform fused, the block CRC as 256 segment CRCs combined by
 //      GF(2) x^(8n) shifts, checked against the stored CRC when the block
 //      completes inside D (read_exact semantics, chunk.rs:112-113).
-// Workspace: per chunk in flight (2 048) L (900 000 B) + selectors + state;
+// Workspace: per chunk in flight (4 096) L (900 000 B) + selectors + state;
 // per stage-B/C workgroup slot (1 024) T (900 000 B) + W (3.6 MB).
 // Algorithmic bytes per chunk: C + D.  Bound: stage A (serial Huffman/MTF),
 // not HBM.
