@@ -78,6 +78,9 @@ enum zcg_status {
 #define ZCG_FLAG_SERIAL_INFLATE 0x100u
 /* Accumulate internal kernel statistics (development builds / profiling). */
 #define ZCG_FLAG_DEBUG_COUNTERS 0x200u
+/* Xz decode keeps 32 KiB of history in LDS instead of 4 KiB: far matches
+ * stop re-reading the output from L2/HBM, at 3 instead of 8 chunks per CU. */
+#define ZCG_FLAG_XZ_RING_32K 0x400u
 
 /* CompressionType + its configuration (camelCase JSON keys in the reference). */
 typedef struct zcg_compression {

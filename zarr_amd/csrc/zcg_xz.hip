@@ -9,11 +9,12 @@
 //   * the probability model (7 990 u16 for lc+lp<=3; 14 134 for lc+lp=4,
 //     via a second launch with the larger LDS carve) lives in LDS; every
 //     lane reads/writes the same entry (LDS broadcast, no bank conflicts);
-//   * decoded bytes go to a 4 KiB LDS history ring; a match copies all its
-//     bytes in one wave-parallel step (byte k of a match at distance d is
-//     byte k mod d of the d bytes before it, all already decoded), reading
-//     the ring for recent history and the chunk's HBM output for far
-//     distances (older than the ring, already flushed and fenced);
+//   * decoded bytes go to an LDS history ring (4 KiB; 32 KiB with
+//     ZCG_FLAG_XZ_RING_32K); a match copies all its bytes in one wave-parallel
+//     step (byte k of a match at distance d is byte k mod d of the d bytes
+//     before it, all already decoded), reading the ring for the last
+//     ring - 512 bytes and the chunk's HBM output for far distances (older,
+//     already flushed and fenced);
 //   * the ring drains to HBM in 16-B-per-lane coalesced stores;
 //   * the block check (CRC32/CRC64) is 64 per-lane segment CRCs over HBM,
 //     combined with GF(2) x^(8n) shifts (zlib's crc32_combine, 64-bit);
@@ -27,11 +28,13 @@
 
 namespace zcg {
 
-constexpr u32 XZ_RING = 4096;
+constexpr u32 XZ_RING = 4096;         // default LDS history (8 chunks per CU)
+constexpr u32 XZ_RING_BIG = 32768;    // ZCG_FLAG_XZ_RING_32K (3 chunks per CU)
 constexpr u32 XZ_PROBS_SMALL = 1846 + (0x300u << 3);  // lc+lp <= 3
 constexpr u32 XZ_PROBS_BIG = 1846 + (0x300u << 4);    // lc+lp == 4
 
 // Device IO of zx::xz_decode: LDS model + LDS ring + HBM output.
+template <u32 XZ_RING>
 struct XzDevIO {
     u64 n, D, pos;
     const gu8* __restrict__ src;
@@ -80,22 +83,27 @@ struct XzDevIO {
         gfl = e;
         __threadfence_block();
     }
+    // The ring keeps the last XZ_RING bytes; flushes run every XZ_RING / 2
+    // bytes, so a byte is read from the ring while it is at most
+    // XZ_RING - 512 back (a copy overwrites <= 273 + 64 slots ahead of its
+    // sources) and from the flushed HBM output beyond that.
+    __device__ __forceinline__ bool in_ring(u64 s) const { return s + (XZ_RING - 512) >= pos; }
     __device__ __forceinline__ void put(u32 b) {
         ring[pos & (XZ_RING - 1)] = (u8)b;
         pos++;
-        if (pos - gfl > XZ_RING - 320) flush(pos & ~15ull);
+        if (pos - gfl > XZ_RING / 2) flush(pos & ~15ull);
     }
     __device__ __forceinline__ u32 back(u64 dist) {
         const u64 s = pos - 1 - dist;
-        return __builtin_amdgcn_readfirstlane(s >= gfl ? (u32)ring[s & (XZ_RING - 1)] : (u32)dst[s]);
+        return __builtin_amdgcn_readfirstlane(in_ring(s) ? (u32)ring[s & (XZ_RING - 1)] : (u32)dst[s]);
     }
     __device__ __forceinline__ void copy(u64 d, u32 len) {
-        if (pos + len - gfl > XZ_RING - 16) flush(pos & ~15ull);
+        if (pos + len - gfl > XZ_RING / 2) flush(pos & ~15ull);
         for (u32 base = 0; base < len; base += 64) {
             const u32 k = base + lane;
             if (k < len) {
                 const u64 s = pos - d + ((u64)k < d ? (u64)k : (u64)k % d);
-                const u8 v = s >= gfl ? ring[s & (XZ_RING - 1)] : dst[s];
+                const u8 v = in_ring(s) ? ring[s & (XZ_RING - 1)] : dst[s];
                 ring[(pos + k) & (XZ_RING - 1)] = v;
             }
         }
@@ -104,7 +112,7 @@ struct XzDevIO {
     __device__ __forceinline__ void copy_in(u64 ip, u32 len) {
         while (len > 0) {
             const u32 k = len < 256 ? len : 256;
-            if (pos + k - gfl > XZ_RING - 16) flush(pos & ~15ull);
+            if (pos + k - gfl > XZ_RING / 2) flush(pos & ~15ull);
             for (u32 q = lane; q < k; q += 64) ring[(pos + q) & (XZ_RING - 1)] = src[ip + q];
             pos += k;
             ip += k;
@@ -120,7 +128,7 @@ struct XzDevIO {
     }
 };
 
-template <u32 NPROB>
+template <u32 NPROB, u32 XZ_RING>
 __global__ __launch_bounds__(64) void xz_decode_kernel(const zcg_chunk* __restrict__ chunks, u32 n,
                                                        u64 D, DType t, int retry,
                                                        i32* __restrict__ status) {
@@ -135,7 +143,7 @@ __global__ __launch_bounds__(64) void xz_decode_kernel(const zcg_chunk* __restri
         if (lane == 0) status[c] = ZCG_ERR_INVALID_INPUT;
         return;
     }
-    XzDevIO io;
+    XzDevIO<XZ_RING> io;
     io.n = ch.src_len;
     io.D = D;
     io.pos = 0;
@@ -158,12 +166,19 @@ hipError_t launch_xz_decode(const zcg_array* a, const zcg_chunk* d_chunks, uint3
     if (n == 0) return hipSuccess;
     const DType t = make_dtype(a->dtype);
     const u64 D = a->chunk_num_elements * (u64)t.es;
-    hipLaunchKernelGGL(xz_decode_kernel<XZ_PROBS_SMALL>, dim3(n), dim3(64), 0, s, d_chunks, n, D, t,
+    if (a->compression.flags & ZCG_FLAG_XZ_RING_32K) {
+        hipLaunchKernelGGL((xz_decode_kernel<XZ_PROBS_SMALL, XZ_RING_BIG>), dim3(n), dim3(64), 0, s, d_chunks, n,
+                           D, t, 0, d_status);
+        hipLaunchKernelGGL((xz_decode_kernel<XZ_PROBS_BIG, XZ_RING_BIG>), dim3(n), dim3(64), 0, s, d_chunks, n, D,
+                           t, 1, d_status);
+        return hipGetLastError();
+    }
+    hipLaunchKernelGGL((xz_decode_kernel<XZ_PROBS_SMALL, XZ_RING>), dim3(n), dim3(64), 0, s, d_chunks, n, D, t,
                        0, d_status);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     // chunks that switched to lc+lp = 4 re-run with the larger model
-    hipLaunchKernelGGL(xz_decode_kernel<XZ_PROBS_BIG>, dim3(n), dim3(64), 0, s, d_chunks, n, D, t,
+    hipLaunchKernelGGL((xz_decode_kernel<XZ_PROBS_BIG, XZ_RING>), dim3(n), dim3(64), 0, s, d_chunks, n, D, t,
                        1, d_status);
     return hipGetLastError();
 }
