@@ -54,8 +54,11 @@ sys.path.insert(0, ROOT)
 METRIC = "decoded chunk GiB/s (device-resident) per CompressionType at 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
 GIB = float(1 << 30)
-KERNEL = {"gzip": "zcg::inflate_par_kernel", "lz4": "zcg::lz4_decode_kernel", "raw": "zcg::raw_kernel",
-          "xz": "zcg::xz_decode_kernel<7990u>", "bzip2": "zcg::bz2_decode_kernel"}
+# The kernels one zcg_decode_batch call launches (kernel_ms and roofline.traffic
+# cover the whole sequence: HIP events around the call, PMC summed per call).
+KERNEL = {"gzip": "zcg::inflate_par_kernel", "lz4": "zcg::lz4_{frames,blocks,finish}_kernel",
+          "raw": "zcg::raw_kernel", "xz": "zcg::xz_decode_kernel<{7990,14134}u, 4096u>",
+          "bzip2": "zcg::bz2_{init,stage_a,stage_bc,decode}_kernel"}
 # per-codec leg shapes: pool of distinct chunks, chunks per rank (weak) or per job (strong)
 LEG = {"gzip": {"pool": 64, "batch": 4096, "strong": False},
        "lz4": {"pool": 512, "batch": 65536, "strong": True},   # C4: fixed 65 536-chunk job

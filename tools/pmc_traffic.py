@@ -2,7 +2,8 @@
 """Reduce tools/pmc_traffic.sh output to HBM bytes per launch of each bench
 leg -> profiles/<name>.json (read by bench.py for roofline.traffic).
 
-Decode legs: the median over dispatches of the leg's decode kernel.
+Decode legs: every zcg:: dispatch of the leg summed, divided by the number
+of decode calls in the pass (warmup 1 + steps 2 = 3).
 Encode legs: every dispatch of the encode pipeline (zcg:: kernels and the
 hipCUB/rocPRIM radix sorts) summed, divided by the number of encode calls
 in the pass (warmup 1 + steps 2 = 3).
@@ -21,6 +22,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from bench import ENCODE_LEG, KERNEL, LEG  # noqa: E402
 
 ENCODE_CALLS = 3
+DECODE_CALLS = 3  # tools/pmc_traffic.sh runs the decode legs with --warmup 1 --steps 2
 
 
 def dispatches(path):
@@ -58,16 +60,18 @@ def main(src, dst):
                                 "fetch_bytes": int(2 * fs * 1024), "write_bytes": int(ws * 1024),
                                 "traffic_bytes": int(2 * fs * 1024 + ws * 1024), "per": "encode call"}
             continue
-        k = KERNEL[leg]
-        fv = sorted(v for n, v in f.values() if n.startswith(k) or k in n)
-        wv = sorted(v for n, v in w.values() if n.startswith(k) or k in n)
+        # every zcg:: dispatch of the leg's decode calls (warmup 1 + steps 2)
+        fv = [v for n, v in f.values() if "zcg::" in n]
+        wv = [v for n, v in w.values() if "zcg::" in n]
         if not fv or not wv:
             continue
-        fm, wm = fv[len(fv) // 2], wv[len(wv) // 2]
+        fm, wm = sum(fv) / DECODE_CALLS, sum(wv) / DECODE_CALLS
+        kn = sorted({n.split("(")[0] for n, _ in f.values() if "zcg::" in n})
         batch = LEG[leg]["batch"]
-        res["legs"][leg] = {"kernel": k, "batch_per_gpu": batch, "fetch_bytes": int(2 * fm * 1024),
-                            "write_bytes": int(wm * 1024), "traffic_bytes": int(2 * fm * 1024 + wm * 1024),
-                            "dispatches": len(fv), "per": "launch"}
+        res["legs"][leg] = {"kernel": KERNEL[leg], "kernels": kn, "batch_per_gpu": batch,
+                            "fetch_bytes": int(2 * fm * 1024), "write_bytes": int(wm * 1024),
+                            "traffic_bytes": int(2 * fm * 1024 + wm * 1024), "dispatches": len(fv),
+                            "per": "decode call"}
     json.dump(res, open(dst, "w"), indent=1)
     print(json.dumps(res, indent=1))
 

@@ -4,10 +4,10 @@
 # One rocprofv3 --pmc pass per counter (FETCH_SIZE takes 3 of the 4 TCC
 # slots, WRITE_SIZE 2, so they cannot share a pass), each under its own
 # time limit; the first failure ends the script.
-#   usage: tools/pmc_traffic.sh OUTDIR [leg ...]   (legs: gzip lz4 raw xz bzip2 gzip_encode ...)
+#   usage: tools/pmc_traffic.sh OUTDIR [leg ...]   (legs: gzip lz4 raw xz bzip2 {gzip,lz4,xz,bzip2}_encode)
 set -o pipefail
 out=$1; shift
-legs=${*:-gzip lz4 raw xz bzip2 gzip_encode}
+legs=${*:-gzip lz4 raw xz bzip2 gzip_encode lz4_encode xz_encode bzip2_encode}
 root="${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p "$out"
 cd /tmp && export TMPDIR=/tmp
