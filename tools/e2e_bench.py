@@ -30,7 +30,7 @@ sys.path.insert(0, ROOT)
 
 import torch  # noqa: E402  (device memory, streams, pinned host buffers)
 
-from bench import build_pool, workload  # noqa: E402
+from bench import host_encode, workload  # noqa: E402
 from zarr_amd.batch import BatchCodec  # noqa: E402
 
 GIB = float(1 << 30)
@@ -49,7 +49,8 @@ def main():
         return encode_e2e(args)
     dev = torch.device("cuda:0")
     meta, gen, _ = workload(args.codec)
-    vals, streams = build_pool(args.codec, meta, gen, 32, 16, dev)
+    vals = [gen(i) for i in range(32)]
+    streams = host_encode(args.codec, vals, 16)
     uniq = [v.tobytes() for v in vals]
     D = len(uniq[0])
     n, sub = args.chunks, args.sub

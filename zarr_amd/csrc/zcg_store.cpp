@@ -135,6 +135,12 @@ struct Slot {
 };
 
 constexpr size_t STORE_BATCH_BYTES = 256ull << 20;  // decoded bytes per pipeline sub-batch
+// The serial-stream codecs need many chunks in flight to fill the GPU (one
+// wave per chunk): their sub-batches are 4x larger.
+size_t store_batch_bytes(const zcg_array* a) {
+    const int32_t c = a->compression.codec;
+    return (c == ZCG_CODEC_XZ || c == ZCG_CODEC_BZIP2) ? 4 * STORE_BATCH_BYTES : STORE_BATCH_BYTES;
+}
 
 struct OpenFile {
     int fd = -1;
@@ -172,7 +178,7 @@ extern "C" int zcg_store_read_chunks(zcg_ctx* ctx, const zcg_array* a, uint32_t 
     zcg_store_slots* S = ctx_store_slots(ctx);
     if (!S) return ZCG_ERR_RUNTIME;
     const uint64_t D = a->chunk_num_elements * (uint64_t)a->dtype.elem_size;
-    const uint32_t per = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(n, D ? STORE_BATCH_BYTES / D : n));
+    const uint32_t per = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(n, D ? store_batch_bytes(a) / D : n));
     const uint32_t nb = (n + per - 1) / per;
     std::vector<std::vector<OpenFile>> files(2);
     std::vector<std::vector<size_t>> offs(2);
@@ -293,7 +299,8 @@ extern "C" int zcg_store_write_chunks(zcg_ctx* ctx, const zcg_array* a, uint32_t
     if (!S) return ZCG_ERR_RUNTIME;
     const uint64_t D = a->chunk_num_elements * (uint64_t)a->dtype.elem_size;
     const uint64_t cap = al256(zcg_encode_bound(&a->compression, D));
-    const uint32_t per = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(n, STORE_BATCH_BYTES / std::max<uint64_t>(D + cap, 1)));
+    const uint32_t per = (uint32_t)std::max<uint64_t>(
+        1, std::min<uint64_t>(n, store_batch_bytes(a) / std::max<uint64_t>(D + cap, 1)));
     const uint32_t nb = (n + per - 1) / per;
     int rc = ZCG_OK;
     auto fail = [&](hipError_t e, const char* what) {

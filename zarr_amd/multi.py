@@ -57,11 +57,12 @@ class MultiDeviceCodec:
                                                         st.ctypes.data), "multi_read_chunks_host")
         return st[:n], outs
 
-    def store_read(self, meta: ArrayMetadata, paths: Sequence[str], t, io_threads: int = 8):
+    def store_read(self, meta: ArrayMetadata, paths: Sequence[str], t, io_threads: int = 16):
         check_array_type(t, meta)
         n = len(paths)
         N = meta.get_chunk_num_elements()
-        outs = [np.empty(N, np.dtype(t).newbyteorder("=")) for _ in range(n)]
+        buf = np.empty(max(n * N, 1), np.dtype(t).newbyteorder("="))
+        outs = [buf[i * N:(i + 1) * N] for i in range(n)]
         enc = [os.fsencode(p) for p in paths]
         cp = (ctypes.c_char_p * max(n, 1))(*enc)
         dsts = (ctypes.c_void_p * max(n, 1))(*[o.ctypes.data for o in outs])
@@ -72,7 +73,7 @@ class MultiDeviceCodec:
                     "multi_store_read_chunks")
         return outs, st[:n]
 
-    def store_write(self, meta: ArrayMetadata, paths: Sequence[str], datas, io_threads: int = 8):
+    def store_write(self, meta: ArrayMetadata, paths: Sequence[str], datas, io_threads: int = 16):
         n = len(paths)
         N = meta.get_chunk_num_elements()
         datas = [np.ascontiguousarray(d) for d in datas]

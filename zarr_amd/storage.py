@@ -117,7 +117,7 @@ class FilesystemHierarchy:
         return True
 
     def read_chunks(self, path_name: str, array_meta: ArrayMetadata, grid_positions, t,
-                    device: int = 0, io_threads: int = 8) -> List[Optional[SliceDataChunk]]:
+                    device: int = 0, io_threads: int = 16) -> List[Optional[SliceDataChunk]]:
         """Batched read_chunk through the native store path
         (zcg_store_read_chunks): files read under a shared flock into pinned
         staging by `io_threads` host threads, pipelined with H2D, the batch
@@ -137,7 +137,7 @@ class FilesystemHierarchy:
         return out
 
     def write_chunks(self, path_name: str, array_meta: ArrayMetadata, chunks: Sequence[SliceDataChunk],
-                     device: int = 0, io_threads: int = 8) -> None:
+                     device: int = 0, io_threads: int = 16) -> None:
         """Batched write_chunk (zcg_store_write_chunks): GPU encode, then each
         file written under an exclusive flock, truncated after locking
         (filesystem.rs:260-280)."""
@@ -176,14 +176,15 @@ def _cstrs(paths):
     return arr, enc
 
 
-def store_read(array_meta: ArrayMetadata, paths: Sequence[str], t, device: int = 0, io_threads: int = 8):
+def store_read(array_meta: ArrayMetadata, paths: Sequence[str], t, device: int = 0, io_threads: int = 16):
     """zcg_store_read_chunks: (list of element arrays, status array)."""
     check_array_type(t, array_meta)
     ctx = _native.context(device)
     n = len(paths)
     dt = np.dtype(t).newbyteorder("=")
     N = array_meta.get_chunk_num_elements()
-    arrs = [np.empty(N, dt) for _ in range(n)]
+    buf = np.empty(max(n * N, 1), dt)  # one allocation (large pages when the kernel offers them)
+    arrs = [buf[i * N:(i + 1) * N] for i in range(n)]
     dp = (ctypes.c_void_p * max(n, 1))(*[a.ctypes.data for a in arrs])
     cp, keep = _cstrs(paths)
     st = np.zeros(max(n, 1), np.int32)
@@ -195,7 +196,7 @@ def store_read(array_meta: ArrayMetadata, paths: Sequence[str], t, device: int =
     return arrs, st[:n]
 
 
-def store_write(array_meta: ArrayMetadata, paths: Sequence[str], datas, device: int = 0, io_threads: int = 8):
+def store_write(array_meta: ArrayMetadata, paths: Sequence[str], datas, device: int = 0, io_threads: int = 16):
     """zcg_store_write_chunks: status array.  Each element array must hold
     exactly get_chunk_num_elements() elements (chunk.rs:309-318)."""
     ctx = _native.context(device)
