@@ -7,17 +7,15 @@
 //      walks the block headers into the slot table (block k of a frame is
 //      placed at k*blockMax: LZ4F emits full blocks except the last);
 //   2. lz4_blocks_kernel — ONE WAVE PER BLOCK (lz4-rs writes independent
-//      blocks, lz.rs:88).  The block is decoded in steps over 64-byte windows
-//      of the compressed stream: every lane parses a sequence speculatively at
-//      its own byte (token, length bytes, offset; the window is one 16-byte
-//      load per lane), a scalar walk through the lanes' "next sequence"
-//      offsets (one v_readlane per sequence) marks the true sequence starts,
-//      a wave prefix sum places their output, and each start lane copies its
-//      literals and match (byte-exact ranges, no over-writes, sources read
-//      from the block's own output, L1/L2-hot).  Matches whose source lies in
-//      this step's own output, and long sequences, are copied afterwards in
-//      order by the whole wave (byte k of a match = byte o - d + (k mod d)).
-//      Stored blocks are a coalesced 16 B/lane copy;
+//      blocks, lz.rs:88), four blocks per 256-thread workgroup.  The block is
+//      decoded in steps over 64-byte windows of the compressed stream: every
+//      lane parses a sequence speculatively at its own byte, pointer doubling
+//      over the lanes' next-sequence offsets finds the true chain, a DPP
+//      prefix sum places the sequences' output, the step's bytes are produced
+//      byte-parallel into the wave's 4 KiB LDS ring (a byte, or a pointer to
+//      an earlier byte), resolved, and stored with coalesced dword stores.
+//      Long sequences go one at a time (section 2 below); stored blocks are
+//      a coalesced 16 B/lane copy;
 //   3. lz4_finish_kernel — one wave per chunk: per-chunk verdict from the
 //      slots, LZ4F's look-ahead at the next block header, the exact serial
 //      fallback (linked-block frames, a short block mid-frame, frames that
