@@ -226,7 +226,7 @@ int zcg_write_region(zcg_ctx* ctx, const zcg_region* r, void* const* d_chunk_tab
  * `io_threads` host threads (open + shared flock + read, as ReadableStore::get,
  * src/store/filesystem.rs:201-210), H2D, zcg_decode_batch, D2H into `dsts`
  * (N*elem_size bytes each), pipelined over two streams in sub-batches of
- * <= 256 MiB; status[i] = ZCG_ABSENT for a missing chunk (read_chunk -> None,
+ * <= 256 MiB (1 GiB for xz/bzip2); status[i] = ZCG_ABSENT for a missing chunk (read_chunk -> None,
  * src/storage.rs:226-234), ZCG_ERR_IO for a filesystem error, else the decode
  * status.  The write direction encodes `elems` (N*elem_size host bytes each)
  * on the GPU and writes each file as WriteableStore::set (filesystem.rs:260-280):
