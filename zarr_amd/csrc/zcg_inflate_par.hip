@@ -385,21 +385,20 @@ __device__ __attribute__((always_inline)) int read_dynamic_par(ParLds& L, BitIn&
         rec[r] = (u16)(adv | (l << 4) | (sym << 7));
     }
     __syncthreads();
-    // 2-symbol jumps (position), then 4-symbol jumps: pos (13 bits) | summed count << 13
+    // 4-symbol jumps: pos (13 bits) | summed count << 13 (positions past the
+    // region read the last record, as zlib's reader would run out there)
     auto cl = [](u32 r) -> u32 { return r < HD_BITS ? r : HD_BITS - 1; };
-    u16* rec2 = (u16*)L.in;
     u32* rec4 = (u32*)(L.ptr + HD_BITS);
     for (u32 r = tid; r < HD_BITS; r += PI_NL) {
-        const u32 r1 = r + (rec[r] & 15);
-        rec2[r] = (u16)(r1 + (rec[cl(r1)] & 15));
-    }
-    __syncthreads();
-    for (u32 r = tid; r < HD_BITS; r += PI_NL) {
-        const u32 r1 = cl(r + (rec[r] & 15));
-        const u32 r2 = cl(rec2[r]);
-        const u32 r3 = cl(r2 + (rec[r2] & 15));
-        const u32 c = hd_cnt(r, rec[r]) + hd_cnt(r1, rec[r1]) + hd_cnt(r2, rec[r2]) + hd_cnt(r3, rec[r3]);
-        rec4[r] = (u32)rec2[r2] | (c << 13);
+        const u32 a0 = rec[r];
+        const u32 r1 = r + (a0 & 15), r1c = cl(r1);
+        const u32 a1 = rec[r1c];
+        const u32 r2 = cl(r1 + (a1 & 15));
+        const u32 a2 = rec[r2];
+        const u32 q1 = r2 + (a2 & 15), q1c = cl(q1);
+        const u32 a3 = rec[q1c];
+        const u32 c = hd_cnt(r, a0) + hd_cnt(r1c, a1) + hd_cnt(r2, a2) + hd_cnt(q1c, a3);
+        rec4[r] = (q1 + (a3 & 15)) | (c << 13);
     }
     __syncthreads();
     // the walk over groups of 4 symbols: gpos[g] = start bit | out index << 13
@@ -496,17 +495,6 @@ __device__ __attribute__((always_inline)) int read_block_header_par(ParLds& L, B
     if (*type == 3) return R_INVALID;  // "invalid block type"
     if (*type == 1) { fixed_tables(L.lens, &L.lh, L.ltab, &L.dh, L.dtab); return R_OK; }
     return read_dynamic_par(L, b, dbg);
-}
-
-// Bit position of token `j` of lane `i`: its segment start plus the bit
-// lengths stored in tokens 0..j-1 (never markers).  Called by one full wave.
-__device__ u32 token_pos(const gu32* gp, u32 R0, u32 i, u32 j) {
-    const u32 lane = threadIdx.x & 63;
-    u32 sum = 0;
-    for (u32 k = lane; k < j; k += 64) sum += tok_bits(tok_at(gp, i, k));
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) sum += __shfl_xor(sum, d, 64);
-    return R0 + i * PI_SEG + sum;
 }
 
 __global__ __launch_bounds__(PI_NL, 2) void inflate_par_kernel(const zcg_chunk* __restrict__ chunks,
@@ -699,7 +687,7 @@ __global__ __launch_bounds__(PI_NL, 2) void inflate_par_kernel(const zcg_chunk* 
             }
             // prefetch the lane's first PF tokens into registers: the loads
             // overlap the chain phase's barriers (placement usually needs no more)
-            constexpr u32 PF = 16;
+            constexpr u32 PF = 32;
             u32 pre[PF];
 #pragma unroll
             for (u32 u = 0; u < PF; u++) pre[u] = u < nt ? tok_at(gp, tid, u) : 0u;
@@ -815,9 +803,18 @@ __global__ __launch_bounds__(PI_NL, 2) void inflate_par_kernel(const zcg_chunk* 
                 // the lane whose output range holds byte `cap`
                 const bool mine = on && olen > 0 && base < cap && base + olen >= cap;
                 if (mine) {
-                    // take tokens while they fit below cap (at N: until cap is reached)
+                    // take tokens while they fit below cap (at N: until cap is reached);
+                    // the first PF come from registers
                     u32 acc = base, a = my_s;
                     bool go = true;
+#pragma unroll
+                    for (u32 u = 0; u < PF; u++) {
+                        if (go && u >= my_s && u < vend) {  // a == u here
+                            const u32 len = tok_len(pre[u]);
+                            if (cap == room ? acc >= cap : acc + len > cap) go = false;
+                            else { acc += len; a++; }
+                        }
+                    }
                     while (go && a < vend) {
                         u32 tk8[8];
 #pragma unroll
@@ -831,10 +828,22 @@ __global__ __launch_bounds__(PI_NL, 2) void inflate_par_kernel(const zcg_chunk* 
                             }
                         }
                     }
+                    // bit position of the first token not taken: the segment start
+                    // plus the stored bit lengths of tokens [0, a), or the lane's end
+                    u32 pos = q;
+                    if (a < nt) {
+                        u32 sb = 0;
+#pragma unroll
+                        for (u32 u = 0; u < PF; u++)
+                            if (u < a) sb += tok_bits(pre[u]);
+                        for (u32 j = PF; j < a; j++) sb += tok_bits(tok_at(gp, tid, j));
+                        pos = R0 + tid * PI_SEG + sb;
+                    }
                     L.ctl[7] = (cap == room && acc == cap) ? 1u : 0u;
                     L.ctl[8] = acc < cap ? acc : cap;  // a token may cross N: clip there
                     L.ctl[9] = tid;
                     L.ctl[10] = a;
+                    L.ctl[11] = pos;
                 }
                 __syncthreads();
                 const u32 cl = L.ctl[9];
@@ -844,12 +853,6 @@ __global__ __launch_bounds__(PI_NL, 2) void inflate_par_kernel(const zcg_chunk* 
                 mk = 0;
                 if (tid > cl) take_end = my_s;
                 if (tid == cl) take_end = L.ctl[10];
-                if (tid < 64) {  // bit position of the first token not taken
-                    const u32 a = L.ctl[10];
-                    const u32 pos = (a < L.ntok[cl]) ? token_pos(gp, R0, cl, a) : L.endp[cl];
-                    if (tid == 0) L.ctl[11] = pos;
-                }
-                __syncthreads();
                 round_end = L.ctl[11];
             }
             // ---- errors on the taken range ----------------------------------------------------
