@@ -75,7 +75,7 @@ __device__ inline u32 bz_xpow8(u64 n) {
 struct BzDevIO {
     const gu8* src;
     u64 n;
-    u64 wbase, wlo, whi;  // 16-byte input window (wave-uniform)
+    u64 cbp, bb;          // bit reader (wave-uniform): bits [cbp, cbp + 64), MSB-first
     // The compressed stream is staged in VGPRs, 2 KiB spread over the wave:
     // lane i holds bytes [vb + 16 i, +16) (wc) and [vb + 1024 + 16 i, +16)
     // (wn).  The 16-byte window refills from these with readlane (no memory
@@ -120,33 +120,41 @@ struct BzDevIO {
         lt0 = lt1 = lt2 = lt3 = lt4 = lt5 = ltc = wc = wn = z;
         ltc_t = 0xFFFFFFFFu;
         vb = ~0ull >> 1;         // next refill re-stages from memory
-        wbase = ~0ull >> 1;      // next peek refills
+        cbp = ~0ull >> 1;        // next peek refills
+    }
+    // The bit reader: bb holds the 64 stream bits from bit cbp on, MSB-first
+    // (bzip2's bit order), so a peek is two scalar shifts; it refills from the
+    // staged window every >= 33 bits, byte-swapping the words in VGPRs before
+    // they are read out (no 64-bit byte swap on the scalar path).
+    __device__ __forceinline__ u32 word_be(u32 widx) {  // staged word widx, big-endian
+        const u32x4 v = widx < 256 ? wc : wn;
+        const u32 c = widx & 3;
+        const u32 x = c == 0 ? v.x : (c == 1 ? v.y : (c == 2 ? v.z : v.w));
+        return (u32)__builtin_amdgcn_readlane((int)__builtin_bswap32(x), (int)((widx >> 2) & 63));
     }
     __device__ __forceinline__ void refill(u64 byte) {
         const u64 a = byte & ~3ull;
-        if (a < vb || a + 20 > vb + 2048 + 1024) {
+        if (a < vb || a + 12 > vb + 2048 + 1024) {
             stage(a);
-        } else if (a + 20 > vb + 2048) {
+        } else if (a + 12 > vb + 2048) {
             wc = wn;
             vb += 1024;
             wn = load16(vb + 1024 + 16ull * lane);
         }
         const u32 w0 = (u32)(a - vb) >> 2;
-        const u64 lo0 = ((u64)word(w0 + 1) << 32) | word(w0);
-        const u64 mid = ((u64)word(w0 + 3) << 32) | word(w0 + 2);
-        const u32 w4 = word(w0 + 4);
+        const u64 hi = ((u64)word_be(w0) << 32) | word_be(w0 + 1);
+        const u32 lo = word_be(w0 + 2);
         const u32 sh = (u32)(byte & 3) * 8;
-        wbase = byte;
-        wlo = sh ? (lo0 >> sh) | (mid << (64 - sh)) : lo0;
-        whi = sh ? (mid >> sh) | ((u64)w4 << (64 - sh)) : mid;
+        bb = sh ? (hi << sh) | (lo >> (32 - sh)) : hi;
+        cbp = byte * 8;
     }
     __device__ __forceinline__ u32 peek(u64 bp, u32 nb) {
-        const u64 byte = bp >> 3;
-        u64 o = byte - wbase;
-        if (o > 8) { refill(byte); o = 0; }
-        u64 v = (o == 0) ? wlo : (o == 8 ? whi : ((wlo >> (8 * o)) | (whi << (64 - 8 * o))));
-        v = __builtin_bswap64(v);
-        return (u32)((v << (bp & 7)) >> (64 - nb));
+        u64 d = bp - cbp;
+        if (d + nb > 64) {
+            refill(bp >> 3);
+            d = bp & 7;
+        }
+        return (u32)((bb << d) >> (64 - nb));
     }
     __device__ __forceinline__ zb::Group* group(u32 t) { return groups + t; }
     __device__ __forceinline__ u8* lens(u32 t) { return (u8*)(lensb + t * 260); }
@@ -627,8 +635,8 @@ __device__ __forceinline__ void bz_io_init(BzDevIO& io, const zcg_chunk& ch, zb:
                                            gu8* sel, gu8* L, int lane) {
     io.src = (const gu8*)ch.src;
     io.n = ch.src_len;
-    io.wbase = ~0ull >> 1;
-    io.wlo = io.whi = 0;
+    io.cbp = ~0ull >> 1;
+    io.bb = 0;
     io.groups = groups;
     io.lensb = (lu8*)lensb;
     io.ltc_t = 0xFFFFFFFFu;
