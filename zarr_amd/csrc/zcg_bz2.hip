@@ -334,6 +334,7 @@ struct BzBcLds {
     u16 succ[BZ_NSAMP + 1];
     u32 slen[BZ_NSAMP + 1];
     u32 soff[BZ_NSAMP + 1];
+    u32 pcap[BZ_NSAMP + 1];  // where a walk longer than CAP stood at step CAP
     u32 tstate[BZ_T];
     u32 tcrc[BZ_T];
     u32 tlen[BZ_T];
@@ -347,13 +348,14 @@ struct BzBcLds {
 // orig, stored_crc, randomised, out_pos}.  Out: X.sh.out_pos advanced,
 // X.tcrc[0] = the block CRC; returns a final chunk status (>= 0) or -1 when
 // the stream continues.
-__device__ __forceinline__ int bz_block_bc(BzBcLds& X, const gu8* L, gu8* T, gu32* W, gu8* dst, u64 D,
-                                           DType t, u32 vflags, u64& t_last) {
+__device__ __forceinline__ int bz_block_bc(BzBcLds& X, const gu8* L, gu8* LB, gu8* T, gu32* W, gu8* dst,
+                                           u64 D, DType t, u32 vflags, u64& t_last) {
     const u32 tid = threadIdx.x, lane = tid & 63;
     const u32 wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     auto& hist = X.hist;
     auto& succ = X.succ;
     auto& slen = X.slen;
+    auto& pcap = X.pcap;
     auto& soff = X.soff;
     auto& tstate = X.tstate;
     auto& tcrc = X.tcrc;
@@ -411,8 +413,17 @@ __device__ __forceinline__ int bz_block_bc(BzBcLds& X, const gu8* L, gu8* T, gu3
 #define BZ_IS_SAMPLE(p) ((((p) & smask) == 0) || ((p) == p0))
 #define BZ_SID(p) ((((p) & smask) == 0) ? ((p) >> lgs) : NR)
     for (u32 k = tid; k <= BZ_NSAMP; k += BZ_T) soff[k] = 0xFFFFFFFFu;
+    // One walk per sample: step m from position p reads W[p] = next << 8 |
+    // L[next], i.e. output byte soff + 1 + m.  The first CAP bytes of each
+    // walk are kept (4 at a time in a register, then one u32 store) in the
+    // L column's space, free once W exists; a walk longer than CAP records
+    // where it was at step CAP and finishes after the ranking.
+    const u32 CAP = S < 16 ? 16u : S;
+    gu32* buf32 = (gu32*)LB;
+    const u32 Lp0 = L[p0];  // T[0] (the cycle's first byte), before LB is overwritten
+    __syncthreads();
     {
-        u32 ps[BZ_WALKS], ln[BZ_WALKS], sidk[BZ_WALKS];
+        u32 ps[BZ_WALKS], ln[BZ_WALKS], sidk[BZ_WALKS], acc[BZ_WALKS];
         u32 act = 0;
 #pragma unroll
         for (int k = 0; k < BZ_WALKS; k++) {
@@ -422,19 +433,32 @@ __device__ __forceinline__ int bz_block_bc(BzBcLds& X, const gu8* L, gu8* T, gu3
             sidk[k] = sd;
             ps[k] = !last ? (sd << lgs) : p0;
             ln[k] = 0;
+            acc[k] = 0;
             if (on) act |= 1u << k;
         }
         while (act) {
-            u32 nx[BZ_WALKS];
+            u32 w[BZ_WALKS];
 #pragma unroll
-            for (int k = 0; k < BZ_WALKS; k++) nx[k] = (act >> k & 1) ? W[ps[k]] >> 8 : 0u;
+            for (int k = 0; k < BZ_WALKS; k++) w[k] = (act >> k & 1) ? W[ps[k]] : 0u;
 #pragma unroll
             for (int k = 0; k < BZ_WALKS; k++) {
                 if (!(act >> k & 1)) continue;
-                ln[k]++;
-                ps[k] = nx[k];
-                if (BZ_IS_SAMPLE(nx[k])) {
-                    succ[sidk[k]] = (u16)BZ_SID(nx[k]);
+                const u32 m = ln[k], nx = w[k] >> 8;
+                if (m < CAP) {
+                    acc[k] |= (w[k] & 0xFF) << (8 * (m & 3));
+                    if ((m & 3) == 3) {
+                        buf32[(sidk[k] * CAP + m) >> 2] = acc[k];
+                        acc[k] = 0;
+                    }
+                } else if (m == CAP) {
+                    pcap[sidk[k]] = ps[k];
+                }
+                ln[k] = m + 1;
+                ps[k] = nx;
+                if (BZ_IS_SAMPLE(nx)) {
+                    const u32 kept = ln[k] < CAP ? ln[k] : CAP;
+                    if (kept & 3) buf32[(sidk[k] * CAP + kept) >> 2] = acc[k];
+                    succ[sidk[k]] = (u16)BZ_SID(nx);
                     slen[sidk[k]] = ln[k];
                     act &= ~(1u << k);
                 }
@@ -457,42 +481,64 @@ __device__ __forceinline__ int bz_block_bc(BzBcLds& X, const gu8* L, gu8* T, gu3
     __syncthreads();
     BZ_TSTAMP(3);
     if (sh.single) {
-        // T[of] = L[p]; the gather W[p] yields L[next] for the next step
-        u32 ps[BZ_WALKS], ln[BZ_WALKS], of[BZ_WALKS], by[BZ_WALKS];
+        // kept bytes -> T (thread per sample; byte m of walk s is T[soff + 1 + m])
+#pragma unroll
+        for (int k = 0; k < BZ_WALKS; k++) {
+            const bool last = k == BZ_WALKS - 1;
+            const u32 sd = !last ? tid + (u32)k * BZ_T : NR;
+            const bool on = !last ? sd < NR : (tid == 0 && extra);
+            if (!on || soff[sd] == 0xFFFFFFFFu) continue;
+            const u32 len = slen[sd], kept = len < CAP ? len : CAP;
+            u32 o = soff[sd] + 1;
+            for (u32 m = 0; m < kept; m += 4) {
+                const u32 v = buf32[(sd * CAP + m) >> 2];
+#pragma unroll
+                for (u32 j = 0; j < 4; j++)
+                    if (m + j < kept) {
+                        const u32 idx = o + m + j;
+                        T[idx < nblock ? idx : idx - nblock] = (u8)(v >> (8 * j));
+                    }
+            }
+        }
+        // walks longer than CAP: the rest, interleaved per thread
+        u32 q[BZ_WALKS], rem[BZ_WALKS], of[BZ_WALKS];
         u32 act = 0;
 #pragma unroll
         for (int k = 0; k < BZ_WALKS; k++) {
             const bool last = k == BZ_WALKS - 1;
             const u32 sd = !last ? tid + (u32)k * BZ_T : NR;
             const bool on = !last ? sd < NR : (tid == 0 && extra);
-            ps[k] = !last ? (sd << lgs) : p0;
-            of[k] = on ? soff[sd] : 0;
-            ln[k] = on ? slen[sd] : 0;
-            by[k] = 0;
-            if (on && of[k] != 0xFFFFFFFFu && ln[k]) {
+            q[k] = 0;
+            rem[k] = 0;
+            of[k] = 0;
+            if (on && soff[sd] != 0xFFFFFFFFu && slen[sd] > CAP) {
+                q[k] = pcap[sd];
+                rem[k] = slen[sd] - CAP;
+                of[k] = soff[sd] + 1 + CAP;
                 act |= 1u << k;
-                by[k] = L[ps[k]];
             }
         }
         while (act) {
             u32 w[BZ_WALKS];
 #pragma unroll
-            for (int k = 0; k < BZ_WALKS; k++) w[k] = (act >> k & 1) ? W[ps[k]] : 0u;
+            for (int k = 0; k < BZ_WALKS; k++) w[k] = (act >> k & 1) ? W[q[k]] : 0u;
 #pragma unroll
             for (int k = 0; k < BZ_WALKS; k++) {
                 if (!(act >> k & 1)) continue;
-                T[of[k]++] = (u8)by[k];
-                by[k] = w[k] & 0xFF;
-                ps[k] = w[k] >> 8;
-                if (--ln[k] == 0) act &= ~(1u << k);
+                const u32 idx = of[k]++;
+                T[idx < nblock ? idx : idx - nblock] = (u8)(w[k] & 0xFF);
+                q[k] = w[k] >> 8;
+                if (--rem[k] == 0) act &= ~(1u << k);
             }
         }
     } else if (tid == 0) {
-        // not one cycle (corrupt): libbz2's serial tPos walk
+        // not one cycle (corrupt): libbz2's serial tPos walk (T[k+1] = L[next] = W[p] & 0xFF)
         u32 p = p0;
-        for (u32 k = 0; k < nblock; k++) {
-            T[k] = L[p];
-            p = W[p] >> 8;
+        T[0] = (u8)Lp0;
+        for (u32 k = 1; k < nblock; k++) {
+            const u32 w = W[p];
+            T[k] = (u8)(w & 0xFF);
+            p = w >> 8;
         }
     }
 #undef BZ_IS_SAMPLE
@@ -763,7 +809,7 @@ __global__ __launch_bounds__(256) void bz2_stage_bc_kernel(const zcg_chunk* __re
     u8* bslot = wsb + (u64)b * BZ_BC_SLOT;
     const zcg_chunk ch = chunks[c];
     u64 t_last = __builtin_readcyclecounter();
-    const int fs = bz_block_bc(S, (const gu8*)slot, (gu8*)bslot, (gu32*)(bslot + BZ_BC_OFF_W), (gu8*)ch.dst, D, t,
+    const int fs = bz_block_bc(S, (const gu8*)slot, (gu8*)slot, (gu8*)bslot, (gu32*)(bslot + BZ_BC_OFF_W), (gu8*)ch.dst, D, t,
                                vflags, t_last);
     __syncthreads();  // all B/C workspace accesses done
     if (tid == 0) {
@@ -836,7 +882,7 @@ __global__ __launch_bounds__(256) void bz2_decode_kernel(const zcg_chunk* __rest
             S.sh.randomised = sh_s.randomised;
         }
         __syncthreads();
-        const int fs = bz_block_bc(S, (const gu8*)slot, (gu8*)bslot, (gu32*)(bslot + BZ_BC_OFF_W), (gu8*)ch.dst,
+        const int fs = bz_block_bc(S, (const gu8*)slot, (gu8*)slot, (gu8*)bslot, (gu32*)(bslot + BZ_BC_OFF_W), (gu8*)ch.dst,
                                    D, t, vflags, t_last);
         __syncthreads();
         if (fs >= 0) { final_status = fs; break; }

@@ -35,9 +35,13 @@
 #if defined(__HIP_DEVICE_COMPILE__)
 #define ZB_U32(x) ((x) = __builtin_amdgcn_readfirstlane(x))
 #define ZB_UB(c) (__builtin_amdgcn_readfirstlane((uint32_t)(c)) != 0)
+// u64 `left` < small k on the scalar unit (it has no 64-bit ordered compare;
+// the readfirstlane keeps the two halves from being re-fused into one)
+#define ZB_LT(left, k) (__builtin_amdgcn_readfirstlane((uint32_t)((left) >> 32)) == 0 && (uint32_t)(left) < (uint32_t)(k))
 #else
 #define ZB_U32(x) ((void)0)
 #define ZB_UB(c) (c)
+#define ZB_LT(left, k) ((left) < (uint64_t)(k))
 #endif
 
 #ifndef ZB_TRACE
@@ -116,7 +120,7 @@ ZB_INL int bz_block(IO& io, BzState& s) {
 // GET_BITS: consuming nb bits needs ceil((bp+nb)/8) <= lim visible bytes
 #define ZB_BITS(nb, out)                                               \
     do {                                                               \
-        if (ZB_UB(bp + (nb) > limbits)) { s.bitpos = bp; return R_STOP; } \
+        if (ZB_LT(limbits - bp, nb)) { s.bitpos = bp; return R_STOP; } /* bp <= limbits */ \
         out = io.peek(bp, (nb));                                       \
         ZB_TRACE(bp, nb, out);                                         \
         bp += (nb);                                                    \
@@ -284,7 +288,7 @@ ZB_INL int bz_block(IO& io, BzState& s) {
         u32 sym;
         {
             u32 hit = 0;
-            if (ZB_UB(bp + LUT_BITS <= limbits)) {
+            if (!ZB_LT(limbits - bp, LUT_BITS)) {
                 const u32 e = io.lut_get(gsel, io.peek(bp, LUT_BITS));
                 if (e) {
                     bp += e & 31;
