@@ -10,7 +10,8 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libzchunk_gpu.so")
+# ZCG_LIB: an alternative build of the same library (A/B kernel experiments)
+LIB_PATH = os.environ.get("ZCG_LIB") or os.path.join(_HERE, "libzchunk_gpu.so")
 
 OK, UNEXPECTED_EOF, INVALID_DATA, INVALID_INPUT, UNSUPPORTED, OUTPUT_TOO_SMALL = 0, 1, 2, 3, 4, 5
 ABSENT, IO = 6, 7  # store: no chunk file (read_chunk -> None); filesystem error

@@ -34,6 +34,18 @@
 // serial kernel (zcg_inflate.hip); tests/ compare the two.
 #include "zcg_inflate_common.h"
 
+// tuning knobs (A/B builds): tokens prefetched into registers per lane, far
+// gathers in flight per thread, waves per SIMD the register budget targets
+#ifndef ZCG_INF_PF
+#define ZCG_INF_PF 16
+#endif
+#ifndef ZCG_INF_FU
+#define ZCG_INF_FU 16
+#endif
+#ifndef ZCG_INF_WPE
+#define ZCG_INF_WPE 3
+#endif
+
 namespace zcg {
 
 constexpr u32 PI_NL = 256;       // lanes per chunk (4 waves)
@@ -95,13 +107,20 @@ constexpr u32 E_FAR = 0x4000u;
 static_assert(PI_STAGE <= E_FAR && E_FAR + PI_WIN <= E_VAL, "stage entry encoding");
 __device__ __forceinline__ bool e_val(u32 v) { return v >= E_VAL; }
 
-// 69 KiB: two chunks' workgroups per CU (8 waves).  The token lists live in a
+// 50 KiB: three chunks' workgroups per CU (12 waves).  The token lists live in a
 // per-workgroup slot of the HBM workspace (coalesced [token][lane] layout,
 // L2-resident while the chunk decodes), not in LDS.
 struct ParLds {
-    u16 ptr[PI_STAGE];               // round bytes (E_VAL / pointer / E_FAR entries); header scratch
-    u32 in[PI_IN_PAD];               // staged stream words (padded: in[padw(w)]); header scratch
-    u32 mark[PI_NL * (PI_SEGW + 1)]; // token-start bitmap of each lane's segment (+1 pad)
+    // The staged stream and the segment marks are dead after pass 2, the round
+    // bytes are first written by placement: they share storage (and the
+    // dynamic-header scratch lives there between rounds).
+    union {
+        u16 ptr[PI_STAGE];               // round bytes (E_VAL / pointer / E_FAR entries); header scratch
+        struct {
+            u32 in[PI_IN_PAD];               // staged stream words (padded: in[padw(w)])
+            u32 mark[PI_NL * (PI_SEGW + 1)]; // token-start bitmap of each lane's segment (+1 pad)
+        };
+    };
     u32 head[PI_STAGE / 32];         // token-start bitmap over the round's output bytes
     u32 ltab[INF_LTAB];
     u32 dtab[INF_DTAB];
@@ -122,7 +141,7 @@ struct ParLds {
 // debug counter add (LDS atomic; flushed to g_inf_dbg once per chunk)
 #define DBG_ADD(slot, v) atomicAdd(&L.dbgc[slot], (u32)(v))
 
-static_assert(sizeof(ParLds) <= 80 * 1024, "ParLds must leave room for two workgroups per CU");
+static_assert(sizeof(ParLds) <= 53 * 1024, "ParLds must leave room for three workgroups per CU");
 
 // Per-workgroup token slots in the workspace: slot s holds PI_TMAX x PI_NL
 // token words, token j of lane i at [j * PI_NL + i].  A workgroup takes a
@@ -305,6 +324,7 @@ __device__ __forceinline__ u32 block_excl_scan(ParLds& L, u32 v, u32* total) {
 // block expands the repeat codes in parallel.
 constexpr u32 HD_BITS = 4608;            // >= 316 symbols * 14 bits
 constexpr u32 HD_WORDS = HD_BITS / 32 + 8;
+static_assert(3 * HD_BITS * 2 + (HD_WORDS + 128 + 320) * 4 <= PI_STAGE * 2, "header scratch fits in ptr[]");
 
 __device__ __attribute__((always_inline)) int read_dynamic_par(ParLds& L, BitIn& b, bool dbg) {
     const u32 tid = threadIdx.x;
@@ -355,7 +375,9 @@ __device__ __attribute__((always_inline)) int read_dynamic_par(ParLds& L, BitIn&
     const u64 H0 = b.consumed;
     const u64 B0 = H0 >> 3;
     const u32 o = (u32)(H0 & 7);
-    u32* hw = L.mark + 512;
+    // header scratch, all inside ptr[] (bytes): rec [0, 9216), rec4 [9216, 27648),
+    // hw [27648, 28256), gpos [28256, 28768), srec [28768, 30048)
+    u32* hw = (u32*)(L.ptr + 3 * HD_BITS);
     for (u32 w = tid; w < HD_WORDS; w += PI_NL) {
         const u64 q = B0 + 4ull * w;
         u32 v = 0;
@@ -402,7 +424,7 @@ __device__ __attribute__((always_inline)) int read_dynamic_par(ParLds& L, BitIn&
     }
     __syncthreads();
     // the walk over groups of 4 symbols: gpos[g] = start bit | out index << 13
-    u32* gpos = L.mark;
+    u32* gpos = hw + HD_WORDS;  // <= 79 groups (each covers >= 4 symbol indices)
     const u32 total = nlen + ndist;
     if (dbg && tid == 0) { const u64 t = __builtin_readcyclecounter(); L.dbgc[26] += (u32)(t - hts); hts = t; }
     if (tid == 0) {
@@ -420,7 +442,7 @@ __device__ __attribute__((always_inline)) int read_dynamic_par(ParLds& L, BitIn&
     }
     __syncthreads();
     // expand the groups: symbol i = 4g + k while its out index < total
-    u32* srec = L.mark + 128;  // idx | cnt << 9 | sym << 17
+    u32* srec = gpos + 128;  // idx | cnt << 9 | sym << 17 (<= 316 symbols)
     {
         const u64 lim64 = b.limit - H0;
         const u32 lim = lim64 < HD_BITS ? (u32)lim64 : HD_BITS;
@@ -497,7 +519,7 @@ __device__ __attribute__((always_inline)) int read_block_header_par(ParLds& L, B
     return read_dynamic_par(L, b, dbg);
 }
 
-__global__ __launch_bounds__(PI_NL, 2) void inflate_par_kernel(const zcg_chunk* __restrict__ chunks,
+__global__ __launch_bounds__(PI_NL, ZCG_INF_WPE) void inflate_par_kernel(const zcg_chunk* __restrict__ chunks,
                                                                u32 n, u64 D, DType t, u32 vflags,
                                                                i32* __restrict__ status,
                                                                u32* __restrict__ owner, gu32* __restrict__ pools) {
@@ -687,7 +709,7 @@ __global__ __launch_bounds__(PI_NL, 2) void inflate_par_kernel(const zcg_chunk* 
             }
             // prefetch the lane's first PF tokens into registers: the loads
             // overlap the chain phase's barriers (placement usually needs no more)
-            constexpr u32 PF = 32;
+            constexpr u32 PF = ZCG_INF_PF;
             u32 pre[PF];
 #pragma unroll
             for (u32 u = 0; u < PF; u++) pre[u] = u < nt ? tok_at(gp, tid, u) : 0u;
@@ -949,7 +971,7 @@ __global__ __launch_bounds__(PI_NL, 2) void inflate_par_kernel(const zcg_chunk* 
             __syncthreads();
             // far codes: read the bytes back from the committed output (the
             // previous rounds' bytes, L2-hot; FU loads in flight per thread)
-            constexpr u32 FU = 16;  // loads in flight per thread
+            constexpr u32 FU = ZCG_INF_FU;  // loads in flight per thread
             for (u32 x = tid; x < emitted; x += FU * PI_NL) {
                 u32 v[FU];
                 u8 bv[FU];
