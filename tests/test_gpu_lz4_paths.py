@@ -1,0 +1,70 @@
+"""ZCG_FLAG_LZ4_WAVE_PER_BLOCK: the two LZ4 block decoders (one lane per block,
+the default; one wave per block) must give the same bytes and statuses on
+valid, truncated and corrupted frames (lz.rs:81-83 -> LZ4F_decompress), and
+both must match the oracle."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+from zarr_amd import ArrayMetadata, Lz4
+from zarr_amd.batch import BatchCodec, PackedStreams
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
+import zref  # noqa: E402  (oracle: checker only)
+
+pytestmark = pytest.mark.gpu
+
+FLAG_WAVE = 0x800
+
+
+def _decode(streams, D, flags):
+    import torch
+    meta = ArrayMetadata.new([D * len(streams)], [D], "u1", Lz4(65536))
+    packed = PackedStreams(streams, D, "cuda:0")
+    BatchCodec(0).decode(meta, packed, flags=flags)
+    torch.cuda.synchronize()
+    return packed.status.cpu().numpy(), packed.dst.view(len(streams), -1).cpu().numpy()
+
+
+def _payloads():
+    rng = np.random.default_rng(44)
+    walk = np.cumsum(rng.integers(-3, 4, 524288)).astype("<i2").tobytes()       # C4 shape
+    far = np.empty(1 << 20, np.uint8)                                             # offsets 128 B .. 64 KiB
+    base = rng.integers(0, 256, 1 << 20, dtype=np.uint8)
+    far[:70000] = base[:70000]
+    p = 70000
+    while p < len(far):
+        d, ln = int(rng.integers(100, 65535)), int(rng.integers(4, 90))
+        ln = min(ln, len(far) - p)
+        far[p:p + ln] = far[p - d:p - d + ln]
+        if p + ln + 3 <= len(far):
+            far[p + ln:p + ln + 3] = rng.integers(0, 256, 3, dtype=np.uint8)
+        p += ln + 3
+    runs = np.repeat(rng.integers(0, 4, 20000, dtype=np.uint8), rng.integers(1, 200, 20000))[: 1 << 20]
+    runs = np.pad(runs, (0, (1 << 20) - len(runs)))
+    return [walk, far.tobytes(), runs.tobytes(), rng.integers(0, 256, 1 << 20, dtype=np.uint8).tobytes()]
+
+
+def test_lane_and_wave_decoders_agree():
+    D = 1 << 20
+    pays = _payloads()
+    streams = [zref.encode(zref.LZ4, 65536, np.frombuffer(p, np.uint8))[1] for p in pays]
+    rng = np.random.default_rng(5)
+    extra = [streams[0][: len(streams[0]) // 3]]
+    for _ in range(60):
+        b = bytearray(streams[int(rng.integers(0, 3))])
+        b[int(rng.integers(7, len(b)))] ^= int(rng.integers(1, 256))
+        extra.append(bytes(b))
+    allst = streams + extra
+    s0, o0 = _decode(allst, D, 0)
+    s1, o1 = _decode(allst, D, FLAG_WAVE)
+    assert s0.tolist() == s1.tolist()
+    for i, p in enumerate(pays):
+        assert s0[i] == 0 and bytes(o0[i]) == p and bytes(o1[i]) == p
+    for i, st in enumerate(allst):
+        ost, ref = zref.decode(zref.LZ4, st, D, 1)
+        assert ost == s0[i], i
+        if ost == 0:
+            assert bytes(o0[i]) == ref and bytes(o1[i]) == ref

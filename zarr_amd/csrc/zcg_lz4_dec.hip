@@ -734,6 +734,185 @@ __global__ __launch_bounds__(256) void lz4_blocks_kernel(const zcg_chunk* __rest
     }
 }
 
+// ---- 2b. one LANE per block (default) ---------------------------------------
+// A C4 stream is ~14 000 sequences of ~4.7 output bytes per 64 KiB block, so
+// per-sequence instruction count is what bounds the decoder.  Here every lane
+// runs LZ4_decompress_safe on its own block (64 blocks per wave, no
+// speculation, no cross-lane steps), and the output goes through a per-lane
+// LDS ring of LZ_LRB bytes that is written to HBM in whole, aligned
+// LZ_LRB/2-byte pieces (16-byte stores), so HBM sees full-sector writes even though
+// the 64 lanes of a wave write 64 different blocks.  Match sources nearer
+// than the ring come from LDS; older ones from the block's own HBM output,
+// which this lane stored earlier (same-thread order).  Input comes through a
+// 16-byte register window (LzWin).
+#ifndef ZCG_LZ4_LRB
+#define ZCG_LZ4_LRB 128
+#endif
+#ifndef ZCG_LZ4_LDS_PAD
+#define ZCG_LZ4_LDS_PAD 0
+#endif
+constexpr u32 LZ_LRB = ZCG_LZ4_LRB;  // ring bytes per lane (>= 2 * LZ_LPC)
+constexpr u32 LZ_LPC = LZ_LRB / 2;  // flush granularity = longest piece written between flushes
+constexpr u32 LZ_LRM = LZ_LRB - 1;
+#ifndef ZCG_LZ4_LWG
+#define ZCG_LZ4_LWG 64
+#endif
+constexpr u32 LZ_LWG = ZCG_LZ4_LWG;  // lanes (blocks) per workgroup
+
+struct LaneRing {
+    lu8* R;      // this lane's ring
+    gu8* dst;    // the block's output
+    u32 lim;     // bytes of the block below N*size (never store at >= lim)
+    u32 fl;      // output below fl is in HBM (a multiple of LZ_LPC)
+    __device__ __forceinline__ void put(u32 p, u32 b) { R[p & LZ_LRM] = (u8)b; }
+    __device__ __forceinline__ u32 get(u32 p) const { return R[p & LZ_LRM]; }
+    __device__ __forceinline__ void store_piece(u32 a) {
+        if (a >= lim) return;
+        const lu8* p = R + (a & LZ_LRM);
+        if (a + LZ_LPC <= lim) {
+#pragma unroll
+            for (u32 i = 0; i < LZ_LPC / 16; i++) {
+                const u32x4 v = *(const __attribute__((address_space(3))) u32x4*)(p + 16 * i);
+                *(gu32x4_ua*)(dst + a + 16 * i) = v;
+            }
+        } else {
+            for (u32 i = 0; a + i < lim; i++) dst[a + i] = p[i];
+        }
+    }
+    // store the whole pieces below op
+    __device__ __forceinline__ void flush(u32 op) {
+        while (op - fl >= LZ_LPC) { store_piece(fl); fl += LZ_LPC; }
+    }
+    __device__ __forceinline__ void finish(u32 op) {
+        flush(op);
+        for (u32 i = fl; i < op && i < lim; i++) dst[i] = R[i & LZ_LRM];
+    }
+    // byte p of the output (p < op, p < lim): LDS when the ring still holds it
+    // (op - p < LZ_LRB), else HBM
+    __device__ __forceinline__ u32 src_byte(u32 p, u32 op) const {
+        return op - p < LZ_LRB ? (u32)R[p & LZ_LRM] : (u32)dst[p];
+    }
+};
+
+// LZ4_decompress_safe of one block (the checks of lz4_block above, in its order),
+// positions block-relative, low = 0 (independent blocks).
+__device__ int lz4_lane_block(const u8* __restrict__ src, u32 iend, u64 avail, LaneRing& O, u32 cap,
+                              u32* out_n) {
+    u32 ip = 0, op = 0;
+    LzWin in{src, avail, u32x4{0, 0, 0, 0}, 0};
+    in.at(0);
+    for (;;) {
+        if (ip >= iend) return ZCG_ERR_INVALID_DATA;
+        const u32 token = in.byte(ip++);
+        u32 lit = token >> 4;
+        if (lit == 15) {
+            if ((i64)ip >= (i64)iend - 15) return ZCG_ERR_INVALID_DATA;
+            u32 s;
+            do {
+                s = in.byte(ip++);
+                lit += s;
+            } while (s == 255 && (i64)ip < (i64)iend - 15);
+        }
+        const u64 cpy = (u64)op + lit;
+        const bool last = cpy + 12 > cap || (i64)ip + lit > (i64)iend - 8;
+        if (last && ((u64)ip + lit != iend || cpy > cap)) return ZCG_ERR_INVALID_DATA;
+        // literals, in pieces of <= LZ_LPC bytes (a flush after each keeps op - fl < LZ_LRB)
+        for (u32 j0 = 0; j0 < lit; j0 += LZ_LPC) {
+            const u32 m = lit - j0 < LZ_LPC ? lit - j0 : LZ_LPC;
+            for (u32 j = 0; j < m; j++) O.put(op + j, in.byte(ip + j));
+            op += m;
+            ip += m;
+            O.flush(op);
+        }
+        if (last) break;
+        const u32 off = in.byte(ip) | (in.byte(ip + 1) << 8);
+        ip += 2;
+        u32 ml = token & 15;
+        if (ml == 15) {
+            u32 s;
+            do {
+                s = in.byte(ip++);
+                ml += s;
+                if ((i64)ip >= (i64)iend - 4) return ZCG_ERR_INVALID_DATA;
+            } while (s == 255);
+        }
+        ml += 4;
+        if (op < off) return ZCG_ERR_INVALID_DATA;
+        if ((u64)op + ml + 5 > cap) return ZCG_ERR_INVALID_DATA;
+        if (off == 0) {  // lz4 1.9.3: offset 0 decodes to zeros
+            for (u32 j0 = 0; j0 < ml; j0 += LZ_LPC) {
+                const u32 m = ml - j0 < LZ_LPC ? ml - j0 : LZ_LPC;
+                for (u32 j = 0; j < m; j++) O.put(op + j, 0);
+                op += m;
+                O.flush(op);
+            }
+        } else if (off >= LZ_LRB && ml <= 16 && ml <= LZ_LPC && op - off + 16 <= O.lim) {
+            // a far source: one 16-byte load from the block's HBM output
+            const u32x4 v = *(const gu32x4_ua*)(O.dst + op - off);
+            for (u32 j = 0; j < ml; j++) O.put(op + j, win_byte(v, j));
+            op += ml;
+            O.flush(op);
+        } else {
+            for (u32 j0 = 0; j0 < ml; j0 += LZ_LPC) {
+                const u32 m = ml - j0 < LZ_LPC ? ml - j0 : LZ_LPC;
+                for (u32 j = 0; j < m; j++) {
+                    const u32 p = op + j - off;
+                    O.put(op + j, p < O.lim ? O.src_byte(p, op + j) : 0u);
+                }
+                op += m;
+                O.flush(op);
+            }
+        }
+        if (ip - in.wb > 8) in.at(ip);  // the next sequence's window, in flight early
+    }
+    *out_n = op;
+    return ZCG_OK;
+}
+
+#ifndef ZCG_LZ4_WPE
+#define ZCG_LZ4_WPE 1
+#endif
+__global__ __launch_bounds__(LZ_LWG, ZCG_LZ4_WPE) void lz4_lanes_kernel(const zcg_chunk* __restrict__ chunks, u32 n, u64 D,
+                                                           u32 S, u32 vflags,
+                                                           const Lz4ChunkInfo* __restrict__ info,
+                                                           Lz4Slot* __restrict__ slots) {
+    __shared__ __attribute__((aligned(16))) u8 rings[LZ_LWG * LZ_LRB + ZCG_LZ4_LDS_PAD];
+    const u64 g = (u64)blockIdx.x * LZ_LWG + threadIdx.x;
+    const u32 c = (u32)(g / S);
+    const u32 k = (u32)(g - (u64)c * S);
+    if (c >= n) return;
+    const Lz4ChunkInfo ci = info[c];
+    if (ci.st != ZCG_OK || k >= ci.nslot) return;
+    const zcg_chunk ch = chunks[c];
+    Lz4Slot* sl = slots + (u64)c * S + k;
+    const u32 bs = sl->bs;
+    const u32 cs = bs & 0x7FFFFFFFu;
+    const u64 so = sl->src_off;
+    const u8* s = (const u8*)ch.src + so;
+    gu8* dst = (gu8*)ch.dst + (u64)k * ci.bmax;
+    const u64 op0 = (u64)k * ci.bmax;
+    const u32 lb = (u32)(D - op0 < ci.bmax ? D - op0 : ci.bmax);
+    int st = ZCG_OK;
+    u32 got = 0;
+    if ((ci.flags & F_BLOCK_CKSUM) && !(vflags & ZCG_FLAG_SKIP_LZ4_BLOCK_CHECKSUM))
+        if (xxh32(s, cs, 0) != ld32(s + cs)) st = ZCG_ERR_INVALID_DATA;
+    if (st == ZCG_OK) {
+        if (bs & 0x80000000u) {  // stored block
+            const u32 m = lb < cs ? lb : cs;
+            u32 i = 0;
+            for (; i + 16 <= m; i += 16) *(gu32x4_ua*)(dst + i) = ld16(s + i);
+            for (; i < m; i++) dst[i] = s[i];
+            got = cs;
+        } else {
+            LaneRing O{(lu8*)(rings + threadIdx.x * LZ_LRB), dst, lb, 0};
+            st = lz4_lane_block(s, cs, ch.src_len - so, O, ci.bmax, &got);
+            if (st == ZCG_OK) O.finish(got);
+        }
+    }
+    sl->got = got;
+    sl->st = st;
+}
+
 // ---- 3. per-chunk verdict, serial fallback, element transform -----------
 __global__ __launch_bounds__(64) void lz4_finish_kernel(const zcg_chunk* __restrict__ chunks, u32 n, u64 D,
                                                         DType t, u32 vflags, u32 S,
@@ -808,9 +987,14 @@ hipError_t launch_lz4_decode(const zcg_array* a, const zcg_chunk* d_chunks, uint
                        slots);
     const u64 waves = (u64)n * S;
     if ((waves + 3) / 4 > 0x7FFFFFFFull) return hipErrorInvalidValue;
-    if (D > 0)
-        hipLaunchKernelGGL(lz4_blocks_kernel, dim3((u32)((waves + 3) / 4)), dim3(256), 0, s, d_chunks, n, D,
-                           (u32)S, a->compression.flags, (const Lz4ChunkInfo*)info, slots);
+    if (D > 0) {
+        if (a->compression.flags & ZCG_FLAG_LZ4_WAVE_PER_BLOCK)
+            hipLaunchKernelGGL(lz4_blocks_kernel, dim3((u32)((waves + 3) / 4)), dim3(256), 0, s, d_chunks, n, D,
+                               (u32)S, a->compression.flags, (const Lz4ChunkInfo*)info, slots);
+        else
+            hipLaunchKernelGGL(lz4_lanes_kernel, dim3((u32)((waves + LZ_LWG - 1) / LZ_LWG)), dim3(LZ_LWG), 0, s,
+                               d_chunks, n, D, (u32)S, a->compression.flags, (const Lz4ChunkInfo*)info, slots);
+    }
     hipLaunchKernelGGL(lz4_finish_kernel, dim3(n), dim3(64), 0, s, d_chunks, n, D, t, a->compression.flags,
                        (u32)S, (const Lz4ChunkInfo*)info, (const Lz4Slot*)slots, d_status);
     return hipGetLastError();
