@@ -760,12 +760,13 @@ constexpr u32 LZ_LRM = LZ_LRB - 1;
 constexpr u32 LZ_LWG = ZCG_LZ4_LWG;  // lanes (blocks) per workgroup
 
 struct LaneRing {
-    lu8* R;      // this lane's ring
+    lu8* R;      // this lane's ring (16-byte aligned)
     gu8* dst;    // the block's output
     u32 lim;     // bytes of the block below N*size (never store at >= lim)
     u32 fl;      // output below fl is in HBM (a multiple of LZ_LPC)
-    __device__ __forceinline__ void put(u32 p, u32 b) { R[p & LZ_LRM] = (u8)b; }
-    __device__ __forceinline__ u32 get(u32 p) const { return R[p & LZ_LRM]; }
+    u32 tw;      // the ring dword holding output byte op (its bytes below op & 3 are valid)
+    __device__ __forceinline__ void wr32(u32 a, u32 v) { *(lu32*)(R + (a & LZ_LRM)) = v; }
+    __device__ __forceinline__ u32 rd32(u32 a) const { return *(const lu32*)(R + (a & LZ_LRM)); }
     __device__ __forceinline__ void store_piece(u32 a) {
         if (a >= lim) return;
         const lu8* p = R + (a & LZ_LRM);
@@ -787,15 +788,74 @@ struct LaneRing {
         flush(op);
         for (u32 i = fl; i < op && i < lim; i++) dst[i] = R[i & LZ_LRM];
     }
-    // byte p of the output (p < op, p < lim): LDS when the ring still holds it
-    // (op - p < LZ_LRB), else HBM
-    __device__ __forceinline__ u32 src_byte(u32 p, u32 op) const {
-        return op - p < LZ_LRB ? (u32)R[p & LZ_LRM] : (u32)dst[p];
+    // append the first k (1..16) bytes of v at op: up to five dword writes
+    // (v_alignbyte merges), the dword holding the new op is kept in tw
+    __device__ __forceinline__ void append16(u32& op, const u32x4& v, u32 k) {
+        const u32 sh = op & 3, a = op & ~3u, t = 4 - sh;
+        const u32 m = sh ? (0xFFFFFFFFu >> (8 * t)) : 0u;
+        u32 d[5];
+        d[0] = (tw & m) | (v.x << (8 * sh));
+        d[1] = sh ? __builtin_amdgcn_alignbyte(v.y, v.x, t) : v.y;
+        d[2] = sh ? __builtin_amdgcn_alignbyte(v.z, v.y, t) : v.z;
+        d[3] = sh ? __builtin_amdgcn_alignbyte(v.w, v.z, t) : v.w;
+        d[4] = sh ? (v.w >> (8 * t)) : 0u;
+        const u32 e = sh + k;
+#pragma unroll
+        for (u32 j = 0; j < 5; j++)
+            if (4 * j < e) wr32(a + 4 * j, d[j]);
+        const u32 q = e >> 2;
+        tw = q == 0 ? d[0] : q == 1 ? d[1] : q == 2 ? d[2] : q == 3 ? d[3] : d[4];
+        op += k;
+    }
+    // the 16 ring bytes at p (p < op; bytes at >= op are stale)
+    __device__ __forceinline__ u32x4 rd16(u32 p) const {
+        const u32 b = p & ~3u, sh = p & 3;
+        const u32 w0 = rd32(b), w1 = rd32(b + 4), w2 = rd32(b + 8), w3 = rd32(b + 12), w4 = rd32(b + 16);
+        if (!sh) return u32x4{w0, w1, w2, w3};
+        return u32x4{__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
+                     __builtin_amdgcn_alignbyte(w3, w2, sh), __builtin_amdgcn_alignbyte(w4, w3, sh)};
     }
 };
 
+// v with its first `off` (1..15) bytes repeated: byte j = byte (j mod off)
+__device__ __forceinline__ u32x4 lz_pattern(u32x4 v, u32 off) {
+    u64 lo = ((u64)v.y << 32) | v.x, hi = ((u64)v.w << 32) | v.z;
+    if (off < 8) { lo &= (1ull << (8 * off)) - 1; hi = 0; }
+    else hi &= (1ull << (8 * (off - 8))) - 1;  // off = 8: keeps nothing of hi
+    for (u32 L = off; L < 16; L *= 2) {  // double the valid prefix
+        u64 slo, shi;
+        if (L >= 8) { shi = lo << (8 * (L - 8)); slo = 0; }
+        else { shi = (hi << (8 * L)) | (lo >> (64 - 8 * L)); slo = lo << (8 * L); }
+        lo |= slo;
+        hi |= shi;
+    }
+    return u32x4{(u32)lo, (u32)(lo >> 32), (u32)hi, (u32)(hi >> 32)};
+}
+
+// the 16 output bytes at op - off (off >= 1; periodic when off < 16): from the
+// ring when the source is near (its slots are not yet reused: off < LZ_LRB - 4,
+// the 4 covering the stale tail of the last written dword), else from HBM
+__device__ __forceinline__ u32x4 lz_src16(const LaneRing& O, u32 op, u32 off) {
+    const u32 p = op - off;
+    if (off < LZ_LRB - 4) {
+        const u32x4 v = O.rd16(p);
+        return off < 16 ? lz_pattern(v, off) : v;
+    }
+    if (p + 16 <= O.lim) return *(const gu32x4_ua*)(O.dst + p);
+    u64 lo = 0, hi = 0;  // the block's last bytes: nothing at >= lim is stored (or needed)
+    for (u32 k = 0; k < 16; k++) {
+        const u64 b = p + k < O.lim ? (u64)O.dst[p + k] : 0ull;
+        if (k < 8) lo |= b << (8 * k); else hi |= b << (8 * (k - 8));
+    }
+    return u32x4{(u32)lo, (u32)(lo >> 32), (u32)hi, (u32)(hi >> 32)};
+}
+
 // LZ4_decompress_safe of one block (the checks of lz4_block above, in its order),
-// positions block-relative, low = 0 (independent blocks).
+// positions block-relative, low = 0 (independent blocks).  Every sequence takes
+// the same short path on all lanes — literals as one 16-byte vector, the match
+// as one 16-byte vector (ring, HBM or a periodic pattern), each appended with
+// dword writes — so a wave's cost per step is one sequence, not the union of
+// per-byte loops of its lanes; longer literals/matches loop in 16-byte pieces.
 __device__ int lz4_lane_block(const u8* __restrict__ src, u32 iend, u64 avail, LaneRing& O, u32 cap,
                               u32* out_n) {
     u32 ip = 0, op = 0;
@@ -816,12 +876,13 @@ __device__ int lz4_lane_block(const u8* __restrict__ src, u32 iend, u64 avail, L
         const u64 cpy = (u64)op + lit;
         const bool last = cpy + 12 > cap || (i64)ip + lit > (i64)iend - 8;
         if (last && ((u64)ip + lit != iend || cpy > cap)) return ZCG_ERR_INVALID_DATA;
-        // literals, in pieces of <= LZ_LPC bytes (a flush after each keeps op - fl < LZ_LRB)
-        for (u32 j0 = 0; j0 < lit; j0 += LZ_LPC) {
-            const u32 m = lit - j0 < LZ_LPC ? lit - j0 : LZ_LPC;
-            for (u32 j = 0; j < m; j++) O.put(op + j, in.byte(ip + j));
-            op += m;
-            ip += m;
+        // literals: 16 bytes at a time, from the window when they lie in it
+        for (u32 j0 = 0; j0 < lit; j0 += 16) {
+            const u32 d = ip - in.wb;
+            const u32x4 v = (d + lit <= 16) ? win_shift(in.w, d) : win_load(src, ip, avail);
+            const u32 k = lit - j0 < 16 ? lit - j0 : 16;
+            O.append16(op, v, k);
+            ip += k;
             O.flush(op);
         }
         if (last) break;
@@ -839,31 +900,15 @@ __device__ int lz4_lane_block(const u8* __restrict__ src, u32 iend, u64 avail, L
         ml += 4;
         if (op < off) return ZCG_ERR_INVALID_DATA;
         if ((u64)op + ml + 5 > cap) return ZCG_ERR_INVALID_DATA;
-        if (off == 0) {  // lz4 1.9.3: offset 0 decodes to zeros
-            for (u32 j0 = 0; j0 < ml; j0 += LZ_LPC) {
-                const u32 m = ml - j0 < LZ_LPC ? ml - j0 : LZ_LPC;
-                for (u32 j = 0; j < m; j++) O.put(op + j, 0);
-                op += m;
-                O.flush(op);
-            }
-        } else if (off >= LZ_LRB && ml <= 16 && ml <= LZ_LPC && op - off + 16 <= O.lim) {
-            // a far source: one 16-byte load from the block's HBM output
-            const u32x4 v = *(const gu32x4_ua*)(O.dst + op - off);
-            for (u32 j = 0; j < ml; j++) O.put(op + j, win_byte(v, j));
-            op += ml;
+        if (ip - in.wb > 8) in.at(ip);  // the next sequence's window, in flight during the copy
+        for (u32 r = ml; r > 0;) {
+            const u32 k = r < 16 ? r : 16;
+            // lz4 1.9.3 decodes offset 0 to zeros
+            const u32x4 v = off ? lz_src16(O, op, off) : u32x4{0u, 0u, 0u, 0u};
+            O.append16(op, v, k);
             O.flush(op);
-        } else {
-            for (u32 j0 = 0; j0 < ml; j0 += LZ_LPC) {
-                const u32 m = ml - j0 < LZ_LPC ? ml - j0 : LZ_LPC;
-                for (u32 j = 0; j < m; j++) {
-                    const u32 p = op + j - off;
-                    O.put(op + j, p < O.lim ? O.src_byte(p, op + j) : 0u);
-                }
-                op += m;
-                O.flush(op);
-            }
+            r -= k;
         }
-        if (ip - in.wb > 8) in.at(ip);  // the next sequence's window, in flight early
     }
     *out_n = op;
     return ZCG_OK;
@@ -904,7 +949,7 @@ __global__ __launch_bounds__(LZ_LWG, ZCG_LZ4_WPE) void lz4_lanes_kernel(const zc
             for (; i < m; i++) dst[i] = s[i];
             got = cs;
         } else {
-            LaneRing O{(lu8*)(rings + threadIdx.x * LZ_LRB), dst, lb, 0};
+            LaneRing O{(lu8*)(rings + threadIdx.x * LZ_LRB), dst, lb, 0, 0};
             st = lz4_lane_block(s, cs, ch.src_len - so, O, ci.bmax, &got);
             if (st == ZCG_OK) O.finish(got);
         }
