@@ -748,6 +748,15 @@ __global__ __launch_bounds__(256) void lz4_blocks_kernel(const zcg_chunk* __rest
 #ifndef ZCG_LZ4_LRB
 #define ZCG_LZ4_LRB 128
 #endif
+#ifndef ZCG_LZ4_BUF
+#define ZCG_LZ4_BUF 1
+#endif
+#ifndef ZCG_LZ4_NT_FAR
+#define ZCG_LZ4_NT_FAR 0
+#endif
+#ifndef ZCG_LZ4_NT_ST
+#define ZCG_LZ4_NT_ST 0
+#endif
 #ifndef ZCG_LZ4_LDS_PAD
 #define ZCG_LZ4_LDS_PAD 0
 #endif
@@ -774,7 +783,11 @@ struct LaneRing {
 #pragma unroll
             for (u32 i = 0; i < LZ_LPC / 16; i++) {
                 const u32x4 v = *(const __attribute__((address_space(3))) u32x4*)(p + 16 * i);
+#if ZCG_LZ4_NT_ST
+                __builtin_nontemporal_store(v, (u32x4 __attribute__((address_space(1)))*)(dst + a + 16 * i));
+#else
                 *(gu32x4_ua*)(dst + a + 16 * i) = v;
+#endif
             }
         } else {
             for (u32 i = 0; a + i < lim; i++) dst[a + i] = p[i];
@@ -841,7 +854,15 @@ __device__ __forceinline__ u32x4 lz_src16(const LaneRing& O, u32 op, u32 off) {
         const u32x4 v = O.rd16(p);
         return off < 16 ? lz_pattern(v, off) : v;
     }
-    if (p + 16 <= O.lim) return *(const gu32x4_ua*)(O.dst + p);
+    if (p + 16 <= O.lim) {
+#if ZCG_LZ4_NT_FAR
+        const gu32* q = (const gu32*)(O.dst + p);  // (dword loads: p is any byte offset)
+        return u32x4{__builtin_nontemporal_load(q), __builtin_nontemporal_load(q + 1),
+                     __builtin_nontemporal_load(q + 2), __builtin_nontemporal_load(q + 3)};
+#else
+        return *(const gu32x4_ua*)(O.dst + p);
+#endif
+    }
     u64 lo = 0, hi = 0;  // the block's last bytes: nothing at >= lim is stored (or needed)
     for (u32 k = 0; k < 16; k++) {
         const u64 b = p + k < O.lim ? (u64)O.dst[p + k] : 0ull;
@@ -850,17 +871,73 @@ __device__ __forceinline__ u32x4 lz_src16(const LaneRing& O, u32 op, u32 off) {
     return u32x4{(u32)lo, (u32)(lo >> 32), (u32)hi, (u32)(hi >> 32)};
 }
 
+// A lane's input through a 64-byte register buffer (four 16-byte loads from a
+// 16-byte aligned address, i.e. one or two whole lines per 48-64 bytes used)
+// and a 16-byte working window cut from it with v_alignbyte.  With every lane
+// streaming its own block, lines do not survive in L2 between the sparse
+// 16-byte reloads of a plain window (each reload fetched a whole line).
+__device__ __forceinline__ u32 sel4(u32 s, u32 a0, u32 a1, u32 a2, u32 a3) {
+    return s == 0 ? a0 : s == 1 ? a1 : s == 2 ? a2 : a3;
+}
+struct LzBuf {
+    const u8* src;
+    u64 avail;
+    u32x4 b0, b1, b2, b3;  // bytes [bb, bb + 64), bb 16-byte aligned
+    u32 bb;
+    u32x4 w;  // bytes [wb, wb + 16)
+    u32 wb;
+    __device__ __forceinline__ void load_buf(u32 q) {
+        bb = q & ~15u;
+        b0 = win_load(src, (u64)bb, avail);
+        b1 = win_load(src, (u64)bb + 16, avail);
+        b2 = win_load(src, (u64)bb + 32, avail);
+        b3 = win_load(src, (u64)bb + 48, avail);
+    }
+    __device__ __forceinline__ void at(u32 q) {
+        if (q - bb > 48) load_buf(q);
+        const u32 d = q - bb;  // 0..48
+        const u32 qd = d >> 4;
+        // (the register barrier keeps the selects on values: folded into a
+        // select of member addresses they would send the buffer to scratch)
+        u32x4 c0 = b0, c1 = b1, c2 = b2, c3 = b3;
+        asm volatile("" : "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3));
+        const u32x4 lo = qd == 0 ? c0 : qd == 1 ? c1 : qd == 2 ? c2 : c3;
+        const u32x4 hi = qd == 0 ? c1 : qd == 1 ? c2 : c3;  // (unused when d == 48)
+        const u32 s4 = (d >> 2) & 3, sb = d & 3;
+        // words s4 .. s4+4 of lo:hi
+        const u32 y0 = sel4(s4, lo.x, lo.y, lo.z, lo.w), y1 = sel4(s4, lo.y, lo.z, lo.w, hi.x);
+        const u32 y2 = sel4(s4, lo.z, lo.w, hi.x, hi.y), y3 = sel4(s4, lo.w, hi.x, hi.y, hi.z);
+        const u32 y4 = sel4(s4, hi.x, hi.y, hi.z, hi.w);
+        w = sb ? u32x4{__builtin_amdgcn_alignbyte(y1, y0, sb), __builtin_amdgcn_alignbyte(y2, y1, sb),
+                       __builtin_amdgcn_alignbyte(y3, y2, sb), __builtin_amdgcn_alignbyte(y4, y3, sb)}
+               : u32x4{y0, y1, y2, y3};
+        wb = q;
+    }
+    __device__ __forceinline__ u32 byte(u32 q) {
+        u32 d = q - wb;
+        if (d >= 16) { at(q); d = 0; }
+        return win_byte(w, d);
+    }
+};
+
 // LZ4_decompress_safe of one block (the checks of lz4_block above, in its order),
 // positions block-relative, low = 0 (independent blocks).  Every sequence takes
 // the same short path on all lanes — literals as one 16-byte vector, the match
 // as one 16-byte vector (ring, HBM or a periodic pattern), each appended with
 // dword writes — so a wave's cost per step is one sequence, not the union of
 // per-byte loops of its lanes; longer literals/matches loop in 16-byte pieces.
-__device__ int lz4_lane_block(const u8* __restrict__ src, u32 iend, u64 avail, LaneRing& O, u32 cap,
+__device__ __forceinline__ int lz4_lane_block(const u8* __restrict__ src, u32 iend, u64 avail, LaneRing& O, u32 cap,
                               u32* out_n) {
     u32 ip = 0, op = 0;
+#if ZCG_LZ4_BUF
+    LzBuf in;
+    in.src = src; in.avail = avail;
+    in.load_buf(0);
+    in.at(0);
+#else
     LzWin in{src, avail, u32x4{0, 0, 0, 0}, 0};
     in.at(0);
+#endif
     for (;;) {
         if (ip >= iend) return ZCG_ERR_INVALID_DATA;
         const u32 token = in.byte(ip++);
