@@ -81,9 +81,11 @@ enum zcg_status {
 /* Xz decode keeps 32 KiB of history in LDS instead of 4 KiB: far matches
  * stop re-reading the output from L2/HBM, at 3 instead of 8 chunks per CU. */
 #define ZCG_FLAG_XZ_RING_32K 0x400u
-/* LZ4 decode with one wave per block (speculative parse, byte-parallel
- * resolve) instead of one lane per block; the two are bit-identical. */
+/* LZ4 block decoder choice (bit-identical): one wave per block (speculative
+ * parse, byte-parallel resolve) or one lane per block; by default the batch
+ * size picks (lanes for large batches). */
 #define ZCG_FLAG_LZ4_WAVE_PER_BLOCK 0x800u
+#define ZCG_FLAG_LZ4_LANE_PER_BLOCK 0x1000u
 
 /* CompressionType + its configuration (camelCase JSON keys in the reference). */
 typedef struct zcg_compression {

@@ -1,7 +1,7 @@
-"""ZCG_FLAG_LZ4_WAVE_PER_BLOCK: the two LZ4 block decoders (one lane per block,
-the default; one wave per block) must give the same bytes and statuses on
-valid, truncated and corrupted frames (lz.rs:81-83 -> LZ4F_decompress), and
-both must match the oracle."""
+"""ZCG_FLAG_LZ4_{WAVE,LANE}_PER_BLOCK: the two LZ4 block decoders (one lane per
+block, picked for large batches; one wave per block, picked for small ones)
+must give the same bytes and statuses on valid, truncated and corrupted
+frames (lz.rs:81-83 -> LZ4F_decompress), and both must match the oracle."""
 import os
 import sys
 
@@ -17,11 +17,12 @@ import zref  # noqa: E402  (oracle: checker only)
 pytestmark = pytest.mark.gpu
 
 FLAG_WAVE = 0x800
+FLAG_LANE = 0x1000
 
 
-def _decode(streams, D, flags):
+def _decode(streams, D, flags, dt="u1"):
     import torch
-    meta = ArrayMetadata.new([D * len(streams)], [D], "u1", Lz4(65536))
+    meta = ArrayMetadata.new([D * len(streams)], [D], dt, Lz4(65536))
     packed = PackedStreams(streams, D, "cuda:0")
     BatchCodec(0).decode(meta, packed, flags=flags)
     torch.cuda.synchronize()
@@ -58,7 +59,7 @@ def test_lane_and_wave_decoders_agree():
         b[int(rng.integers(7, len(b)))] ^= int(rng.integers(1, 256))
         extra.append(bytes(b))
     allst = streams + extra
-    s0, o0 = _decode(allst, D, 0)
+    s0, o0 = _decode(allst, D, FLAG_LANE)
     s1, o1 = _decode(allst, D, FLAG_WAVE)
     assert s0.tolist() == s1.tolist()
     for i, p in enumerate(pays):
@@ -68,3 +69,28 @@ def test_lane_and_wave_decoders_agree():
         assert ost == s0[i], i
         if ost == 0:
             assert bytes(o0[i]) == ref and bytes(o1[i]) == ref
+
+
+FRAMES = {"reference": {}, "linked": dict(linked=True), "block_checksum": dict(block_checksum=True),
+          "content_size": dict(content_size=True), "bd256k": dict(block_size_id=5),
+          "bd4m": dict(block_size_id=7), "small_blocks": dict(auto_flush=True, feed=10000)}
+
+
+@pytest.mark.parametrize("frame", list(FRAMES))
+def test_lane_decoder_frame_variants(frame):
+    """Every frame layout the reference decoder accepts, through the lane
+    decoder, at full length and truncating read_exact lengths."""
+    pays = _payloads()
+    streams = []
+    for p in pays:
+        if frame == "reference":
+            streams.append(zref.encode(zref.LZ4, 65536, np.frombuffer(p, np.uint8))[1])
+        else:
+            streams.append(zref.lz4_frame_custom(p, **FRAMES[frame]))
+    for D in (1 << 20, (1 << 20) - 1000, 65536 * 3, 65536 * 3 + 7):
+        st, out = _decode(streams, D, FLAG_LANE)
+        for i, s in enumerate(streams):
+            ost, ref = zref.decode(zref.LZ4, s, D, 1)
+            assert ost == st[i], (frame, D, i)
+            if ost == 0:
+                assert bytes(out[i]) == ref, (frame, D, i)

@@ -284,10 +284,12 @@ def test_lz4_errors():
     check("lz4", bytes(bad), "u1", len(payload))
 
 
-def test_lz4_corruption_sweep():
+@pytest.mark.parametrize("lz4_flags", [0, 0x1000], ids=["auto", "lane_per_block"])
+def test_lz4_corruption_sweep(lz4_flags):
     """Byte corruptions and truncations of LZ4 frames everywhere (block
     headers, tokens, length bytes, offsets, literals, end mark, checksums),
-    batched, each classified and decoded like LZ4F_decompress (oracle)."""
+    batched, each classified and decoded like LZ4F_decompress (oracle); both
+    block decoders (small batches pick one wave per block by default)."""
     rng = np.random.default_rng(31)
     payloads = [rw(100000, seed=3).tobytes(), DATASETS["text_like"]()[:150000],
                 np.random.default_rng(8).integers(0, 4, 120000, dtype=np.uint8).tobytes()]
@@ -306,7 +308,7 @@ def test_lz4_corruption_sweep():
                     q = int(rng.integers(0, len(b)))
                     b[q] = int(rng.integers(0, 256))
                 streams.append(bytes(b))
-            check_many("lz4", streams, "u1", D)
+            check_many("lz4", streams, "u1", D, flags=lz4_flags)
 
 
 @pytest.mark.parametrize("dt", ["<i2", ">i2", ">f8", "bool", "u1"])

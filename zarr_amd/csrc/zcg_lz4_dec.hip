@@ -751,6 +751,9 @@ __global__ __launch_bounds__(256) void lz4_blocks_kernel(const zcg_chunk* __rest
 #ifndef ZCG_LZ4_BUF
 #define ZCG_LZ4_BUF 1
 #endif
+#ifndef ZCG_LZ4_LANE_MIN_BLOCKS
+#define ZCG_LZ4_LANE_MIN_BLOCKS 196608  // ~12 288 chunks of 16 blocks (measured crossover 8-16 K chunks)
+#endif
 #ifndef ZCG_LZ4_NT_FAR
 #define ZCG_LZ4_NT_FAR 0
 #endif
@@ -1110,7 +1113,12 @@ hipError_t launch_lz4_decode(const zcg_array* a, const zcg_chunk* d_chunks, uint
     const u64 waves = (u64)n * S;
     if ((waves + 3) / 4 > 0x7FFFFFFFull) return hipErrorInvalidValue;
     if (D > 0) {
-        if (a->compression.flags & ZCG_FLAG_LZ4_WAVE_PER_BLOCK)
+        // one lane per block needs ~16 waves per CU of blocks to hide its
+        // latency; smaller batches run one wave per block
+        const u32 fl = a->compression.flags;
+        const bool wave = (fl & ZCG_FLAG_LZ4_WAVE_PER_BLOCK) ||
+                          (!(fl & ZCG_FLAG_LZ4_LANE_PER_BLOCK) && waves < ZCG_LZ4_LANE_MIN_BLOCKS);
+        if (wave)
             hipLaunchKernelGGL(lz4_blocks_kernel, dim3((u32)((waves + 3) / 4)), dim3(256), 0, s, d_chunks, n, D,
                                (u32)S, a->compression.flags, (const Lz4ChunkInfo*)info, slots);
         else
