@@ -827,16 +827,19 @@ __global__ __launch_bounds__(PI_NL, ZCG_INF_WPE) void inflate_par_kernel(const z
                 if (mine) {
                     // take tokens while they fit below cap (at N: until cap is reached);
                     // the first PF come from registers
-                    u32 acc = base, a = my_s;
+                    // sb: stream bits of tokens [0, a), summed as they are taken
+                    u32 acc = base, a = my_s, sb = 0;
                     bool go = true;
 #pragma unroll
                     for (u32 u = 0; u < PF; u++) {
+                        if (u < my_s) sb += tok_bits(pre[u]);
                         if (go && u >= my_s && u < vend) {  // a == u here
                             const u32 len = tok_len(pre[u]);
                             if (cap == room ? acc >= cap : acc + len > cap) go = false;
-                            else { acc += len; a++; }
+                            else { acc += len; sb += tok_bits(pre[u]); a++; }
                         }
                     }
+                    for (u32 j = PF; j < my_s; j++) sb += tok_bits(tok_at(gp, tid, j));  // rare
                     while (go && a < vend) {
                         u32 tk8[8];
 #pragma unroll
@@ -846,21 +849,13 @@ __global__ __launch_bounds__(PI_NL, ZCG_INF_WPE) void inflate_par_kernel(const z
                             if (go && a < vend) {  // while go holds, a == (a at the load) + u
                                 const u32 len = tok_len(tk8[u]);
                                 if (cap == room ? acc >= cap : acc + len > cap) go = false;
-                                else { acc += len; a++; }
+                                else { acc += len; sb += tok_bits(tk8[u]); a++; }
                             }
                         }
                     }
                     // bit position of the first token not taken: the segment start
                     // plus the stored bit lengths of tokens [0, a), or the lane's end
-                    u32 pos = q;
-                    if (a < nt) {
-                        u32 sb = 0;
-#pragma unroll
-                        for (u32 u = 0; u < PF; u++)
-                            if (u < a) sb += tok_bits(pre[u]);
-                        for (u32 j = PF; j < a; j++) sb += tok_bits(tok_at(gp, tid, j));
-                        pos = R0 + tid * PI_SEG + sb;
-                    }
+                    const u32 pos = a < nt ? R0 + tid * PI_SEG + sb : q;
                     L.ctl[7] = (cap == room && acc == cap) ? 1u : 0u;
                     L.ctl[8] = acc < cap ? acc : cap;  // a token may cross N: clip there
                     L.ctl[9] = tid;
@@ -931,7 +926,11 @@ __global__ __launch_bounds__(PI_NL, ZCG_INF_WPE) void inflate_par_kernel(const z
             // before the match start.  Thread t expands the contiguous byte
             // range [x0, x1), carrying in the match that covers x0.
             {
-                const u32 ch = (emitted + PI_NL - 1) / PI_NL;
+                // range length ≡ 2 (mod 4) entries: an odd dword stride between
+                // threads, so a wave's reads spread over all banks (a full 16 KiB
+                // stage gives 64 entries = 32 dwords: every thread in one bank)
+                const u32 c0 = (emitted + PI_NL - 1) / PI_NL;
+                const u32 ch = c0 + ((2u - c0) & 3u);
                 const u32 x0 = tid * ch;
                 const u32 x1 = (x0 + ch < emitted) ? x0 + ch : emitted;
                 u32 mo = 0, md = 0, mj = 0;  // current match: start, distance, k mod d
