@@ -115,10 +115,16 @@ class DefaultChunk:
     @staticmethod
     def _decode_into(buffer, meta, out: np.ndarray, device: int, flags: int) -> None:
         ctx = _native.context(device)
-        src = bytes(buffer) if not isinstance(buffer, (bytes, bytearray)) else buffer
+        # the stream is passed in place (zcg_read_chunk only reads it): no copy
+        # for bytes / bytearray / contiguous memoryviews
+        try:
+            src = np.frombuffer(buffer, dtype=np.uint8)
+        except (TypeError, ValueError, BufferError):
+            src = np.frombuffer(bytes(buffer), dtype=np.uint8)
+        if src.size == 0:
+            src = np.zeros(1, np.uint8)[:0]
         arr = abi_array(meta, flags)
-        sbuf = ctypes.create_string_buffer(bytes(src), max(len(src), 1))
-        st = ctx.lib.zcg_read_chunk(ctx.handle, ctypes.byref(arr), ctypes.addressof(sbuf), len(src),
+        st = ctx.lib.zcg_read_chunk(ctx.handle, ctypes.byref(arr), src.ctypes.data, src.size,
                                     out.ctypes.data if out.size else None)
         _raise_status(st, ctx, "read_chunk")
 
