@@ -2,7 +2,7 @@
 """Time the GPU encoders per data distribution (kernel time via HIP events),
 with the CPU reference library's ratio on the same data for comparison.
     python tools/enc_stats.py [n_chunks] [lz4|gzip|xz|bzip2]"""
-import os, sys, json, zlib, bz2, lzma
+import os, sys, json, zlib, bz2, lzma, hashlib
 import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -37,6 +37,10 @@ for name, g in gens.items():
         ref = round(4 * D / sum(len(bz2.compress(pool[i].tobytes(), 9)) for i in range(4)), 3)
     elif codec == "xz":
         ref = round(4 * D / sum(len(lzma.compress(pool[i].tobytes(), preset=6)) for i in range(4)), 3)
-    print(json.dumps({"codec": codec, "data": name, "ms": round(ms, 2), "GiBps": round(n * D / ms / 1e-3 / 2**30, 2),
+    olc = ol.cpu().numpy()
+    dcpu = dst.view(n, -1)[:, :int(olc.max())].cpu().numpy() if n else None
+    h = hashlib.sha1()
+    for i in range(n): h.update(dcpu[i, :int(olc[i])].tobytes())
+    print(json.dumps({"codec": codec, "data": name, "sha1": h.hexdigest()[:16], "ms": round(ms, 2), "GiBps": round(n * D / ms / 1e-3 / 2**30, 2),
                       "ratio": round(n * D / float(ol.sum().item()), 3), "ref_ratio": ref,
                       "ok": bool((st == 0).all().item())}), flush=True)
