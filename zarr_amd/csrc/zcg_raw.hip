@@ -13,15 +13,18 @@
 namespace zcg {
 
 constexpr int RAW_THREADS = 256;
-constexpr int RAW_VEC_PER_THREAD = 4;
-constexpr u64 RAW_TILE = (u64)RAW_THREADS * RAW_VEC_PER_THREAD * 16;  // 16 KiB
+// one 16-byte vector per thread (4 KiB tiles): measured 2 650 / 2 685 / 2 865
+// GiB/s at 4 / 2 / 1 vectors per thread (1 GiB batch); 128/512-thread
+// workgroups and non-temporal stores are within noise of this
+#ifndef ZCG_RAW_VPT
+#define ZCG_RAW_VPT 1
+#endif
+constexpr int RAW_VEC_PER_THREAD = ZCG_RAW_VPT;
+constexpr u64 RAW_TILE = (u64)RAW_THREADS * RAW_VEC_PER_THREAD * 16;  // 4 KiB
 
-__global__ __launch_bounds__(RAW_THREADS) void raw_kernel(const zcg_chunk* __restrict__ chunks,
-                                                          u32 n, u64 nbytes, u64 tiles_per_chunk,
-                                                          DType t, int encode,
-                                                          i32* __restrict__ status,
-                                                          u64* __restrict__ out_len) {
-    const u64 gtile = blockIdx.x;
+__device__ __forceinline__ void raw_tile(const zcg_chunk* __restrict__ chunks, u32 n, u64 nbytes,
+                                         u64 tiles_per_chunk, DType t, int encode,
+                                         i32* __restrict__ status, u64* __restrict__ out_len, u64 gtile) {
     const u32 c = (u32)(gtile / tiles_per_chunk);
     const u64 tile = gtile - (u64)c * tiles_per_chunk;
     if (c >= n) return;
@@ -68,6 +71,16 @@ __global__ __launch_bounds__(RAW_THREADS) void raw_kernel(const zcg_chunk* __res
     }
 }
 
+// one tile per workgroup; a grid larger than the launch limit strides
+__global__ __launch_bounds__(RAW_THREADS) void raw_kernel(const zcg_chunk* __restrict__ chunks,
+                                                          u32 n, u64 nbytes, u64 tiles_per_chunk,
+                                                          DType t, int encode,
+                                                          i32* __restrict__ status,
+                                                          u64* __restrict__ out_len, u64 ntiles) {
+    for (u64 g = blockIdx.x; g < ntiles; g += gridDim.x)
+        raw_tile(chunks, n, nbytes, tiles_per_chunk, t, encode, status, out_len, g);
+}
+
 hipError_t launch_raw(const zcg_array* a, const zcg_chunk* d_chunks, uint32_t n, int32_t* d_status,
                       uint64_t* d_out_len, int encode, hipStream_t s) {
     const DType t = make_dtype(a->dtype);
@@ -75,8 +88,9 @@ hipError_t launch_raw(const zcg_array* a, const zcg_chunk* d_chunks, uint32_t n,
     const u64 tiles = nbytes ? (nbytes + RAW_TILE - 1) / RAW_TILE : 1;
     const u64 grid = tiles * n;
     if (grid == 0) return hipSuccess;
-    hipLaunchKernelGGL(raw_kernel, dim3((unsigned)grid), dim3(RAW_THREADS), 0, s, d_chunks, n,
-                       nbytes, tiles, t, encode, d_status, d_out_len);
+    const u32 blocks = (u32)(grid < (1ull << 30) ? grid : (1ull << 30));
+    hipLaunchKernelGGL(raw_kernel, dim3(blocks), dim3(RAW_THREADS), 0, s, d_chunks, n,
+                       nbytes, tiles, t, encode, d_status, d_out_len, grid);
     return hipGetLastError();
 }
 
