@@ -28,6 +28,11 @@ namespace zcg {
 namespace {
 
 constexpr u32 RG_T = 256;
+// pieces per lane in flight per work unit (A/B: 1 / 2 / 4 / 8 / 16 -> 1 753 /
+// 2 249 / 2 385 / 1 852 / 1 254 GiB/s of box on the bench leg)
+#ifndef ZCG_RG_U
+#define ZCG_RG_U 4
+#endif
 
 struct Pos {
     u32 x[ZCG_MAX_DIMS];
@@ -160,7 +165,15 @@ __global__ __launch_bounds__(RG_T) void region_rows_kernel(RegionArgs a, u64 nro
     const u32x4 fill16 = {(u32)fv, (u32)(fv >> 32), (u32)fv, (u32)(fv >> 32)};
     const u32 V = a.V, bs0 = a.bs[0], cs0 = a.cs[0], orr0 = a.orr[0];
     const i64 es = a.es;
-    for (u64 row = ru64(wid); row < nrows; row += nwaves) {
+    // work unit = (row, piece of U*64*V elements of it): many short units
+    // keep more loads in flight per CU than one long walk per row
+    constexpr u32 U = ZCG_RG_U;
+    const u32 span = U * 64 * V;
+    const u32 ppr = (bs0 + span - 1) / span;
+    const u64 nunits = nrows * ppr;
+    for (u64 unit = ru64(wid); unit < nunits; unit += nwaves) {
+        const u64 row = unit / ppr;
+        const u32 piece = (u32)(unit - row * ppr);
         // slow-dimension coordinates of this row (scalar)
         u64 e = row, ti = 0, wi = 0;
         i64 drow = 0;
@@ -178,9 +191,9 @@ __global__ __launch_bounds__(RG_T) void region_rows_kernel(RegionArgs a, u64 nro
             drow += (i64)x * a.ostr[k];
         }
         u8* drow_p = out + drow * es;
-        // four pieces per lane in flight: loads first, then stores
-        constexpr u32 U = 4;
-        for (u32 xb = lane * V; xb < bs0; xb += U * 64 * V) {
+        // U pieces per lane in flight: loads first, then stores
+        const u32 xend = (piece + 1) * span;
+        for (u32 xb = piece * span + lane * V; xb < bs0 && xb < xend; xb += span) {
             u32x4 v[U];
             u8* dp[U];
             u32 mode[U];  // 0 skip, 1 load+store, 2 fill, 3 element runs
@@ -231,8 +244,10 @@ hipError_t launch_region(const RegionArgs& a, const void* const* d_table, void* 
     if (a.total == 0) return hipSuccess;
     if (a.bs[0] >= 32u * a.V) {  // long rows: a wave per row
         const u64 nrows = a.total / a.bs[0];
-        const u64 wgs = (nrows + 3) / 4;
-        const u32 grid = (u32)(wgs < 65536 ? wgs : 65536);
+        const u64 span = (u64)ZCG_RG_U * 64 * a.V;
+        const u64 units = nrows * ((a.bs[0] + span - 1) / span);
+        const u64 wgs = (units + 3) / 4;
+        const u32 grid = (u32)(wgs < (1u << 20) ? wgs : (1u << 20));
         hipLaunchKernelGGL(region_rows_kernel, dim3(grid), dim3(RG_T), 0, s, a, nrows, (const u8* const*)d_table,
                            (u8*)d_out);
         return hipGetLastError();
