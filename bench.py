@@ -500,7 +500,9 @@ def host_cpu_info():
     except (OSError, ValueError):
         pass
     aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
-    return {"cpu_model": model, "affinity_cpus": aff, "os_cpu_count": os.cpu_count(), "cgroup_cpu_quota": quota}
+    usable = aff if quota is None else max(1, min(aff, int(-(-quota // 1))))
+    return {"cpu_model": model, "usable_cpus": usable, "affinity_cpus": aff, "os_cpu_count": os.cpu_count(),
+            "cgroup_cpu_quota": quota}
 
 
 def _oracle():
@@ -522,20 +524,43 @@ def _cpu_decode_rate(codec, streams, D, seconds, threads):
         assert (st == 0).all()
         done += len(srcs)
     el = time.perf_counter() - t0
-    return done * D / el / GIB, done, el
+    cbytes = sum(len(s) for s in streams) * (done // max(len(srcs), 1))
+    return done * D / el / GIB, done, el, (cbytes + done * D) / el / 1e9
 
 
 def cpu_leg(codec, streams, D, seconds, threads_all):
     """The oracle (reference C codec libraries, oracle/zref.c) decoding the
-    same pool on host threads: T = all usable CPUs for `seconds`, T = 1 for
-    a third of that — cpu_baseline only."""
-    v, done, el = _cpu_decode_rate(codec, streams, D, seconds, threads_all)
-    v1, done1, el1 = _cpu_decode_rate(codec, streams[:8], D, max(1.0, seconds / 3), 1)
+    same pool on host threads: T = the CPUs this process may use (affinity
+    capped by the cgroup quota) for `seconds`, T = 1 for a third of that —
+    cpu_baseline only.  value = decoded GiB/s; value_cd_gbs = (C + D) GB/s,
+    the roofline's algorithmic bytes."""
+    v, done, el, cd = _cpu_decode_rate(codec, streams, D, seconds, threads_all)
+    v1, done1, el1, cd1 = _cpu_decode_rate(codec, streams[:8], D, max(1.0, seconds / 3), 1)
     info = host_cpu_info()
     return {"value": round(v, 4), "unit": "GiB/s", "cores": threads_all, "kind": "port",
-            "value_t1": round(v1, 4), **info,
+            "value_cd_gbs": round(cd, 3), "value_t1": round(v1, 4), **info,
             "sample": f"{done} decodes of the {len(streams)}-chunk pool (1 MiB each) by {CPU_LIB[codec]} "
                       f"(oracle/zref.c), {threads_all} threads, {el:.1f} s; T=1: {done1} decodes, {el1:.1f} s"}
+
+
+def compact_leg(r):
+    """A per_codec leg as it goes on the bench line (the full record stays in
+    DESIGN.md): value, time, batch, ratio, roofline fraction, PMC traffic as a
+    multiple of the algorithmic bytes, kernel ms, CPU baseline [T=usable, T=1,
+    usable CPUs]."""
+    rf = r.get("roofline", {})
+    out = {"value": r["value"], "unit": r["unit"], "ms": r.get("ms_per_step"),
+           "batch": r.get("batch_per_gpu"), "ratio": r.get("ratio"), "frac": rf.get("frac"),
+           "kernel_ms": rf.get("kernel_ms", r.get("device_ms"))}
+    tr, ab = rf.get("traffic"), rf.get("algorithmic_bytes_per_launch")
+    if tr and ab:
+        out["traffic_x"] = round(tr / ab, 2)
+    if "ref_ratio" in r:
+        out["ref_ratio"] = r["ref_ratio"]
+    cb = r.get("cpu_baseline")
+    if cb:
+        out["cpu"] = [cb["value"], cb["value_t1"], cb["cores"]]
+    return out
 
 
 def cpu_encode_leg(codec, vals, seconds, threads_all):
@@ -594,7 +619,7 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=dev)
 
-    threads_all = host_cpu_info()["affinity_cpus"]
+    threads_all = host_cpu_info()["usable_cpus"]
     pool_threads = max(1, min(16, threads_all))  # input synthesis only
     cfg = dict(LEG[args.codec])
     if args.global_batch:
@@ -631,14 +656,15 @@ def main():
                                    lc["pool"], rank, world, dev, pool_threads)
             if rank == 0 and world == 1 and not args.no_cpu_baseline and c != "raw":
                 r["cpu_baseline"] = cpu_leg(c, s_c, r["chunk_bytes"], 3.0, threads_all)
-            per[c] = r
+            per[c] = compact_leg(r)
             del s_c
         cs = 0.0 if args.no_cpu_baseline else 3.0
         for c, (nb, st) in ENCODE_LEG.items():  # gzip = C5
             if "encode" in legs or f"{c}_encode" in legs:
-                per[f"{c}_encode"] = encode_leg(c, nb, st, 1, 64, rank, world, dev, cs, threads_all)
+                per[f"{c}_encode"] = compact_leg(encode_leg(c, nb, st, 1, 64, rank, world, dev, cs,
+                                                            threads_all))
         if "region" in legs:
-            per["region"] = region_leg(max(3, args.steps), dev)
+            per["region"] = compact_leg(region_leg(max(3, args.steps), dev))
         result["per_codec"] = per
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

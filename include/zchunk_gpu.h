@@ -86,6 +86,10 @@ enum zcg_status {
  * size picks (lanes for large batches). */
 #define ZCG_FLAG_LZ4_WAVE_PER_BLOCK 0x800u
 #define ZCG_FLAG_LZ4_LANE_PER_BLOCK 0x1000u
+/* Gzip decode with the 256-lane round kernel (fine 256-bit segments, one
+ * workgroup of 4 waves per chunk) instead of the default one-wave-per-chunk
+ * kernel (coarse segments); bit-identical, kept as a differential reference. */
+#define ZCG_FLAG_INFLATE_BLOCK_PAR 0x2000u
 
 /* CompressionType + its configuration (camelCase JSON keys in the reference). */
 typedef struct zcg_compression {
@@ -241,6 +245,21 @@ int zcg_store_read_chunks(zcg_ctx* ctx, const zcg_array* array, uint32_t n, cons
                           void* const* dsts, int32_t* status, uint32_t io_threads);
 int zcg_store_write_chunks(zcg_ctx* ctx, const zcg_array* array, uint32_t n, const char* const* paths,
                            const void* const* elems, int32_t* status, uint32_t io_threads);
+/* Device-resident ends of the same two calls, for callers whose chunks live in
+ * HBM (read_ndarray / write_ndarray, ndarray.rs:195-268,276-385, which call
+ * read_chunk_into / write_chunk per chunk through the same store get()/set()):
+ *  - zcg_store_read_chunks_device decodes each file straight into the caller's
+ *    DEVICE slot d_dsts[i] (N*elem_size bytes); only the statuses come back.
+ *    A slot whose chunk is absent or unreadable is left untouched.
+ *  - zcg_store_write_chunks_device encodes the DEVICE element slots d_elems[i]
+ *    and writes each file as set() does (exclusive flock, then truncate).
+ * `status` is a host array; both calls block until the files are read/written.
+ * Destinations of zcg_store_read_chunks that are page-locked host memory
+ * (hipHostMalloc / hipHostRegister) receive the decoded chunk by a direct D2H. */
+int zcg_store_read_chunks_device(zcg_ctx* ctx, const zcg_array* array, uint32_t n, const char* const* paths,
+                                 void* const* d_dsts, int32_t* status, uint32_t io_threads);
+int zcg_store_write_chunks_device(zcg_ctx* ctx, const zcg_array* array, uint32_t n, const char* const* paths,
+                                  const void* const* d_elems, int32_t* status, uint32_t io_threads);
 
 /* ---- several GPUs in one process -------------------------
  * Chunk i goes to devices[i mod n_devices]; one host thread and one context
@@ -291,6 +310,16 @@ typedef struct zcg_array_meta {
 } zcg_array_meta;
 
 int zcg_array_meta_from_json(const char* json, uint64_t len, zcg_array_meta* out, char* err, uint64_t err_cap);
+
+/* get_chunk_key (storage.rs:109-127): "/data/root/<path>/c<g0><sep><g1>...<sep><g(n-1)>",
+ * with `path` canonicalised as canonicalize_path does (leading and trailing '/'
+ * removed, lib.rs:187-189; an empty path gives "/data/root/c...") and `separator`
+ * = chunk_grid.separator (zcg_array_meta.separator).  Writes at most cap-1 bytes
+ * and a NUL (cap > 0); returns the key's full length, so a caller can size
+ * `out`.  A FilesystemHierarchy file is the store root joined with the key
+ * (filesystem.rs:142-190). */
+uint64_t zcg_chunk_key(const char* path, const char* separator, const uint64_t* grid_position, uint32_t ndim,
+                       char* out, uint64_t cap);
 
 #ifdef __cplusplus
 }

@@ -77,6 +77,7 @@ def test_c_caller_compiles_against_header():
     r = subprocess.run(["make", "-s", "-B", "-C", C_ABI_DIR], capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
     assert os.path.isfile(os.path.join(C_ABI_DIR, "doc_spec_c"))
+    assert os.path.isfile(os.path.join(C_ABI_DIR, "zarrita_c"))
 
 
 @pytest.mark.gpu
@@ -88,3 +89,17 @@ def test_c_caller_doc_spec_roundtrip():
     assert os.path.isfile(exe), "build tests/c_abi first (__graft_entry__.build)"
     r = subprocess.run([exe, "0"], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and "doc_spec_c: ok" in r.stdout, (r.stdout, r.stderr)
+
+
+@pytest.mark.gpu
+def test_c_caller_reads_zarrita_hierarchy():
+    """A plain-C caller opens the reference's zarrita store with no Python in
+    the loop: zcg_array_meta_from_json on meta/root/seq/i2.array.json, the 8
+    chunk keys from zcg_chunk_key, zcg_store_read_chunks (shared flock, GPU
+    decode), compared with arange(120) (tests/zarrita_compat.rs:16-46)."""
+    import subprocess
+    exe = os.path.join(C_ABI_DIR, "zarrita_c")
+    assert os.path.isfile(exe), "build tests/c_abi first (__graft_entry__.build)"
+    store = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "zarrita")
+    r = subprocess.run([exe, store, "0"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "zarrita_c: ok (8 chunks" in r.stdout, (r.stdout, r.stderr)

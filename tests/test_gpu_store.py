@@ -157,3 +157,97 @@ def test_multi_device_round_robin(tmp_path):
     for i in range(40):
         assert rst[i] == 0 and np.array_equal(outs[i], datas[i]), i
     mc.close()
+
+
+# ---- device-resident ends and the region path on the store's semantics --------------
+def test_store_read_device_into_slots(tmp_path):
+    """zcg_store_read_chunks_device: files decoded straight into device slots;
+    absent chunks leave their slot untouched; pinned host destinations take
+    the direct D2H path and agree."""
+    import torch
+    from zarr_amd.storage import store_read_device, store_write_device
+    h = FilesystemHierarchy.open_or_create(str(tmp_path))
+    meta = ArrayMetadata.new([20 * 4096], [4096], ">i4", Gzip(6))
+    h.create_array("d", meta)
+    datas = [_walk(4096, 70 + i, np.int32) for i in range(20)]
+    h.write_chunks("d", meta, [SliceDataChunk([i], d) for i, d in enumerate(datas) if i != 3])
+    paths = [h.chunk_path("d", meta, [i]) for i in range(20)]
+    D = 4096 * 4
+    slots = torch.full((20 * D,), 0xAB, dtype=torch.uint8, device="cuda:0")
+    st = store_read_device(meta, paths, [slots.data_ptr() + i * D for i in range(20)])
+    out = slots.cpu().numpy().reshape(20, D)
+    assert st[3] == _native.ABSENT and (out[3] == 0xAB).all()
+    for i in range(20):
+        if i != 3:
+            assert st[i] == 0 and np.array_equal(out[i].view(np.int32), datas[i]), i
+    arrs, st2 = store_read(meta, paths, np.int32, pinned=True)
+    assert st2[3] == _native.ABSENT
+    for i in range(20):
+        if i != 3:
+            assert st2[i] == 0 and np.array_equal(arrs[i], datas[i]), i
+    # the write direction from device slots: files decode with the reference library
+    wpaths = [str(tmp_path / "w" / f"c{i}") for i in range(20)]
+    wst = store_write_device(meta, wpaths, [slots.data_ptr() + i * D for i in range(20)])
+    assert (wst == 0).all()
+    for i in (0, 7, 19):
+        s = open(wpaths[i], "rb").read()
+        rs, dec = zref.decode(zref.GZIP, s, D, 4, True, False)
+        assert rs == zref.OK and np.frombuffer(dec, "<i4").tolist() == datas[i].tolist()
+
+
+def test_store_read_under_low_descriptor_limit(tmp_path):
+    """More chunk files than RLIMIT_NOFILE: the reader pool holds at most one
+    descriptor per thread (no EMFILE -> 'Other' for small chunks)."""
+    import resource
+    h = FilesystemHierarchy.open_or_create(str(tmp_path))
+    meta = ArrayMetadata.new([1500 * 2048], [2048], "<i2", Lz4(65536))
+    h.create_array("s", meta)
+    datas = [_walk(2048, 9000 + i) for i in range(1500)]
+    h.write_chunks("s", meta, [SliceDataChunk([i], d) for i, d in enumerate(datas)])
+    soft, hard = resource.getrlimit(resource.RLIMIT_NOFILE)
+    resource.setrlimit(resource.RLIMIT_NOFILE, (256, hard))
+    try:
+        got = h.read_chunks("s", meta, [[i] for i in range(1500)], np.int16)
+    finally:
+        resource.setrlimit(resource.RLIMIT_NOFILE, (soft, hard))
+    for i in range(1500):
+        assert np.array_equal(got[i].get_data(), datas[i]), i
+
+
+def test_write_ndarray_takes_the_store_locks(tmp_path):
+    """write_ndarray writes through set(): it waits for a reader's shared lock
+    and does not truncate the chunk before it holds the exclusive lock
+    (filesystem.rs:268-275); read_ndarray waits for a writer's exclusive lock
+    (get(), filesystem.rs:201-210)."""
+    from zarr_amd.region import BoundingBox, read_ndarray, write_ndarray
+    h = FilesystemHierarchy.open_or_create(str(tmp_path))
+    meta = ArrayMetadata.new([64, 48], [16, 16], "<i2", Gzip(6))
+    h.create_array("r", meta)
+    base = (np.arange(64 * 48) % 3000).astype(np.int16).reshape(64, 48)
+    write_ndarray(h, "r", meta, [0, 0], base)
+    p = h.chunk_path("r", meta, [1, 1])
+    before = open(p, "rb").read()
+    patch = np.full((20, 20), -7, np.int16)
+    res = {}
+    with open(p, "rb") as f:
+        fcntl.flock(f, fcntl.LOCK_SH)  # a reader holds chunk (1, 1)
+        t = threading.Thread(target=lambda: res.setdefault("w", write_ndarray(h, "r", meta, [10, 10], patch)))
+        t.start()
+        time.sleep(1.0)
+        assert t.is_alive(), "write_ndarray did not wait for the shared lock"
+        assert open(p, "rb").read() == before  # not truncated before the lock
+        fcntl.flock(f, fcntl.LOCK_UN)
+    t.join(120)
+    assert not t.is_alive()
+    want = base.copy()
+    want[10:30, 10:30] = -7
+    with open(p, "rb+") as f:
+        fcntl.flock(f, fcntl.LOCK_EX)  # a writer holds chunk (1, 1)
+        t = threading.Thread(target=lambda: res.setdefault(
+            "r", read_ndarray(h, "r", meta, BoundingBox([0, 0], [64, 48]), np.int16)))
+        t.start()
+        time.sleep(1.0)
+        assert t.is_alive(), "read_ndarray did not wait for the exclusive lock"
+        fcntl.flock(f, fcntl.LOCK_UN)
+    t.join(120)
+    assert np.array_equal(res["r"], want)

@@ -171,3 +171,19 @@ def test_unicode_and_escapes():
     st, m, err = native(json.dumps(d))
     assert st == _native.OK, err
     assert m.separator == b"."
+
+
+def test_chunk_key_matches_get_chunk_key():
+    """zcg_chunk_key is storage.rs:109-127 (with canonicalize_path, lib.rs:187-189),
+    including the reference's doctest (storage.rs:86-108)."""
+    from zarr_amd.storage import chunk_key_native, get_chunk_key
+    assert chunk_key_native("/foo/baz", "/", []) == "/data/root/foo/baz/c"
+    assert chunk_key_native("foo/baz", "/", [1, 2, 3]) == "/data/root/foo/baz/c1/2/3"
+    assert chunk_key_native("", ".", [0, 10]) == "/data/root/c0.10"
+    assert chunk_key_native("///", "/", [7]) == "/data/root/c7"
+    for path in ("/seq/i2", "a/b/", "//x//", "", "/"):
+        for sep in ("/", ".", "--"):
+            for grid in ([], [0], [3, 4], [2 ** 40, 0, 5, 1]):
+                meta = ArrayMetadata.new([1] * max(len(grid), 1), [1] * max(len(grid), 1), "<i2", Raw())
+                meta.separator = sep
+                assert chunk_key_native(path, sep, grid) == get_chunk_key(path, meta, grid), (path, sep, grid)

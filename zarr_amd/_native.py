@@ -21,6 +21,8 @@ FLAG_VERIFY_GZIP_CRC = 0x1
 FLAG_VERIFY_LZ4_CONTENT_CHECKSUM = 0x2
 FLAG_SKIP_LZ4_BLOCK_CHECKSUM = 0x4
 FLAG_SERIAL_INFLATE = 0x100
+FLAG_DEBUG_COUNTERS = 0x200
+FLAG_INFLATE_BLOCK_PAR = 0x2000
 
 STATUS_NAMES = {OK: "Ok", UNEXPECTED_EOF: "UnexpectedEof", INVALID_DATA: "InvalidData",
                 INVALID_INPUT: "InvalidInput", UNSUPPORTED: "Unsupported",
@@ -35,7 +37,8 @@ EXPORTED_SYMBOLS = (
     "zcg_store_read_chunks", "zcg_store_write_chunks",
     "zcg_multi_create", "zcg_multi_destroy", "zcg_multi_last_error", "zcg_multi_device_count",
     "zcg_multi_read_chunks_host", "zcg_multi_store_read_chunks", "zcg_multi_store_write_chunks",
-    "zcg_array_meta_from_json",
+    "zcg_array_meta_from_json", "zcg_chunk_key",
+    "zcg_store_read_chunks_device", "zcg_store_write_chunks_device",
 )
 
 
@@ -161,6 +164,12 @@ def load_library(path: str = LIB_PATH):
         L.zcg_multi_store_write_chunks.restype = ctypes.c_int
         L.zcg_array_meta_from_json.argtypes = [ctypes.c_char_p, u64, ctypes.POINTER(ArrayMeta), vp, u64]
         L.zcg_array_meta_from_json.restype = ctypes.c_int
+        L.zcg_chunk_key.argtypes = [ctypes.c_char_p, ctypes.c_char_p, vp, u32, vp, u64]
+        L.zcg_chunk_key.restype = u64
+        L.zcg_store_read_chunks_device.argtypes = [vp, ctypes.POINTER(Array), u32, vp, vp, vp, u32]
+        L.zcg_store_read_chunks_device.restype = ctypes.c_int
+        L.zcg_store_write_chunks_device.argtypes = [vp, ctypes.POINTER(Array), u32, vp, vp, vp, u32]
+        L.zcg_store_write_chunks_device.restype = ctypes.c_int
         _lib = L
         return L
 

@@ -184,7 +184,9 @@ uint64_t zcg_workspace_bytes(const zcg_array* a, uint32_t n, int encode) {
     if (a->compression.codec == ZCG_CODEC_XZ && encode) return xz_encode_ws_bytes(a, n);
     if (a->compression.codec == ZCG_CODEC_GZIP)
         return encode ? deflate_ws_bytes(a, n)
-                      : ((a->compression.flags & ZCG_FLAG_SERIAL_INFLATE) ? 0 : inflate_par_ws_bytes(a, n));
+                      : ((a->compression.flags & ZCG_FLAG_SERIAL_INFLATE) ? 0
+                         : (a->compression.flags & ZCG_FLAG_INFLATE_BLOCK_PAR) ? inflate_par_ws_bytes(a, n)
+                                                                                : inflate_wave_ws_bytes(a, n));
     if (a->compression.codec == ZCG_CODEC_LZ4) return encode ? lz4_encode_ws_bytes(a, n) : lz4_decode_ws_bytes(a, n);
     return 0;
 }
@@ -212,9 +214,15 @@ int zcg_decode_batch(zcg_ctx* ctx, const zcg_array* a, const zcg_chunk* d_chunks
             break;
         }
         zcg_ctx::Ws* w = nullptr;
-        const int r = stream_ws(ctx, stream, inflate_par_ws_bytes(a, n), &w);
+        if (a->compression.flags & ZCG_FLAG_INFLATE_BLOCK_PAR) {
+            const int r = stream_ws(ctx, stream, inflate_par_ws_bytes(a, n), &w);
+            if (r != ZCG_OK) return r;
+            e = launch_inflate_par(a, d_chunks, n, d_status, w->p, w->bytes, s);
+            break;
+        }
+        const int r = stream_ws(ctx, stream, inflate_wave_ws_bytes(a, n), &w);
         if (r != ZCG_OK) return r;
-        e = launch_inflate_par(a, d_chunks, n, d_status, w->p, w->bytes, s);
+        e = launch_inflate_wave(a, d_chunks, n, d_status, w->p, w->bytes, s);
         break;
     }
     case ZCG_CODEC_XZ: e = launch_xz_decode(a, d_chunks, n, d_status, nullptr, 0, s); break;

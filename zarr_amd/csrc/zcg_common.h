@@ -252,6 +252,9 @@ hipError_t launch_inflate(const zcg_array* a, const zcg_chunk* d_chunks, uint32_
 hipError_t launch_inflate_par(const zcg_array* a, const zcg_chunk* d_chunks, uint32_t n,
                               int32_t* d_status, void* ws, uint64_t ws_bytes, hipStream_t s);
 uint64_t inflate_par_ws_bytes(const zcg_array* a, uint32_t n);
+hipError_t launch_inflate_wave(const zcg_array* a, const zcg_chunk* d_chunks, uint32_t n,
+                               int32_t* d_status, void* ws, uint64_t ws_bytes, hipStream_t s);
+uint64_t inflate_wave_ws_bytes(const zcg_array* a, uint32_t n);
 hipError_t launch_deflate(const zcg_array* a, const zcg_chunk* d_chunks, uint32_t n,
                           uint64_t* d_out_len, int32_t* d_status, void* ws, uint64_t ws_bytes,
                           hipStream_t s);

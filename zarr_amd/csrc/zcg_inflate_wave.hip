@@ -1,0 +1,854 @@
+// zcg_inflate_wave.hip — gzip chunk decode with ONE WAVE PER CHUNK on gfx950
+// (GzipCompression decode, src/compression/gzip.rs:49-52 -> flate2 -> zlib).
+//
+// A deflate block body is one serial Huffman bit stream; its symbols come in
+// tokens (literal, or length/distance match), 16 383 per block for zlib's
+// default memLevel (a C2 chunk has 17 blocks of ~195 Kbit, ~60 KB output).
+// The wave owns the chunk and works block by block:
+//
+//  H (Huffman) round: the block body is cut into 64 COARSE segments, one per
+//    lane (~3 Kbit, ~250 tokens each, sized from the previous block).  Each
+//    lane decodes its own segment from its first bit as if a token started
+//    there, appending its tokens to a private list in the HBM workspace and
+//    marking token starts inside the first IW_MW bits of its segment (LDS).
+//    A misaligned Huffman decoder falls into step with the true one within a
+//    few tokens (median 64 bits, p99 ~450 bits on zlib-6 data), so when a
+//    lane runs past its segment end it soon lands on a token start the next
+//    lane marked: from there that lane's list is the true path.  Lane 0 starts
+//    at the true position; the chain of sync points gives every lane the
+//    first valid token of its list.  Segments are long, so the resync tail
+//    costs ~15 % of the decode instead of the ~60 % that 256-bit segments cost.
+//    A lane that hits an invalid code or an end-of-block in its own segment
+//    records it and keeps decoding after it (the record is real only if the
+//    lane's valid range reaches it), so a garbage path never ends a segment
+//    early.
+//  L (LZ77) phase: the valid tokens, in stream order, are resolved IW_S output
+//    bytes at a time in LDS: one 16-bit entry per output byte (final byte,
+//    pointer to an earlier byte of the stage, or a far code for a byte before
+//    the stage, read back from the chunk's committed output), pointer jumping
+//    until every entry is final, and one coalesced 16-B store pass with the
+//    byte-order transform fused.
+//
+// Everything is wave-synchronous: no s_barrier between phases, and the other
+// chunks' waves on the SIMD fill the dependent-LDS latency.  Block headers,
+// stored blocks and zlib's post-N look-ahead use the wave-uniform reader of
+// zcg_inflate_common.h.  Results are bit-identical to the serial kernel
+// (zcg_inflate.hip) and the 256-lane round kernel (zcg_inflate_par.hip);
+// tests/ compare all three against the oracle.
+#include <climits>
+
+#include "zcg_inflate_common.h"
+
+// A/B knobs: stage entries, tokens per lane list, waves per SIMD the register
+// budget targets, far-byte loads in flight per lane
+#ifndef ZIW_S
+#define ZIW_S 2048
+#endif
+#ifndef ZIW_TCAP
+#define ZIW_TCAP 768
+#endif
+#ifndef ZIW_WPE
+#define ZIW_WPE 3
+#endif
+#ifndef ZIW_EST_PCT
+#define ZIW_EST_PCT 108
+#endif
+
+namespace zcg {
+
+constexpr u32 IW_S = ZIW_S;            // stage ring entries: 64 lane blocks of IW_BLK
+constexpr u32 IW_BLK = IW_S / 64;
+constexpr u32 IW_TCAP = ZIW_TCAP;
+constexpr u32 IW_SEGMIN = 128;   // bits per lane segment
+constexpr u32 IW_SEGMAX = 4096;
+constexpr u32 IW_MWORDS = IW_SEGMAX / 32 + 3;  // mark words per segment (+ the tail of the last token)
+constexpr u32 IW_EST0 = 64 * 3072;  // first block's body estimate (zlib-6 blocks: ~195 Kbit)
+static_assert(IW_S == 2048 && IW_BLK == 32, "the L phase keeps one 32-entry block per lane in registers");
+
+// token word (same layout as zcg_inflate_par.hip, plus bit lengths on markers):
+//   literal  = bits << 24 | byte
+//   match    = 1 << 31 | bits << 24 | (len - 3) << 16 | (dist - 1)
+//   marker   = 1 << 30 | bits << 24 | code   (EOB / invalid code / input exhausted)
+// bits = the token's stream bits (<= 48), so a token's start is the lane's
+// segment start plus the bits of the tokens before it in the lane's list.
+constexpr u32 W_MATCH = 0x80000000u;
+constexpr u32 W_MARK = 0x40000000u;
+enum : u32 { M_EOB = 0, M_BAD = 1, M_EXH = 2, M_END = 3 /* synthetic: no more tokens in the round */ };
+__device__ __forceinline__ bool w_marker(u32 t) { return (t & 0xC0000000u) == W_MARK; }
+__device__ __forceinline__ u32 w_bits(u32 t) { return (t >> 24) & 63; }
+__device__ __forceinline__ u32 w_len(u32 t) { return (t & W_MATCH) ? ((t >> 16) & 0xFF) + 3 : (w_marker(t) ? 0u : 1u); }
+
+// lane stop codes (>= 64)
+constexpr u32 S_NONE = 0xFFFFFFFFu;
+constexpr u32 S_ROUND_END = 64;  // reached the end of the round's range
+constexpr u32 S_MARKER = 65;     // pass 2 ended on a marker (last token of the list)
+constexpr u32 S_CAP = 66;        // token list full
+
+// stage entries (u16): IE_VAL|byte = a final byte; a value below IW_S = the
+// ring index of an earlier byte of the stage; IE_FAR + k - 1 = the byte k
+// (1..32768) positions before the stage, read back from the committed output
+constexpr u32 IE_VAL = 0xFF00u;
+constexpr u32 IE_FAR = 0x4000u;
+static_assert(IW_S <= IE_FAR && IE_FAR + 32768 <= IE_VAL, "stage entry encoding");
+
+__device__ unsigned long long g_iw_dbg[32];
+enum { IWD_ROUNDS, IWD_BLOCKS, IWD_STAGES, IWD_GROUPS, IWD_P1_IT, IWD_P2_IT, IWD_CHAIN, IWD_TOKENS,
+       IWD_BYTES, IWD_MRR, IWD_CAPS, IWD_NOEOB,
+       IWT_HDR = 16, IWT_P1, IWT_P2, IWT_CHAIN, IWT_HEADS, IWT_EXPAND, IWT_GATHER, IWT_JUMP, IWT_COMMIT,
+       IWT_TOTAL };
+
+struct IwLds {
+    u32 ltab[INF_LTAB];
+    u32 dtab[INF_DTAB];
+    union {
+        struct {  // block headers and the look-ahead (wave-uniform reader)
+            HuffLds lh, dh;
+            u8 lens[320];
+            u32 bcache[BI_CACHE_WORDS];
+        } h;
+        struct {  // L phase: the stage ring and its token-start bits (one word per lane block)
+            u16 ptr[IW_S];
+            u32 head[IW_S / 32];
+        } st;
+    } u;
+    u16 ch_lane[65], ch_s[65], ch_e[65];  // chain members: lane, first valid token, list length
+    u32 mlim[65];                         // marked extent (bits) of each segment
+    u32 dbgc[32];
+};
+
+// wave-local ordering point for LDS (and the compiler): a wave's LDS
+// operations are performed in issue order, so a fence at wavefront scope is
+// enough to publish one lane's LDS writes to the other lanes
+__device__ __forceinline__ void wsync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ u32 iw_incl_scan(u32 v) {
+    v += (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
+    v += (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
+    v += (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
+    v += (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
+    const u32 t0 = (u32)__builtin_amdgcn_readlane((int)v, 15);
+    const u32 t1 = t0 + (u32)__builtin_amdgcn_readlane((int)v, 31);
+    const u32 t2 = t1 + (u32)__builtin_amdgcn_readlane((int)v, 47);
+    const u32 lane = (u32)lane_id();
+    return v + (lane < 16 ? 0u : (lane < 32 ? t0 : (lane < 48 ? t1 : t2)));
+}
+
+__device__ __forceinline__ u32 iw_wave_sum(u32 v) {
+    const u32 x = iw_incl_scan(v);
+    return (u32)__builtin_amdgcn_readlane((int)x, 63);
+}
+
+// ---- per-lane bit reader straight from HBM --------------------------------------------
+// The stream is read as aligned 16-byte vectors from base = ds & ~15 (an
+// aligned vector holding any stream byte is readable; bytes outside the
+// stream are don't-care: a token that needs bits past the end becomes the
+// input-exhausted marker).  A 96-bit window (lo:hi) holds the next nb bits;
+// words are appended from `cur`, and `nxt` is in flight one vector ahead.
+struct GBits {
+    u64 lo;
+    u32 hi;
+    u32 nb;
+    u32x4 cur;
+    u32x4 nxt;
+    u32 wi;  // next word of cur
+    u32 vn;  // vector index to load after nxt
+};
+
+__device__ __forceinline__ u32x4 gb_vec(const u8* base, u32 nvec, u32 v) {
+    if (v < nvec) return *(const u32x4*)(base + 16ull * v);
+    return u32x4{0u, 0u, 0u, 0u};
+}
+
+__device__ __forceinline__ void gb_word(GBits& s, const u8* base, u32 nvec) {
+    const u32 w = s.wi == 0 ? s.cur.x : s.wi == 1 ? s.cur.y : s.wi == 2 ? s.cur.z : s.cur.w;
+    if (s.nb < 64) {
+        s.lo |= (u64)w << s.nb;
+        s.hi = s.nb > 32 ? w >> (64 - s.nb) : 0u;
+    } else {
+        s.hi = w;
+    }
+    s.nb += 32;
+    if (++s.wi == 4) {
+        s.cur = s.nxt;
+        s.nxt = gb_vec(base, nvec, s.vn++);
+        s.wi = 0;
+    }
+}
+
+// >= 48 valid bits in lo afterwards (one token's worst case)
+__device__ __forceinline__ void gb_fill(GBits& s, const u8* base, u32 nvec) {
+    if (s.nb <= 64) gb_word(s, base, nvec);
+    if (s.nb < 48) gb_word(s, base, nvec);
+}
+
+__device__ __forceinline__ void gb_drop(GBits& s, u32 k) {  // 0 < k <= 48
+    s.lo = (s.lo >> k) | ((u64)s.hi << (64 - k));
+    s.hi = k >= 32 ? 0u : (s.hi >> k);
+    s.nb -= k;
+}
+
+// qa = bit position relative to base
+__device__ __forceinline__ void gb_init(GBits& s, const u8* base, u32 nvec, u32 qa) {
+    const u32 v0 = qa >> 7;
+    s.cur = gb_vec(base, nvec, v0);
+    s.nxt = gb_vec(base, nvec, v0 + 1);
+    s.vn = v0 + 2;
+    s.wi = (qa >> 5) & 3;
+    s.lo = 0;
+    s.hi = 0;
+    s.nb = 0;
+    gb_word(s, base, nvec);
+    gb_word(s, base, nvec);
+    gb_word(s, base, nvec);
+    const u32 k = qa & 31;
+    if (k) gb_drop(s, k);
+}
+
+// Decode one token from >= 48 valid bits: both table lookups always run, so
+// lanes holding different token kinds do not serialise.
+__device__ __forceinline__ u32 iw_decode(const IwLds& L, u64 v, u32* adv) {
+    u32 e = L.ltab[(u32)v & ((1u << INF_LBITS) - 1)];
+    if (((e >> 24) & 15) == K_SUB)
+        e = L.ltab[(e & 0xFFFF) + (((u32)v >> INF_LBITS) & ((1u << ((e >> 16) & 0xFF)) - 1))];
+    const u32 l = e >> 28, kind = (e >> 24) & 15, ex = (e >> 16) & 0xFF;
+    const u32 t = l + ex;
+    const u64 vd = v >> t;
+    u32 de = L.dtab[(u32)vd & ((1u << INF_DBITS) - 1)];
+    if (((de >> 24) & 15) == K_SUB)
+        de = L.dtab[(de & 0xFFFF) + (((u32)vd >> INF_DBITS) & ((1u << ((de >> 16) & 0xFF)) - 1))];
+    const u32 dl = de >> 28, dex = (de >> 16) & 0xFF;
+    const u32 len = (e & 0xFFFF) + ((u32)(v >> l) & ((1u << ex) - 1));
+    const u32 dist = (de & 0xFFFF) + ((u32)(vd >> dl) & ((1u << dex) - 1));
+    const u32 madv = t + dl + dex;
+    const bool dok = ((de >> 24) & 15) == K_DIST;
+    u32 a = l ? l : 1;
+    u32 tk = W_MARK | (a << 24) | M_BAD;
+    if (kind == K_LIT) tk = (l << 24) | (e & 0xFF);
+    if (kind == K_EOB) tk = W_MARK | (l << 24) | M_EOB;
+    if (kind == K_LEN) {
+        a = dok ? madv : t + (dl ? dl : 1);
+        tk = dok ? (W_MATCH | (madv << 24) | ((len - 3) << 16) | (dist - 1)) : (W_MARK | (a << 24) | M_BAD);
+    }
+    *adv = a;
+    return tk;
+}
+
+// stream bit of token j of the list of `lm` (segment start + bits before it)
+__device__ __forceinline__ u32 iw_pos(const gu32* gl, u32 lm, u32 j, u32 seg0) {
+    const u32 lane = (u32)lane_id();
+    const gu32* lst = gl + (u64)lm * IW_TCAP;
+    u32 s = 0;
+    for (u32 x = lane; x < j; x += 64) s += w_bits(lst[x]);
+    return seg0 + iw_wave_sum(s);
+}
+
+// Flush resolved stage bytes [from, to) to dst (byte-order transform fused,
+// bool deferred to the end of the chunk: the committed bytes are the window).
+__device__ void iw_commit(IwLds& L, u8* dst, u64 from, u64 to, DType t) {
+    const u32 lane = (u32)lane_id();
+    wsync();
+    const u64 a16 = (from + 15) & ~15ull, b16 = to & ~15ull;
+    if (a16 < b16) {
+        for (u64 p = a16 + (u64)lane * 16; p < b16; p += 64 * 16) {
+            const u32 i = (u32)(p & (IW_S - 1));
+            const u32x4 lo = *(const u32x4*)(L.u.st.ptr + i);
+            const u32x4 hi = *(const u32x4*)(L.u.st.ptr + i + 8);
+            auto pk = [](u32 a, u32 b) -> u32 { return __builtin_amdgcn_perm(b, a, 0x06040200u); };
+            const u32x4 v = u32x4{pk(lo.x, lo.y), pk(lo.z, lo.w), pk(hi.x, hi.y), pk(hi.z, hi.w)};
+            st16(dst + p, transform16(v, t));
+        }
+    }
+    const u64 e0 = a16 < b16 ? a16 : to;
+    for (u64 q = from + lane; q < e0; q += 64) dst[swap_pos(q, t)] = (u8)L.u.st.ptr[q & (IW_S - 1)];
+    if (a16 < b16)
+        for (u64 q = b16 + lane; q < to; q += 64) dst[swap_pos(q, t)] = (u8)L.u.st.ptr[q & (IW_S - 1)];
+    // the next stage's far reads come back through this CU's L1/L2: wait
+    // for the stores (same-CU stores refresh the L1)
+    __syncthreads();
+}
+
+__device__ void iw_bool_norm(u8* dst, u64 D) {
+    __syncthreads();
+    const u32 lane = (u32)lane_id();
+    const bool al = (((uintptr_t)dst) & 15) == 0;
+    for (u64 p = (u64)lane * 16; p < D; p += 64 * 16) {
+        if (p + 16 <= D) {
+            u32x4 v = al ? *(u32x4*)(dst + p) : ld16(dst + p);
+            v.x = bool_norm32(v.x); v.y = bool_norm32(v.y); v.z = bool_norm32(v.z); v.w = bool_norm32(v.w);
+            if (al) *(u32x4*)(dst + p) = v; else st16(dst + p, v);
+        } else {
+            for (u64 q = p; q < D; q++) dst[q] = dst[q] != 0;
+        }
+    }
+}
+
+#define IW_T(slot)                                                              \
+    do {                                                                        \
+        if (dbg) {                                                              \
+            const u64 _t = __builtin_readcyclecounter();                        \
+            if (lane == 0) L.dbgc[slot] += (u32)(_t - t_last);                  \
+            t_last = _t;                                                        \
+        }                                                                       \
+    } while (0)
+#define IW_ADD(slot, v) do { if (dbg && lane == 0) L.dbgc[slot] += (u32)(v); } while (0)
+
+// inclusive max over the wave (DPP row shifts, then the row maxima)
+__device__ __forceinline__ int iw_incl_max(int v) {
+    v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x111, 0xf, 0xf, false));  // row_shr:1
+    v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x112, 0xf, 0xf, false));  // row_shr:2
+    v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x114, 0xf, 0xf, false));  // row_shr:4
+    v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x118, 0xf, 0xf, false));  // row_shr:8
+    const int t0 = __builtin_amdgcn_readlane(v, 15);
+    const int t1 = max(t0, __builtin_amdgcn_readlane(v, 31));
+    const int t2 = max(t1, __builtin_amdgcn_readlane(v, 47));
+    const u32 lane = (u32)lane_id();
+    return lane < 16 ? v : max(v, lane < 32 ? t0 : (lane < 48 ? t1 : t2));
+}
+
+__device__ __forceinline__ u32 e16(const u32x4* r, u32 k) {  // entry k of a lane block held in 4 x u32x4
+    const u32x4 q = r[k >> 3];
+    const u32 w = ((k >> 1) & 3) == 0 ? q.x : ((k >> 1) & 3) == 1 ? q.y : ((k >> 1) & 3) == 2 ? q.z : q.w;
+    return (k & 1) ? (w >> 16) : (w & 0xFFFF);
+}
+__device__ __forceinline__ void e16_set(u32x4* r, u32 k, u32 v) {
+    u32x4 q = r[k >> 3];
+    const u32 j = (k >> 1) & 3;
+    u32 w = j == 0 ? q.x : j == 1 ? q.y : j == 2 ? q.z : q.w;
+    w = (k & 1) ? ((w & 0xFFFFu) | (v << 16)) : ((w & 0xFFFF0000u) | (v & 0xFFFFu));
+    if (j == 0) q.x = w; else if (j == 1) q.y = w; else if (j == 2) q.z = w; else q.w = w;
+    r[k >> 3] = q;
+}
+
+constexpr u32 IW_NSLOT_MAX = 8192;
+constexpr u64 IW_LIST_WORDS = 64ull * IW_TCAP;              // token lists of a slot (u32)
+constexpr u64 IW_MARK_WORDS = 64ull * IW_MWORDS * 2;        // mark words of a slot (u64 as 2 x u32)
+constexpr u64 IW_SLOT_WORDS = IW_LIST_WORDS + IW_MARK_WORDS;
+constexpr u64 IW_OWNER_BYTES = IW_NSLOT_MAX * 4;
+
+__global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chunk* __restrict__ chunks, u32 n,
+                                                                  u64 D, DType t, u32 vflags,
+                                                                  i32* __restrict__ status,
+                                                                  u32* __restrict__ owner, u32 nslot,
+                                                                  gu32* __restrict__ pools) {
+    extern __shared__ __attribute__((aligned(16))) u8 smem_raw[];
+    IwLds& L = *(IwLds*)smem_raw;
+    const u32 c = blockIdx.x;
+    if (c >= n) return;
+    const u32 lane = threadIdx.x;
+    const bool dbg = (vflags & ZCG_FLAG_DEBUG_COUNTERS) != 0;
+    const zcg_chunk ch = chunks[c];
+    if (D == 0) { if (lane == 0) status[c] = ZCG_OK; return; }
+    if (ch.dst_cap < D) { if (lane == 0) status[c] = ZCG_ERR_INVALID_INPUT; return; }
+    const u8* s = (const u8*)ch.src;
+    const u64 n_in = ch.src_len;
+    u64 h = 0;
+    int st = gzip_header(s, n_in, &h);
+    if (st == ZCG_OK && n_in - h >= (1ull << 28)) st = ZCG_ERR_UNSUPPORTED;  // u32 bit positions
+    if (st != ZCG_OK) { if (lane == 0) status[c] = st; return; }
+
+    u8* dst = (u8*)ch.dst;
+    const u8* ds = s + h;
+    const u64 n_ds = n_in - h;
+    const u32 total_bits = (u32)(n_ds * 8);
+    const u8* vbase = (const u8*)((uintptr_t)ds & ~(uintptr_t)15);
+    const u32 a0b = (u32)((uintptr_t)ds & 15) * 8;  // stream bit 0 relative to vbase
+    const u32 nvec = (u32)(((uintptr_t)ds & 15) + n_ds + 15) / 16;
+    DType tw = t;
+    tw.isbool = 0;
+
+    // workspace slot (freed at the end; every path below reaches it)
+    u32 slot = 0;
+    if (lane == 0) {
+        u32 sl = c % nslot;
+        while (atomicCAS(&owner[sl], 0u, 1u) != 0u) sl = (sl + 1) % nslot;
+        slot = sl;
+    }
+    slot = __builtin_amdgcn_readfirstlane(slot);
+    gu32* const gl = pools + (u64)slot * IW_SLOT_WORDS;                 // token lists [lane][IW_TCAP]
+    gu32* const my = gl + (u64)lane * IW_TCAP;
+    typedef __attribute__((address_space(1))) u64 gu64;
+    gu64* const marks = (gu64*)(gl + IW_LIST_WORDS);                    // mark words [lane][IW_MWORDS]
+    gu64* const mk = marks + (u64)lane * IW_MWORDS;
+
+    BitIn b;
+    bi_init(b, ds, n_ds, L.u.h.bcache);
+    u64 P = 0;
+    bool last = false, boundary = false, after_stored = false;
+    int r = R_OK;
+    u32 est = IW_EST0;
+    if (dbg) {
+        if (lane < 32) L.dbgc[lane] = 0;
+        wsync();
+    }
+    u64 t_last = __builtin_readcyclecounter();
+    const u64 t_start = t_last;
+
+    while (r == R_OK && P < D) {
+        // ---- block header (wave-uniform reader) ------------------------------------
+        if (last) { r = R_EXHAUSTED; break; }
+        u32 type = 0, slen = 0;
+        b.cbase = ~0ull;  // the reader's LDS cache shares storage with the stage
+        wsync();
+        r = read_block_header(b, &last, &type, &slen, L.u.h.lens, &L.u.h.lh, L.ltab, &L.u.h.dh, L.dtab);
+        const u32 hdr_end = (u32)b.consumed;
+        IW_T(IWT_HDR);
+        if (r != R_OK) break;
+        IW_ADD(IWD_BLOCKS, 1);
+        wsync();
+        if (type == 0) {
+            // ---- stored block: byte copies through the stage ------------------------
+            u64 in0 = hdr_end >> 3;  // byte aligned after LEN/NLEN
+            u32 done = 0;
+            while (done < slen && P < D) {
+                u32 k = slen - done;
+                if (k > IW_S) k = IW_S;
+                if ((u64)k > D - P) k = (u32)(D - P);
+                if (in0 + k > n_ds) { r = R_EXHAUSTED; break; }
+                wsync();
+                for (u32 i = lane; i < k; i += 64) L.u.st.ptr[(P + i) & (IW_S - 1)] = (u16)(IE_VAL | ds[in0 + i]);
+                iw_commit(L, dst, P, P + k, tw);
+                P += k; in0 += k; done += k;
+            }
+            if (r != R_OK) break;
+            b.cbase = ~0ull;
+            bi_seek(b, in0 * 8);
+            boundary = (done == slen);
+            after_stored = true;
+            continue;
+        }
+        after_stored = false;
+        const u32 body0 = hdr_end;
+        u32 R0 = hdr_end;
+        bool block_end = false;
+        bool final_cut = false;
+        u32 seg = (u32)(((u64)est * ZIW_EST_PCT / 100 / 64 + 31) & ~31ull);
+        seg = seg < IW_SEGMIN ? IW_SEGMIN : seg > IW_SEGMAX ? IW_SEGMAX : seg;
+        while (!block_end && !final_cut && r == R_OK && P < D) {
+            // ================= H round: coarse speculative Huffman decode =================
+            IW_ADD(IWD_ROUNDS, 1);
+            const u32 round_hi = R0 + 64 * seg;
+            const u32 p = R0 + lane * seg;
+            const u32 pend = p + seg;
+            u32 q = p, nt = 0, nxt = S_NONE, give = 0;
+            u32 cw = 0, cb = 0, cpre = 0;  // current mark word, its bits, marks before it
+            const bool active = p < total_bits;
+            GBits bs;
+            if (active) {
+                gb_init(bs, vbase, nvec, p + a0b);
+            } else if (lane == 0) {  // the block body starts at the stream end
+                my[0] = W_MARK | M_EXH;
+                nt = 1;
+                nxt = S_MARKER;
+            } else {
+                nxt = S_ROUND_END;  // (never on the chain: the lane before it ends in EXH)
+            }
+            u32 it1 = 0;
+            // pass 1: my segment; markers other than EXH do not stop it.  Token
+            // starts are marked in u64 words {bits, marks before the word}.
+            while (nxt == S_NONE && q < pend) {
+                gb_fill(bs, vbase, nvec);
+                u32 adv;
+                u32 tk = iw_decode(L, bs.lo, &adv);
+                if (q + adv > total_bits) tk = W_MARK | M_EXH;
+                if (nt == IW_TCAP) { nxt = S_CAP; break; }
+                my[nt] = tk;
+                nt++;
+                const u32 off = q - p, wi = off >> 5;
+                if (wi != cw) {  // (a token is <= 48 bits: at most one word skipped)
+                    mk[cw] = (u64)cb | ((u64)cpre << 32);
+                    cpre += __popc(cb);
+                    if (wi > cw + 1) mk[cw + 1] = (u64)cpre << 32;
+                    cw = wi;
+                    cb = 0;
+                }
+                cb |= 1u << (off & 31);
+                if (tk == (W_MARK | M_EXH)) { nxt = S_MARKER; break; }
+                gb_drop(bs, adv);
+                q += adv;
+                it1++;
+            }
+            if (active) {  // the last word and the words the last token spans
+                mk[cw] = (u64)cb | ((u64)cpre << 32);
+                cpre += __popc(cb);
+                mk[cw + 1] = (u64)cpre << 32;
+                mk[cw + 2] = (u64)cpre << 32;
+            }
+            // marked extent: the whole segment, or up to where the lane stopped
+            L.mlim[lane] = !active ? 0u : nxt == S_NONE ? seg : (q - p) + (nxt == S_MARKER ? 1u : 0u);
+            if (lane == 0) L.mlim[64] = 0;
+            __syncthreads();  // every lane's marks and list are stored
+            IW_T(IWT_P1);
+            // pass 2: follow my path until it meets a token start a later lane marked
+            u32 ks = lane + 1, pk = pend, it2 = 0;
+            u32 lim = L.mlim[ks];
+            u32 cwi = 0xFFFFFFFFu;
+            u64 cwv = 0;
+            while (nxt == S_NONE) {
+                if (q >= round_hi) { nxt = S_ROUND_END; break; }
+                if (q >= pk + seg) { ks++; pk += seg; lim = L.mlim[ks]; cwi = 0xFFFFFFFFu; }
+                const u32 off = q - pk;
+                if (off < lim) {
+                    const u32 wi = off >> 5;
+                    if (wi != cwi) { cwv = marks[(u64)ks * IW_MWORDS + wi]; cwi = wi; }
+                    const u32 bits = (u32)cwv;
+                    if ((bits >> (off & 31)) & 1u) {
+                        give = (u32)(cwv >> 32) + __popc(bits & ((1u << (off & 31)) - 1u));
+                        nxt = ks;
+                        break;
+                    }
+                }
+                gb_fill(bs, vbase, nvec);
+                u32 adv;
+                u32 tk = iw_decode(L, bs.lo, &adv);
+                if (q + adv > total_bits) tk = W_MARK | M_EXH;
+                if (nt == IW_TCAP) { nxt = S_CAP; break; }
+                my[nt] = tk;
+                nt++;
+                it2++;
+                if (w_marker(tk)) {
+                    if (tk != (W_MARK | M_EXH)) q += adv;
+                    nxt = S_MARKER;
+                    break;
+                }
+                gb_drop(bs, adv);
+                q += adv;
+            }
+            if (dbg) {
+                const u32 m1 = iw_wave_sum(it1), m2 = iw_wave_sum(it2);
+                const u32 m3 = iw_wave_sum(nxt == S_CAP ? 1u : 0u);
+                IW_ADD(IWD_P1_IT, m1);
+                IW_ADD(IWD_P2_IT, m2);
+                IW_ADD(IWD_CAPS, m3);
+            }
+            IW_T(IWT_P2);
+            // ---- chain: lane 0 is true; follow the sync targets (wave-uniform walk) ----
+            u32 ncm = 0, cur = 0, sidx = 0;
+            for (;;) {
+                const u32 e = (u32)__builtin_amdgcn_readlane((int)nt, (int)cur);
+                const u32 nx = (u32)__builtin_amdgcn_readlane((int)nxt, (int)cur);
+                if (lane == 0) { L.ch_lane[ncm] = (u16)cur; L.ch_s[ncm] = (u16)sidx; L.ch_e[ncm] = (u16)e; }
+                ncm++;
+                if (nx < 64) {
+                    sidx = (u32)__builtin_amdgcn_readlane((int)give, (int)cur);
+                    cur = nx;
+                    continue;
+                }
+                break;
+            }
+            const u32 endq = (u32)__builtin_amdgcn_readlane((int)q, (int)cur);  // after the last member's list
+            if ((u32)__builtin_amdgcn_readlane((int)nxt, (int)cur) == S_CAP && seg > IW_SEGMIN)
+                seg = (seg / 2 + 31) & ~31u;  // lists overflowed: shorter segments next round
+            if (lane == 0) { L.ch_lane[ncm] = 0; L.ch_s[ncm] = 0; L.ch_e[ncm] = 0; }
+            IW_ADD(IWD_CHAIN, ncm);
+            // token lists of other lanes are read below: their stores must be done
+            __syncthreads();
+            IW_T(IWT_CHAIN);
+
+            // ================= L phase: the chain's tokens, one stage at a time =========
+            // Stage: output [S, S + emit) in the ring; lane l owns the 32-entry
+            // block at absolute B0 + 32 l, B0 = S & ~31 (64 blocks = the ring).
+            u32 cm = 0, cj = 0;  // cursor: chain member, token index in its list
+            // lane's token at the cursor + lane (a member's list may end inside a group)
+            auto fetch = [&](u32 cm0, u32 cj0) -> u32 {
+                u32 m = cm0, jj = cj0 + lane;
+                while (m < ncm && jj >= L.ch_e[m]) { jj = jj - L.ch_e[m] + L.ch_s[m + 1]; m++; }
+                return m < ncm ? (u32)gl[(u64)L.ch_lane[m] * IW_TCAP + jj] : (W_MARK | M_END);
+            };
+            auto advance = [&](u32& cm0, u32& cj0, u32 k) {
+                cj0 += k;
+                while (cm0 < ncm && cj0 >= L.ch_e[cm0]) { cj0 = cj0 - L.ch_e[cm0] + L.ch_s[cm0 + 1]; cm0++; }
+            };
+            u32 tk_next = fetch(cm, cj);
+            bool round_done = false;
+            while (!round_done && r == R_OK) {
+                const u64 S = P;
+                const u32 sa = (u32)(S & 31);
+                const u64 room = D - P;
+                const u32 capS = IW_S - sa;
+                const u32 cap = room < capS ? (u32)room : capS;
+                const bool fin = (u64)cap == room;
+                L.u.st.head[lane] = 0;
+                wsync();
+                u32 emitted = 0;
+                bool far = false;
+                u32 why = 0;  // 1 final cut, 2 marker / round end, 3 capacity
+                u32 mcode = 0;
+                for (;;) {
+                    IW_ADD(IWD_GROUPS, 1);
+                    const u32 tk = tk_next;
+                    {  // prefetch the next group (right whenever this one is taken whole)
+                        u32 cm1 = cm, cj1 = cj;
+                        advance(cm1, cj1, 64);
+                        tk_next = fetch(cm1, cj1);
+                    }
+                    const bool ismk = w_marker(tk);
+                    const u64 mm = __ballot(ismk);
+                    const u32 fm = mm ? (u32)__builtin_ctzll(mm) : 64u;
+                    const u32 len = lane < fm ? w_len(tk) : 0u;
+                    const u32 incl = iw_incl_scan(len);
+                    const u32 o = emitted + incl - len;
+                    const bool take = lane < fm && (fin ? o < cap : o + len <= cap);
+                    const u64 tm = __ballot(take);
+                    const u32 ntk = (u32)__popcll(tm);
+                    if (take) {
+                        u16 v;
+                        if (tk & W_MATCH) {
+                            const u32 d = (tk & 0x7FFF) + 1;
+                            if ((u64)d > S + o) far = true;  // before the stream start
+                            v = (u16)(d - 1);
+                        } else {
+                            v = (u16)(IE_VAL | (tk & 0xFF));
+                        }
+                        const u32 ri = (u32)((S + o) & (IW_S - 1));
+                        L.u.st.ptr[ri] = v;
+                        atomicOr(&L.u.st.head[ri >> 5], 1u << (ri & 31));
+                    }
+                    if (ntk) emitted += (u32)__builtin_amdgcn_readlane((int)incl, (int)(ntk - 1));
+                    advance(cm, cj, ntk);
+                    if (fin && emitted >= cap) { why = 1; break; }
+                    if (ntk < 64) {
+                        if (ntk == fm) {
+                            why = 2;
+                            mcode = (u32)__builtin_amdgcn_readlane((int)tk, (int)fm) & 3u;
+                        } else {
+                            why = 3;
+                        }
+                        break;
+                    }
+                }
+                if (why != 0) tk_next = fetch(cm, cj);  // the next stage starts at the cursor
+                IW_ADD(IWD_STAGES, 1);
+                if (__ballot(far) != 0) { r = R_INVALID; break; }
+                const u32 emit = emitted < cap ? emitted : cap;  // a token may cross N: clip
+                wsync();
+                IW_T(IWT_HEADS);
+                if (emit) {
+                    // ---- LZ77 resolution, my 32-entry block in registers -----------------
+                    const u64 B0 = S & ~31ull;
+                    const u32 rb = (u32)((B0 + 32ull * lane) & (IW_S - 1));  // my block's ring index
+                    const int xr0 = 32 * (int)lane - (int)sa;                 // my block's first entry, stage-relative
+                    const u32 hw = L.u.st.head[rb >> 5];
+                    // the token covering my first entry: the last token start below it
+                    const int lastpos = hw ? xr0 + 31 - (int)__builtin_clz(hw) : INT_MIN;
+                    int carry = iw_incl_max(lastpos);
+                    carry = __shfl_up(carry, 1, 64);
+                    if (lane == 0) carry = INT_MIN;
+                    u32x4 ev[4];
+                    const u32x4* lp = (const u32x4*)(L.u.st.ptr + rb);
+                    ev[0] = lp[0]; ev[1] = lp[1]; ev[2] = lp[2]; ev[3] = lp[3];
+                    int mo = 0;
+                    u32 md = 0, mj = 0;
+                    bool in_match = false;
+                    if (!(hw & 1u) && carry != INT_MIN && xr0 >= 0 && xr0 < (int)emit) {
+                        mo = carry;
+                        md = (u32)L.u.st.ptr[(u32)((S + (u32)carry) & (IW_S - 1))] + 1;
+                        const u32 k0 = (u32)(xr0 - carry - 1);  // the loop steps mj before use
+                        mj = k0 < md ? k0 : k0 % md;
+                        in_match = md < IE_VAL;  // (a literal cannot cover a later byte)
+                    }
+                    u32 nfar = 0;
+#pragma unroll
+                    for (u32 k = 0; k < 32; k++) {
+                        const int xr = xr0 + (int)k;
+                        if (xr < 0 || xr >= (int)emit) continue;
+                        u32 v = e16(ev, k);
+                        if ((hw >> k) & 1u) {
+                            if (v >= IE_VAL) { in_match = false; continue; }  // literal: final
+                            mo = xr; md = v + 1; mj = 0; in_match = true;
+                        } else if (!in_match) {
+                            continue;  // (unreachable for a well-formed stage)
+                        } else {
+                            mj = (mj + 1 == md) ? 0 : mj + 1;
+                        }
+                        const int sp = mo - (int)md + (int)mj;
+                        if (sp < 0) { v = IE_FAR - 1 + (u32)(-sp); nfar++; }
+                        else v = (u32)((S + (u32)sp) & (IW_S - 1));
+                        e16_set(ev, k, v);
+                    }
+                    IW_T(IWT_EXPAND);
+                    // far codes: bytes before the stage, from the committed output
+                    if (__ballot(nfar != 0)) {
+#pragma unroll
+                        for (u32 half = 0; half < 2; half++) {
+                            u32 bv[16];
+#pragma unroll
+                            for (u32 u = 0; u < 16; u++) {
+                                const u32 v = e16(ev, half * 16 + u);
+                                const int xr = xr0 + (int)(half * 16 + u);
+                                bv[u] = 0;
+                                if (xr >= 0 && xr < (int)emit && v >= IE_FAR && v < IE_VAL)
+                                    bv[u] = ((const gu8*)dst)[swap_pos(S - (v - IE_FAR + 1), tw)];
+                            }
+#pragma unroll
+                            for (u32 u = 0; u < 16; u++) {
+                                const u32 v = e16(ev, half * 16 + u);
+                                const int xr = xr0 + (int)(half * 16 + u);
+                                if (xr >= 0 && xr < (int)emit && v >= IE_FAR && v < IE_VAL)
+                                    e16_set(ev, half * 16 + u, IE_VAL | bv[u]);
+                            }
+                        }
+                    }
+                    u32x4* wp = (u32x4*)(L.u.st.ptr + rb);
+                    wp[0] = ev[0]; wp[1] = ev[1]; wp[2] = ev[2]; wp[3] = ev[3];
+                    wsync();
+                    IW_T(IWT_GATHER);
+                    // pointer jumping: every pointer points strictly backwards, so
+                    // log2(IW_S) passes resolve any stage (the cap guards the invariant)
+                    for (u32 pass = 0;; pass++) {
+                        bool pending = false;
+                        u32 nw[32];
+#pragma unroll
+                        for (u32 k = 0; k < 32; k++) {
+                            const u32 v = e16(ev, k);
+                            const int xr = xr0 + (int)k;
+                            nw[k] = (xr >= 0 && xr < (int)emit && v < IW_S) ? (u32)L.u.st.ptr[v] : v;
+                        }
+#pragma unroll
+                        for (u32 k = 0; k < 32; k++) {
+                            const int xr = xr0 + (int)k;
+                            if (xr >= 0 && xr < (int)emit && e16(ev, k) < IW_S) {
+                                e16_set(ev, k, nw[k]);
+                                pending |= nw[k] < IW_S;
+                            }
+                        }
+                        wp[0] = ev[0]; wp[1] = ev[1]; wp[2] = ev[2]; wp[3] = ev[3];
+                        IW_ADD(IWD_MRR, 1);
+                        wsync();
+                        if (__ballot(pending) == 0) break;
+                        if (pass >= 12) { r = R_INVALID; break; }
+                    }
+                    IW_T(IWT_JUMP);
+                    if (r != R_OK) break;
+                    iw_commit(L, dst, S, S + emit, tw);
+                    P = S + emit;
+                    IW_ADD(IWD_BYTES, emit);
+                    IW_T(IWT_COMMIT);
+                }
+                if (why == 1) {
+                    // output full: zlib's look-ahead continues at the first untaken token
+                    boundary = emitted == cap;
+                    final_cut = true;
+                    round_done = true;
+                    if (boundary) {
+                        u32 qn = endq;
+                        if (cm < ncm) qn = iw_pos(gl, L.ch_lane[cm], cj, R0 + L.ch_lane[cm] * seg);
+                        b.cbase = ~0ull;
+                        bi_seek(b, qn);
+                    }
+                } else if (why == 2) {
+                    round_done = true;
+                    if (mcode == M_END) {
+                        R0 = endq;  // the chain ended without a marker: next round from there
+                        IW_ADD(IWD_NOEOB, 1);
+                        // the rest of the block is likely short: size the next round for it
+                        const u32 used = R0 - body0;
+                        const u32 rem = est > used ? est - used : est / 8;
+                        u32 sg = (rem / 64 + 31) & ~31u;
+                        seg = sg < IW_SEGMIN ? IW_SEGMIN : sg > IW_SEGMAX ? IW_SEGMAX : sg;
+                    } else if (mcode == M_EOB) {
+                        const u32 lm = L.ch_lane[cm];
+                        const u32 qe = iw_pos(gl, lm, cj + 1, R0 + lm * seg);  // after the EOB code
+                        block_end = true;
+                        b.cbase = ~0ull;
+                        bi_seek(b, qe);
+                        est = qe - body0;
+                    } else if (mcode == M_BAD) {
+                        r = R_INVALID;
+                    } else {
+                        r = R_EXHAUSTED;
+                    }
+                }
+            }
+        }
+    }
+    // zlib's post-N look-ahead (wave-uniform); see zcg_inflate_common.h
+    if (r == R_OK && P >= D && boundary) {
+        const u64 last_byte = h + (b.consumed ? (b.consumed - 1) / 8 : 0);
+        u64 wend = (last_byte / 32768 + 1) * 32768;
+        if (wend > n_in) wend = n_in;
+        b.limit = (wend - h) * 8;
+        b.cbase = ~0ull;
+        wsync();
+        if (b.limit >= b.consumed) {
+            const int la = inf_lookahead(b, last, after_stored, L.u.h.lens, &L.u.h.lh, L.ltab, &L.u.h.dh, L.dtab);
+            if (la == R_INVALID) r = R_INVALID;
+        }
+    }
+    if (r == R_INVALID) st = ZCG_ERR_INVALID_DATA;
+    else if (r == R_EXHAUSTED || P < D) st = ZCG_ERR_UNEXPECTED_EOF;
+    if (t.isbool) iw_bool_norm(dst, P < D ? P : D);
+    if (dbg) {
+        if (lane == 0) L.dbgc[IWT_TOTAL] = (u32)(__builtin_readcyclecounter() - t_start);
+        wsync();
+        if (lane < 32 && L.dbgc[lane]) atomicAdd(&g_iw_dbg[lane], (unsigned long long)L.dbgc[lane]);
+    }
+    __syncthreads();  // every workspace access of this wave is done
+    if (lane == 0) {
+        status[c] = st;
+        atomicExch(&owner[slot], 0u);
+    }
+}
+
+extern "C" int zcg__debug_inflate_wave_counters(unsigned long long* out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_iw_dbg), sizeof(unsigned long long) * 32) != hipSuccess)
+        return -1;
+    if (reset) {
+        unsigned long long z[32] = {0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_iw_dbg), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+
+// Slots: one per resident wave (the LDS footprint bounds residency), never
+// more than the batch.
+static u32 iw_nslot(uint32_t n) {
+    static u32 cus = 0;
+    if (!cus) {
+        int dev = 0, v = 0;
+        (void)hipGetDevice(&dev);
+        cus = (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
+                  ? (u32)v : 256u;
+    }
+    u32 per_cu = (u32)(160 * 1024 / sizeof(IwLds));
+    if (per_cu < 1) per_cu = 1;
+    u64 ns = (u64)cus * per_cu;
+    if (ns > n) ns = n;
+    if (ns > IW_NSLOT_MAX) ns = IW_NSLOT_MAX;
+    return (u32)ns;
+}
+
+uint64_t inflate_wave_ws_bytes(const zcg_array* a, uint32_t n) {
+    (void)a;
+    if (n == 0) return 0;
+    return IW_OWNER_BYTES + (u64)iw_nslot(n) * IW_SLOT_WORDS * 4;
+}
+
+hipError_t launch_inflate_wave(const zcg_array* a, const zcg_chunk* d_chunks, uint32_t n,
+                               int32_t* d_status, void* ws, uint64_t ws_bytes, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    if (!ws || ws_bytes < inflate_wave_ws_bytes(a, n)) return hipErrorInvalidValue;
+    const DType t = make_dtype(a->dtype);
+    const u64 D = a->chunk_num_elements * (u64)t.es;
+    static bool attr_set = false;
+    const size_t lds = sizeof(IwLds);
+    if (!attr_set) {
+        hipError_t e = hipFuncSetAttribute((const void*)inflate_wave_kernel,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+        attr_set = true;
+    }
+    const u32 nslot = iw_nslot(n);
+    u32* owner = (u32*)ws;
+    hipError_t e = hipMemsetAsync(owner, 0, (size_t)nslot * 4, s);
+    if (e != hipSuccess) return e;
+    gu32* pools = (gu32*)((u8*)ws + IW_OWNER_BYTES);
+    hipLaunchKernelGGL(inflate_wave_kernel, dim3(n), dim3(64), lds, s, d_chunks, n, D, t,
+                       a->compression.flags, d_status, owner, nslot, pools);
+    return hipGetLastError();
+}
+
+}  // namespace zcg

@@ -486,3 +486,24 @@ extern "C" int zcg_array_meta_from_json(const char* json, uint64_t len, zcg_arra
     }
     return st;
 }
+
+extern "C" uint64_t zcg_chunk_key(const char* path, const char* separator, const uint64_t* grid_position,
+                                  uint32_t ndim, char* out, uint64_t cap) {
+    std::string p = path ? path : "";
+    size_t a = 0, b = p.size();
+    while (a < b && p[a] == '/') a++;  // trim_start_matches('/')
+    while (b > a && p[b - 1] == '/') b--;  // trim_end_matches('/')
+    std::string key = "/data/root";
+    if (b > a) key += "/" + p.substr(a, b - a);
+    key += "/c";
+    for (uint32_t i = 0; i < ndim; i++) {
+        key += std::to_string(grid_position[i]);
+        if (i + 1 < ndim && separator) key += separator;
+    }
+    if (out && cap) {
+        const size_t k = key.size() < cap - 1 ? key.size() : (size_t)cap - 1;
+        memcpy(out, key.data(), k);
+        out[k] = 0;
+    }
+    return key.size();
+}

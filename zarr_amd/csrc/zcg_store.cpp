@@ -23,8 +23,10 @@
 
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
 #include <cstring>
 #include <functional>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -50,23 +52,71 @@ using namespace zcg;
 
 size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 
-// run fn(i) for i in [0, count) on up to `threads` host threads
-void pfor(uint32_t threads, size_t count, const std::function<void(size_t)>& fn) {
-    if (count == 0) return;
-    const uint32_t t = (uint32_t)std::min<size_t>(std::max<uint32_t>(threads, 1), count);
-    if (t == 1) {
-        for (size_t i = 0; i < count; i++) fn(i);
-        return;
+// Persistent fork-join pool of host I/O threads (one per context's store):
+// run(t, n, fn) calls fn(i) for i in [0, n) on the caller plus t-1 workers.
+// Workers are created once and reused by every phase of every call.
+class IoPool {
+  public:
+    ~IoPool() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            quit_ = true;
+        }
+        start_.notify_all();
+        for (auto& t : workers_) t.join();
     }
-    std::atomic<size_t> next{0};
-    std::vector<std::thread> pool;
-    pool.reserve(t);
-    for (uint32_t k = 0; k < t; k++)
-        pool.emplace_back([&] {
-            for (size_t i; (i = next.fetch_add(1)) < count;) fn(i);
-        });
-    for (auto& th : pool) th.join();
-}
+    void run(uint32_t threads, size_t count, const std::function<void(size_t)>& fn) {
+        if (count == 0) return;
+        const uint32_t t = (uint32_t)std::min<size_t>(std::max<uint32_t>(threads, 1), count);
+        if (t == 1) {
+            for (size_t i = 0; i < count; i++) fn(i);
+            return;
+        }
+        std::unique_lock<std::mutex> lk(mu_);
+        while (workers_.size() < t - 1) {
+            const uint32_t id = (uint32_t)workers_.size();
+            workers_.emplace_back([this, id] { worker(id); });
+        }
+        fn_ = &fn;
+        count_ = count;
+        next_.store(0);
+        want_ = t - 1;
+        finished_ = 0;
+        gen_++;
+        lk.unlock();
+        start_.notify_all();
+        for (size_t i; (i = next_.fetch_add(1)) < count;) fn(i);
+        lk.lock();
+        done_.wait(lk, [&] { return finished_ == want_; });
+        fn_ = nullptr;
+    }
+
+  private:
+    void worker(uint32_t id) {
+        uint64_t seen = 0;
+        std::unique_lock<std::mutex> lk(mu_);
+        for (;;) {
+            start_.wait(lk, [&] { return quit_ || (gen_ != seen && id < want_); });
+            if (quit_) return;
+            seen = gen_;
+            const std::function<void(size_t)>* fn = fn_;
+            const size_t count = count_;
+            lk.unlock();
+            for (size_t i; (i = next_.fetch_add(1)) < count;) (*fn)(i);
+            lk.lock();
+            if (++finished_ == want_) done_.notify_one();
+        }
+    }
+    std::mutex mu_;
+    std::condition_variable start_, done_;
+    std::vector<std::thread> workers_;
+    const std::function<void(size_t)>* fn_ = nullptr;
+    size_t count_ = 0;
+    std::atomic<size_t> next_{0};
+    uint32_t want_ = 0, finished_ = 0;
+    uint64_t gen_ = 0;
+    bool quit_ = false;
+};
 
 // create_dir_all of the parent of `path`
 bool mkdirs_parent(const std::string& path) {
@@ -142,16 +192,24 @@ size_t store_batch_bytes(const zcg_array* a) {
     return (c == ZCG_CODEC_XZ || c == ZCG_CODEC_BZIP2) ? 4 * STORE_BATCH_BYTES : STORE_BATCH_BYTES;
 }
 
-struct OpenFile {
-    int fd = -1;
-    uint64_t size = 0;
-    int32_t st = ZCG_OK;
-};
+// true when every pointer is page-locked host memory the GPU can copy into
+bool all_pinned(void* const* p, uint32_t n) {
+    for (uint32_t i = 0; i < n; i++) {
+        hipPointerAttribute_t at;
+        if (hipPointerGetAttributes(&at, p[i]) != hipSuccess) {
+            (void)hipGetLastError();
+            return false;
+        }
+        if (at.type != hipMemoryTypeHost) return false;
+    }
+    return true;
+}
 
 }  // namespace
 
 struct zcg_store_slots {
     Slot s[2];
+    IoPool pool;
 };
 
 namespace zcg {
@@ -169,113 +227,156 @@ zcg_store_slots* store_slots_new(int device) {
 }
 }  // namespace zcg
 
-extern "C" int zcg_store_read_chunks(zcg_ctx* ctx, const zcg_array* a, uint32_t n, const char* const* paths,
-                                     void* const* dsts, int32_t* status, uint32_t io_threads) {
+namespace {
+
+// How one store read lands its decoded chunks.
+enum class Dst {
+    HostStaged,  // pageable host buffers: D2H into pinned staging, copied out by the pool
+    HostPinned,  // page-locked host buffers: D2H straight into them
+    Device,      // device buffers: decoded in place, nothing crosses back but statuses
+};
+
+// ReadableStore::get for a batch (filesystem.rs:201-210): is_file() (stat;
+// anything but a regular file -> Ok(None) -> ZCG_ABSENT), then open + shared
+// flock + read under the lock, close.  The reader pool holds at most one
+// descriptor per thread.  Files are read into pinned staging sized from the
+// stat pass; a file that grew between stat and its locked read makes the
+// sub-batch re-stage (bounded retries).
+int store_read_impl(zcg_ctx* ctx, const zcg_array* a, uint32_t n, const char* const* paths, void* const* dsts,
+                    int32_t* status, uint32_t io_threads, bool device_dsts) {
     if (!ctx || !a || (n && (!paths || !dsts || !status))) return ZCG_ERR_INVALID_INPUT;
     if (n == 0) return ZCG_OK;
     const int dev = ctx_device(ctx);
     (void)hipSetDevice(dev);
     zcg_store_slots* S = ctx_store_slots(ctx);
     if (!S) return ZCG_ERR_RUNTIME;
+    IoPool& pool = S->pool;
     const uint64_t D = a->chunk_num_elements * (uint64_t)a->dtype.elem_size;
+    const Dst mode = device_dsts ? Dst::Device : (all_pinned(dsts, n) ? Dst::HostPinned : Dst::HostStaged);
     const uint32_t per = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(n, D ? store_batch_bytes(a) / D : n));
     const uint32_t nb = (n + per - 1) / per;
-    std::vector<std::vector<OpenFile>> files(2);
-    std::vector<std::vector<size_t>> offs(2);
+    std::vector<int32_t> fst[2];  // per sub-batch slot: file status (OK / ABSENT / IO)
     int rc = ZCG_OK;
     auto fail = [&](hipError_t e, const char* what) {
         ctx_set_error(ctx, std::string(what) + ": " + hipGetErrorString(e));
         rc = ZCG_ERR_RUNTIME;
     };
-    // copy-out of sub-batch b (after its D2H): decoded chunks -> caller buffers
+    // sub-batch b is done on the GPU: statuses (and staged chunks) -> caller
     auto finish = [&](uint32_t b) {
         Slot& sl = S->s[b & 1];
         sl.pending = false;
         hipError_t e = hipEventSynchronize(sl.done);
         if (e != hipSuccess) { fail(e, "store decode"); return; }
         const uint32_t i0 = b * per, m = std::min(per, n - i0);
-        const std::vector<OpenFile>& fs = files[b & 1];
-        const int32_t* st = (const int32_t*)((uint8_t*)sl.h_out + (size_t)m * D);
-        pfor(io_threads, m, [&](size_t k) {
-            if (fs[k].st != ZCG_OK) { status[i0 + k] = fs[k].st; return; }
+        const std::vector<int32_t>& fs = fst[b & 1];
+        const size_t o_st = mode == Dst::HostStaged ? (size_t)m * D : 0;
+        const int32_t* st = (const int32_t*)((uint8_t*)sl.h_out + o_st);
+        pool.run(io_threads, m, [&](size_t k) {
+            if (fs[k] != ZCG_OK) { status[i0 + k] = fs[k]; return; }
             status[i0 + k] = st[k];
-            if (st[k] == ZCG_OK && D) memcpy(dsts[i0 + k], (uint8_t*)sl.h_out + k * D, D);
+            if (mode == Dst::HostStaged && st[k] == ZCG_OK && D)
+                memcpy(dsts[i0 + k], (uint8_t*)sl.h_out + k * D, D);
         });
     };
+    std::vector<uint64_t> size(per), off(per);
+    std::vector<uint8_t> grew(per);
     for (uint32_t b = 0; b < nb && rc == ZCG_OK; b++) {
         Slot& sl = S->s[b & 1];
         if (sl.pending) finish(b - 2);  // the slot's previous sub-batch
         if (rc != ZCG_OK) break;
         const uint32_t i0 = b * per, m = std::min(per, n - i0);
-        std::vector<OpenFile>& fs = files[b & 1];
-        fs.assign(m, OpenFile{});
-        // 1. open + shared lock + size (filesystem.rs:201-210)
-        pfor(io_threads, m, [&](size_t k) {
-            OpenFile& f = fs[k];
-            f.fd = open(paths[i0 + k], O_RDONLY | O_CLOEXEC);
-            if (f.fd < 0) { f.st = errno == ENOENT ? ZCG_ABSENT : ZCG_ERR_IO; return; }
-            struct stat sb;
-            if (fstat(f.fd, &sb) != 0) f.st = ZCG_ERR_IO;
-            else if (!S_ISREG(sb.st_mode)) f.st = ZCG_ABSENT;  // not a file: get() -> Ok(None) (is_file())
-            else if (flock(f.fd, LOCK_SH) != 0) f.st = ZCG_ERR_IO;
-            if (f.st != ZCG_OK) {
-                close(f.fd);
-                f.fd = -1;
-                return;
+        std::vector<int32_t>& fs = fst[b & 1];
+        fs.assign(m, ZCG_OK);
+        size_t in_bytes = 0;
+        for (int attempt = 0;; attempt++) {
+            // 1. is_file() + size of every chunk file
+            pool.run(io_threads, m, [&](size_t k) {
+                struct stat sb;
+                grew[k] = 0;
+                if (stat(paths[i0 + k], &sb) != 0 || !S_ISREG(sb.st_mode)) {
+                    fs[k] = ZCG_ABSENT;  // get() -> Ok(None) -> read_chunk None (storage.rs:226-234)
+                    size[k] = 0;
+                } else {
+                    fs[k] = ZCG_OK;
+                    size[k] = (uint64_t)sb.st_size;
+                }
+            });
+            // staging layout: [desc m][status m][streams, 256-B aligned]
+            size_t p = al256(sizeof(zcg_chunk) * m) + al256(sizeof(int32_t) * m);
+            for (uint32_t k = 0; k < m; k++) {
+                off[k] = p;
+                p = al256(p + size[k]);
             }
-            f.size = (uint64_t)sb.st_size;
-        });
-        // layout of the pinned staging: [desc m][status m][streams 256-aligned]
-        std::vector<size_t>& of = offs[b & 1];
-        of.assign(m, 0);
-        size_t p = al256(sizeof(zcg_chunk) * m) + al256(sizeof(int32_t) * m);
-        const size_t off_src = p;
-        for (uint32_t k = 0; k < m; k++) {
-            of[k] = p;
-            p = al256(p + fs[k].size);
+            in_bytes = p;
+            const size_t out_bytes = (mode == Dst::HostStaged ? (size_t)m * D : 0) + al256(sizeof(int32_t) * m);
+            const size_t dev_bytes = al256(in_bytes) + (mode == Dst::Device ? 0 : (size_t)m * D);
+            hipError_t e = sl.grow(in_bytes, out_bytes, dev_bytes);
+            if (e != hipSuccess) { fail(e, "store staging"); break; }
+            // 2. open + shared lock + read under the lock + close, one file per task
+            std::atomic<uint32_t> n_grew{0};
+            pool.run(io_threads, m, [&](size_t k) {
+                if (fs[k] != ZCG_OK) return;
+                const int fd = open(paths[i0 + k], O_RDONLY | O_CLOEXEC);
+                if (fd < 0) { fs[k] = ZCG_ERR_IO; return; }
+                struct stat sb;
+                if (flock(fd, LOCK_SH) != 0 || fstat(fd, &sb) != 0) {
+                    fs[k] = ZCG_ERR_IO;
+                } else if ((uint64_t)sb.st_size > size[k]) {
+                    grew[k] = 1;  // changed since the stat pass: re-stage this sub-batch
+                    n_grew++;
+                } else {
+                    const uint64_t want = (uint64_t)sb.st_size;
+                    uint8_t* d = (uint8_t*)sl.h_in + off[k];
+                    uint64_t got = 0;
+                    while (got < want) {
+                        const ssize_t r = pread(fd, d + got, want - got, (off_t)got);
+                        if (r < 0 && errno == EINTR) continue;
+                        if (r <= 0) break;
+                        got += (uint64_t)r;
+                    }
+                    size[k] = got;
+                }
+                close(fd);  // releases the lock
+            });
+            if (n_grew.load() == 0) break;
+            if (attempt >= 4) {  // a writer keeps growing the files: report them as I/O errors
+                for (uint32_t k = 0; k < m; k++)
+                    if (grew[k]) fs[k] = ZCG_ERR_IO;
+                break;
+            }
         }
-        const size_t in_bytes = p, out_bytes = (size_t)m * D + al256(sizeof(int32_t) * m);
-        hipError_t e = sl.grow(in_bytes, out_bytes, in_bytes + (size_t)m * D);
-        if (e != hipSuccess) { fail(e, "store staging"); break; }
-        // 2. read every file straight into pinned memory; the lock ends with close
-        pfor(io_threads, m, [&](size_t k) {
-            OpenFile& f = fs[k];
-            if (f.fd < 0) return;
-            uint8_t* d = (uint8_t*)sl.h_in + of[k];
-            uint64_t got = 0;
-            while (got < f.size) {
-                const ssize_t r = pread(f.fd, d + got, f.size - got, (off_t)got);
-                if (r <= 0) break;
-                got += (uint64_t)r;
-            }
-            f.size = got;  // a file that shrank while read: the bytes that were there
-            close(f.fd);
-            f.fd = -1;
-        });
-        // 3. descriptors (device pointers), H2D, decode, D2H of elements + status
+        if (rc != ZCG_OK) break;
+        // 3. descriptors (device pointers), H2D, decode, D2H of statuses (+ elements)
         uint8_t* dbase = (uint8_t*)sl.d_buf;
         zcg_chunk* hd = (zcg_chunk*)sl.h_in;
         const size_t d_out = al256(in_bytes);
         for (uint32_t k = 0; k < m; k++) {
-            hd[k].src = dbase + of[k];
-            hd[k].src_len = fs[k].st == ZCG_OK ? fs[k].size : 0;
-            hd[k].dst = dbase + d_out + (size_t)k * D;
+            hd[k].src = dbase + off[k];
+            hd[k].src_len = fs[k] == ZCG_OK ? size[k] : 0;
+            hd[k].dst = mode == Dst::Device ? dsts[i0 + k] : (void*)(dbase + d_out + (size_t)k * D);
             hd[k].dst_cap = D;
         }
-        (void)off_src;
-        e = hipMemcpyAsync(dbase, sl.h_in, in_bytes, hipMemcpyHostToDevice, sl.stream);
+        hipError_t e = hipMemcpyAsync(dbase, sl.h_in, in_bytes, hipMemcpyHostToDevice, sl.stream);
         if (e != hipSuccess) { fail(e, "store H2D"); break; }
         int32_t* d_status = (int32_t*)(dbase + al256(sizeof(zcg_chunk) * m));
         const int r = zcg_decode_batch(ctx, a, (const zcg_chunk*)dbase, m, d_status, (void*)sl.stream);
         if (r != ZCG_OK) { rc = r; break; }
-        if (D) e = hipMemcpyAsync(sl.h_out, dbase + d_out, (size_t)m * D, hipMemcpyDeviceToHost, sl.stream);
+        uint8_t* ho = (uint8_t*)sl.h_out;
+        if (mode == Dst::HostStaged && D) {
+            e = hipMemcpyAsync(ho, dbase + d_out, (size_t)m * D, hipMemcpyDeviceToHost, sl.stream);
+            ho += (size_t)m * D;
+        } else if (mode == Dst::HostPinned && D) {
+            for (uint32_t k = 0; k < m && e == hipSuccess; k++)  // absent / unreadable: left untouched
+                if (fs[k] == ZCG_OK)
+                    e = hipMemcpyAsync(dsts[i0 + k], dbase + d_out + (size_t)k * D, D, hipMemcpyDeviceToHost,
+                                       sl.stream);
+        }
         if (e == hipSuccess)
-            e = hipMemcpyAsync((uint8_t*)sl.h_out + (size_t)m * D, d_status, sizeof(int32_t) * m,
-                               hipMemcpyDeviceToHost, sl.stream);
+            e = hipMemcpyAsync(ho, d_status, sizeof(int32_t) * m, hipMemcpyDeviceToHost, sl.stream);
         if (e == hipSuccess) e = hipEventRecord(sl.done, sl.stream);
         if (e != hipSuccess) { fail(e, "store D2H"); break; }
         sl.pending = true;
-        // 4. copy out the previous sub-batch while this one runs on the GPU
+        // 4. finish the previous sub-batch while this one runs on the GPU
         if (b >= 1 && S->s[(b - 1) & 1].pending) finish(b - 1);
     }
     for (uint32_t b = nb >= 2 ? nb - 2 : 0; b < nb; b++)
@@ -283,20 +384,20 @@ extern "C" int zcg_store_read_chunks(zcg_ctx* ctx, const zcg_array* a, uint32_t 
             if (rc == ZCG_OK) finish(b);
             else { (void)hipEventSynchronize(S->s[b & 1].done); S->s[b & 1].pending = false; }
         }
-    for (auto& fs : files)
-        for (auto& f : fs)
-            if (f.fd >= 0) close(f.fd);
     return rc;
 }
 
-extern "C" int zcg_store_write_chunks(zcg_ctx* ctx, const zcg_array* a, uint32_t n, const char* const* paths,
-                                      const void* const* elems, int32_t* status, uint32_t io_threads) {
+// WriteableStore::set for a batch (filesystem.rs:260-280) after a GPU encode of
+// host (device_src = false) or device-resident element slots.
+int store_write_impl(zcg_ctx* ctx, const zcg_array* a, uint32_t n, const char* const* paths,
+                     const void* const* elems, int32_t* status, uint32_t io_threads, bool device_src) {
     if (!ctx || !a || (n && (!paths || !elems || !status))) return ZCG_ERR_INVALID_INPUT;
     if (n == 0) return ZCG_OK;
     const int dev = ctx_device(ctx);
     (void)hipSetDevice(dev);
     zcg_store_slots* S = ctx_store_slots(ctx);
     if (!S) return ZCG_ERR_RUNTIME;
+    IoPool& pool = S->pool;
     const uint64_t D = a->chunk_num_elements * (uint64_t)a->dtype.elem_size;
     const uint64_t cap = al256(zcg_encode_bound(&a->compression, D));
     const uint32_t per = (uint32_t)std::max<uint64_t>(
@@ -317,7 +418,7 @@ extern "C" int zcg_store_write_chunks(zcg_ctx* ctx, const zcg_array* a, uint32_t
         const uint8_t* ho = (const uint8_t*)sl.h_out;
         const uint64_t* lens = (const uint64_t*)(ho + (size_t)m * cap);
         const int32_t* st = (const int32_t*)(ho + (size_t)m * cap + al256(8 * m));
-        pfor(io_threads, m, [&](size_t k) {
+        pool.run(io_threads, m, [&](size_t k) {
             if (st[k] != ZCG_OK) { status[i0 + k] = st[k]; return; }
             const std::string path = paths[i0 + k];
             if (!mkdirs_parent(path)) { status[i0 + k] = ZCG_ERR_IO; return; }
@@ -330,6 +431,7 @@ extern "C" int zcg_store_write_chunks(zcg_ctx* ctx, const zcg_array* a, uint32_t
             uint64_t put = 0;
             while (s2 == ZCG_OK && put < lens[k]) {
                 const ssize_t w = pwrite(fd, d + put, lens[k] - put, (off_t)put);
+                if (w < 0 && errno == EINTR) continue;
                 if (w <= 0) s2 = ZCG_ERR_IO;
                 else put += (uint64_t)w;
             }
@@ -342,23 +444,25 @@ extern "C" int zcg_store_write_chunks(zcg_ctx* ctx, const zcg_array* a, uint32_t
         if (sl.pending) finish(b - 2);
         if (rc != ZCG_OK) break;
         const uint32_t i0 = b * per, m = std::min(per, n - i0);
-        // device: [desc][status][out_len][elements m*D][encoded m*cap]
+        // device: [desc][status][out_len][elements m*D (host source only)][encoded m*cap]
         const size_t o_st = al256(sizeof(zcg_chunk) * m), o_len = o_st + al256(4 * m);
-        const size_t o_el = o_len + al256(8 * m), o_enc = al256(o_el + (size_t)m * D);
+        const size_t o_el = o_len + al256(8 * m);
+        const size_t el_bytes = device_src ? 0 : (size_t)m * D;
+        const size_t o_enc = al256(o_el + el_bytes);
         const size_t out_bytes = (size_t)m * cap + al256(8 * m) + al256(4 * m);
-        hipError_t e = sl.grow(o_el + (size_t)m * D, out_bytes, o_enc + (size_t)m * cap);
+        hipError_t e = sl.grow(o_el + el_bytes, out_bytes, o_enc + (size_t)m * cap);
         if (e != hipSuccess) { fail(e, "store staging"); break; }
         uint8_t* hb = (uint8_t*)sl.h_in;
         uint8_t* db = (uint8_t*)sl.d_buf;
         zcg_chunk* hd = (zcg_chunk*)hb;
-        pfor(io_threads, m, [&](size_t k) {
-            if (D) memcpy(hb + o_el + k * D, elems[i0 + k], D);
-            hd[k].src = db + o_el + k * D;
+        pool.run(io_threads, m, [&](size_t k) {
+            if (!device_src && D) memcpy(hb + o_el + k * D, elems[i0 + k], D);
+            hd[k].src = device_src ? elems[i0 + k] : (const void*)(db + o_el + k * D);
             hd[k].src_len = D;
             hd[k].dst = db + o_enc + k * cap;
             hd[k].dst_cap = cap;
         });
-        e = hipMemcpyAsync(db, hb, o_el + (size_t)m * D, hipMemcpyHostToDevice, sl.stream);
+        e = hipMemcpyAsync(db, hb, o_el + el_bytes, hipMemcpyHostToDevice, sl.stream);
         if (e != hipSuccess) { fail(e, "store H2D"); break; }
         const int r = zcg_encode_batch(ctx, a, (const zcg_chunk*)db, m, (uint64_t*)(db + o_len),
                                        (int32_t*)(db + o_st), (void*)sl.stream);
@@ -381,6 +485,29 @@ extern "C" int zcg_store_write_chunks(zcg_ctx* ctx, const zcg_array* a, uint32_t
             else { (void)hipEventSynchronize(S->s[b & 1].done); S->s[b & 1].pending = false; }
         }
     return rc;
+}
+
+}  // namespace
+
+extern "C" int zcg_store_read_chunks(zcg_ctx* ctx, const zcg_array* a, uint32_t n, const char* const* paths,
+                                     void* const* dsts, int32_t* status, uint32_t io_threads) {
+    return store_read_impl(ctx, a, n, paths, dsts, status, io_threads, false);
+}
+
+extern "C" int zcg_store_read_chunks_device(zcg_ctx* ctx, const zcg_array* a, uint32_t n, const char* const* paths,
+                                            void* const* d_dsts, int32_t* status, uint32_t io_threads) {
+    return store_read_impl(ctx, a, n, paths, d_dsts, status, io_threads, true);
+}
+
+extern "C" int zcg_store_write_chunks(zcg_ctx* ctx, const zcg_array* a, uint32_t n, const char* const* paths,
+                                      const void* const* elems, int32_t* status, uint32_t io_threads) {
+    return store_write_impl(ctx, a, n, paths, elems, status, io_threads, false);
+}
+
+extern "C" int zcg_store_write_chunks_device(zcg_ctx* ctx, const zcg_array* a, uint32_t n,
+                                             const char* const* paths, const void* const* d_elems,
+                                             int32_t* status, uint32_t io_threads) {
+    return store_write_impl(ctx, a, n, paths, d_elems, status, io_threads, true);
 }
 
 // ---- multi-GPU: chunk i -> devices[i mod G], one host thread

@@ -16,7 +16,7 @@ from typing import List, Sequence
 import numpy as np
 
 from . import _native
-from .batch import BatchCodec, PackedStreams
+from .batch import BatchCodec
 from .chunk import ZarrIOError, _raise_status, check_array_type
 from .metadata import ArrayMetadata
 
@@ -139,35 +139,32 @@ WRITE_BATCH_BYTES = 1 << 30
 
 
 def _decode_visited(hier, path_name: str, meta: ArrayMetadata, bbox: BoundingBox, device: int):
-    """Read + batch-decode the chunks bounded_coord_iter visits; returns
-    (table tensor, keep-alive objects)."""
+    """Read + batch-decode the chunks bounded_coord_iter visits, through the
+    store's get() semantics (shared flock, filesystem.rs:201-210) straight
+    into device slots (zcg_store_read_chunks_device); returns (table tensor,
+    keep-alive objects).  An absent chunk is skipped (ndarray.rs:229-231)."""
     import torch
+    from .storage import store_read_device
     lo, n = region_grid(meta, bbox)
     coords = list(itertools.product(*[range(l, l + k) for l, k in zip(lo, n)]))  # C order
-    bufs, idx = [], []
-    for i, c in enumerate(coords):
+    for c in coords:
         assert meta.in_bounds(c)  # storage.rs:217 (read_chunk panics out of bounds)
-        p = hier.chunk_path(path_name, meta, c)
-        try:
-            with open(p, "rb") as f:
-                bufs.append(f.read())
-            idx.append(i)
-        except FileNotFoundError:
-            pass  # read_chunk -> Ok(None): the chunk is skipped (ndarray.rs:229-231)
     dev = torch.device("cuda", device)
     table = np.zeros(max(len(coords), 1), np.int64)
     keep = []
-    if bufs:
+    if coords:
         es = meta.effective_type().size_of()
         D = meta.get_chunk_num_elements() * es
-        packed = PackedStreams(bufs, D, dev)
-        BatchCodec(device).decode(meta, packed)
-        st = packed.status.cpu().numpy()
-        for k, i in enumerate(idx):
-            if st[k] != 0:
-                raise ZarrIOError(_native.STATUS_NAMES.get(int(st[k]), str(st[k])), f"chunk {list(coords[i])}")
-            table[i] = packed.dst.data_ptr() + k * D
-        keep.append(packed)
+        slots = torch.empty(max(len(coords) * D, 1), dtype=torch.uint8, device=dev)
+        ptrs = [slots.data_ptr() + i * D for i in range(len(coords))]
+        st = store_read_device(meta, [hier.chunk_path(path_name, meta, c) for c in coords], ptrs, device)
+        for i, c in enumerate(coords):
+            if st[i] == _native.ABSENT:
+                continue  # read_chunk -> Ok(None)
+            if st[i] != _native.OK:
+                raise ZarrIOError(_native.STATUS_NAMES.get(int(st[i]), str(st[i])), f"chunk {list(c)}")
+            table[i] = ptrs[i]
+        keep.append(slots)
     return torch.from_numpy(table).to(dev), keep
 
 
@@ -223,9 +220,9 @@ def write_ndarray(hier, path_name: str, meta: ArrayMetadata, offset: Sequence[in
     """ZarrNdarrayWriter::write_ndarray (ndarray.rs:276-385) on the GPU: the
     chunks the box touches are read and decoded when only partly covered
     (absent ones start as fill value), the box is scattered into them by
-    zcg_write_region, and all of them are encoded in one batch and written."""
+    zcg_write_region, and all of them are encoded in one batch and written
+    through the store's set() semantics (filesystem.rs:260-280)."""
     import torch
-    from .batch import make_encode_batch
     if array.ndim != meta.get_ndim():
         raise ZarrIOError("InvalidData", "Wrong number of dimensions")
     dt = array.dtype.newbyteorder("=")
@@ -253,64 +250,49 @@ def write_ndarray(hier, path_name: str, meta: ArrayMetadata, offset: Sequence[in
 
 
 def _write_sub_batch(hier, path_name, meta, bbox, coords, b0, b1, dt, D, N, cap, box, ctx, r, h, codec, dev):
-    """write_ndarray for coords[b0:b1]: read/decode the partly covered chunks,
-    scatter the box into all of them, encode, write each chunk's bytes."""
+    """write_ndarray for coords[b0:b1]: read/decode the partly covered chunks
+    into their slots (store get(): shared flock), scatter the box into all of
+    them, encode and write every chunk file through the store's set()
+    (zcg_store_write_chunks_device: exclusive flock, then truncate)."""
     import torch
-    from .batch import make_encode_batch
+    from .storage import store_read_device, store_write_device
     cs = meta.get_chunk_shape()
     m = b1 - b0
     slots = torch.empty(m * D, dtype=torch.uint8, device=dev)
-    partial_bufs, partial_idx, absent_idx = [], [], []
+    ptrs = [slots.data_ptr() + i * D for i in range(m)]
+    paths = [hier.chunk_path(path_name, meta, coords[b0 + i]) for i in range(m)]
+    partial = []
     for i in range(m):
         c = coords[b0 + i]
         assert meta.in_bounds(c)  # storage.rs:217
         nom = BoundingBox([ci * s for ci, s in zip(c, cs)], cs)
         wb = BoundingBox(nom.offset, nom.shape)
         wb.intersect(bbox)
-        if wb == nom:
-            continue  # fully overwritten: no read (ndarray.rs:328-337)
-        p = hier.chunk_path(path_name, meta, c)
-        try:
-            with open(p, "rb") as f:
-                partial_bufs.append(f.read())
-            partial_idx.append(i)
-        except FileNotFoundError:
-            absent_idx.append(i)  # starts as fill value (ndarray.rs:357-368)
-    if partial_bufs:
-        packed = PackedStreams(partial_bufs, D, dev)
-        codec.decode(meta, packed)
-        st = packed.status.cpu().numpy()
-        for k, i in enumerate(partial_idx):
-            if st[k] != 0:
+        if wb != nom:
+            partial.append(i)  # fully overwritten chunks are not read (ndarray.rs:328-337)
+    absent = []
+    if partial:
+        st = store_read_device(meta, [paths[i] for i in partial], [ptrs[i] for i in partial], ctx.device)
+        for k, i in enumerate(partial):
+            if st[k] == _native.ABSENT:
+                absent.append(i)  # starts as fill value (ndarray.rs:357-368)
+            elif st[k] != _native.OK:
                 raise ZarrIOError(_native.STATUS_NAMES.get(int(st[k]), str(st[k])), f"chunk {list(coords[b0 + i])}")
-            slots[i * D:(i + 1) * D].copy_(packed.dst[k * D:(k + 1) * D])
-        del packed
-    if absent_idx:
+    if absent:
         fill = np.full(N, 0 if meta.fill_value is None else meta.fill_value, dtype=dt)
         ft = torch.from_numpy(fill.view(np.uint8)).to(dev)
-        for i in absent_idx:
+        for i in absent:
             slots[i * D:(i + 1) * D].copy_(ft)
     # the region call covers the whole grid range: chunks outside this
     # sub-batch get NULL slots and are skipped
     table_h = np.zeros(len(coords), np.int64)
-    table_h[b0:b1] = slots.data_ptr() + np.arange(m, dtype=np.int64) * D
+    table_h[b0:b1] = ptrs
     table = torch.from_numpy(table_h).to(dev)
     _raise_status(ctx.lib.zcg_write_region(ctx.handle, ctypes.byref(r), table.data_ptr(), box.data_ptr(), h),
                   ctx, "write_region")
-    desc, dst, out_len, status = make_encode_batch(slots, m, cap, dev)
-    codec.encode(meta, desc, m, out_len, status)
-    torch.cuda.synchronize(dev)
-    st = status.cpu().numpy()
-    ol = out_len.cpu().numpy().astype(np.int64)
+    torch.cuda.synchronize(dev)  # the store's streams read the slots next
+    st = store_write_device(meta, paths, ptrs, ctx.device)
     bad = np.nonzero(st != 0)[0]
     if len(bad):
         i = int(bad[0])
         raise ZarrIOError(_native.STATUS_NAMES.get(int(st[i]), str(st[i])), f"chunk {list(coords[b0 + i])}")
-    # only each chunk's encoded bytes cross to the host, compacted on the device
-    packed_out = torch.cat([dst[i * cap:i * cap + int(ol[i])] for i in range(m)]).cpu().numpy()
-    starts = np.concatenate([[0], np.cumsum(ol)])
-    for i in range(m):
-        p = hier.chunk_path(path_name, meta, coords[b0 + i])
-        os.makedirs(os.path.dirname(p), exist_ok=True)
-        with open(p, "wb") as f:
-            f.write(packed_out[starts[i]:starts[i + 1]].tobytes())

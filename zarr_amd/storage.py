@@ -113,7 +113,13 @@ class FilesystemHierarchy:
         if got is None:
             return None
         chunk.grid_position = list(grid_position)
-        chunk.data = got.get_data()
+        new = got.get_data()
+        old = chunk.data
+        if isinstance(old, np.ndarray) and old.shape == new.shape and old.dtype == new.dtype \
+                and old.flags.writeable:
+            np.copyto(old, new)  # the caller's buffer is filled in place (read_chunk_into)
+        else:
+            chunk.data = new
         return True
 
     def read_chunks(self, path_name: str, array_meta: ArrayMetadata, grid_positions, t,
@@ -176,14 +182,34 @@ def _cstrs(paths):
     return arr, enc
 
 
-def store_read(array_meta: ArrayMetadata, paths: Sequence[str], t, device: int = 0, io_threads: int = 16):
-    """zcg_store_read_chunks: (list of element arrays, status array)."""
+# batches at least this large land in page-locked host memory, which the
+# store fills by direct D2H copies (no staging copy, no first-touch faults)
+PINNED_MIN_BYTES = 64 << 20
+
+
+def _host_buffer(nbytes: int, pinned: bool) -> np.ndarray:
+    if pinned:
+        try:
+            import torch
+            return torch.empty(max(nbytes, 1), dtype=torch.uint8, pin_memory=True).numpy()
+        except Exception:
+            pass
+    return np.empty(max(nbytes, 1), np.uint8)
+
+
+def store_read(array_meta: ArrayMetadata, paths: Sequence[str], t, device: int = 0, io_threads: int = 16,
+               pinned=None):
+    """zcg_store_read_chunks: (list of element arrays, status array).  The
+    arrays are views of one host allocation, page-locked for large batches."""
     check_array_type(t, array_meta)
     ctx = _native.context(device)
     n = len(paths)
     dt = np.dtype(t).newbyteorder("=")
     N = array_meta.get_chunk_num_elements()
-    buf = np.empty(max(n * N, 1), dt)  # one allocation (large pages when the kernel offers them)
+    nbytes = n * N * dt.itemsize
+    if pinned is None:
+        pinned = nbytes >= PINNED_MIN_BYTES
+    buf = _host_buffer(nbytes, pinned)[:max(nbytes, dt.itemsize)].view(dt)
     arrs = [buf[i * N:(i + 1) * N] for i in range(n)]
     dp = (ctypes.c_void_p * max(n, 1))(*[a.ctypes.data for a in arrs])
     cp, keep = _cstrs(paths)
@@ -219,3 +245,49 @@ def store_write(array_meta: ArrayMetadata, paths: Sequence[str], datas, device: 
     if r != _native.OK:
         raise ZarrIOError(_native.STATUS_NAMES.get(r, str(r)), f"store_write_chunks: {ctx.last_error()}")
     return st[:n]
+
+
+def store_read_device(array_meta: ArrayMetadata, paths: Sequence[str], d_ptrs: Sequence[int], device: int = 0,
+                      io_threads: int = 16):
+    """zcg_store_read_chunks_device: chunk files (shared flock, reader pool,
+    pinned staging) decoded straight into the device slots `d_ptrs`
+    (N*elem_size bytes each); returns the status array."""
+    ctx = _native.context(device)
+    n = len(paths)
+    dp = (ctypes.c_void_p * max(n, 1))(*[int(p) for p in d_ptrs])
+    cp, keep = _cstrs(paths)
+    st = np.zeros(max(n, 1), np.int32)
+    arr = abi_array(array_meta)
+    r = ctx.lib.zcg_store_read_chunks_device(ctx.handle, ctypes.byref(arr), n, ctypes.addressof(cp),
+                                             ctypes.addressof(dp), st.ctypes.data, io_threads)
+    if r != _native.OK:
+        raise ZarrIOError(_native.STATUS_NAMES.get(r, str(r)), f"store_read_chunks_device: {ctx.last_error()}")
+    return st[:n]
+
+
+def store_write_device(array_meta: ArrayMetadata, paths: Sequence[str], d_ptrs: Sequence[int], device: int = 0,
+                       io_threads: int = 16):
+    """zcg_store_write_chunks_device: the device element slots `d_ptrs`
+    encoded on the GPU and written as set() does (exclusive flock, truncate
+    after the lock); returns the status array."""
+    ctx = _native.context(device)
+    n = len(paths)
+    dp = (ctypes.c_void_p * max(n, 1))(*[int(p) for p in d_ptrs])
+    cp, keep = _cstrs(paths)
+    st = np.zeros(max(n, 1), np.int32)
+    arr = abi_array(array_meta)
+    r = ctx.lib.zcg_store_write_chunks_device(ctx.handle, ctypes.byref(arr), n, ctypes.addressof(cp),
+                                              ctypes.addressof(dp), st.ctypes.data, io_threads)
+    if r != _native.OK:
+        raise ZarrIOError(_native.STATUS_NAMES.get(r, str(r)), f"store_write_chunks_device: {ctx.last_error()}")
+    return st[:n]
+
+
+def chunk_key_native(base_path: str, separator: str, grid_position: Sequence[int]) -> str:
+    """zcg_chunk_key (the C-ABI restatement of get_chunk_key, storage.rs:109-127)."""
+    L = _native.load_library()
+    g = (ctypes.c_uint64 * max(len(grid_position), 1))(*[int(x) for x in grid_position])
+    need = L.zcg_chunk_key(base_path.encode(), separator.encode(), ctypes.addressof(g), len(grid_position), None, 0)
+    out = ctypes.create_string_buffer(int(need) + 1)
+    L.zcg_chunk_key(base_path.encode(), separator.encode(), ctypes.addressof(g), len(grid_position), out, need + 1)
+    return out.value.decode()
