@@ -65,9 +65,9 @@ codec.decode(meta, packed, flags=_native.FLAG_DEBUG_COUNTERS)
 torch.cuda.synchronize()
 fn(out.ctypes.data, 1)
 names = {0: "rounds", 1: "blocks", 2: "stages", 3: "groups", 4: "p1_lane_it", 5: "p2_lane_it", 6: "chain",
-         7: "tokens", 8: "bytes", 9: "jump_passes", 10: "caps", 11: "rounds_no_eob",
-         16: "cyc_hdr", 17: "cyc_p1", 18: "cyc_p2", 19: "cyc_chain", 20: "cyc_heads", 21: "cyc_expand",
-         22: "cyc_gather", 23: "cyc_jump", 24: "cyc_commit", 25: "cyc_total"}
+         7: "jump_passes", 8: "caps", 9: "rounds_no_eob", 10: "cyc_hdr", 11: "cyc_p1", 12: "cyc_p2",
+         13: "cyc_chain", 14: "cyc_heads", 15: "cyc_expand", 16: "cyc_gather", 17: "cyc_jump", 18: "cyc_commit",
+         19: "cyc_total"}
 d = {v: int(out[k]) for k, v in names.items()}
 res["per_chunk"] = {k: round(v / packed.n, 1) for k, v in d.items()}
 cyc = {k: v for k, v in d.items() if k.startswith("cyc_") and k != "cyc_total"}

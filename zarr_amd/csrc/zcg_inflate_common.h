@@ -343,7 +343,10 @@ __device__ __forceinline__ int decode_sym(BitIn& b, const u32* tab, int root, u3
     return R_OK;
 }
 
+// Table geometry: literal/length root bits + table capacity, distance root
+// bits + capacity (defaults: the serial and 256-lane kernels' 10/8-bit roots).
 // Dynamic block header (RFC 1951 3.2.7) -> tables; zlib's validity rules.
+template <int LB = INF_LBITS, u32 LCAP = INF_LTAB, int DB = INF_DBITS, u32 DCAP = INF_DTAB>
 __device__ __attribute__((always_inline)) int read_dynamic(BitIn& b, u8* lens, HuffLds* lh, u32* ltab, HuffLds* dh, u32* dtab) {
     const u32 tid = threadIdx.x, nth = blockDim.x;
     if (!bi_has(b, 14)) return R_EXHAUSTED;
@@ -363,7 +366,7 @@ __device__ __attribute__((always_inline)) int read_dynamic(BitIn& b, u8* lens, H
     __syncthreads();
     for (u32 i = tid; i < 19; i += nth) lens[i] = cl[i];
     __syncthreads();
-    build_table(lens, 19, lh, ltab, 7, false, INF_LTAB);
+    build_table(lens, 19, lh, ltab, 7, false, LCAP);
     u32 idx = 0;
     u8 prev = 0;
     while (idx < nlen + ndist) {
@@ -405,25 +408,27 @@ __device__ __attribute__((always_inline)) int read_dynamic(BitIn& b, u8* lens, H
     if (tid < 32) lens[288 + tid] = tid < ndist ? dl : 0;
     __syncthreads();
     if (lens[256] == 0) return R_INVALID;  // "invalid code -- missing end-of-block"
-    if (build_table(lens, 288, lh, ltab, INF_LBITS, false, INF_LTAB) != 0) return R_INVALID;
-    if (build_table(lens + 288, 30, dh, dtab, INF_DBITS, true, INF_DTAB) != 0) return R_INVALID;
+    if (build_table(lens, 288, lh, ltab, LB, false, LCAP) != 0) return R_INVALID;
+    if (build_table(lens + 288, 30, dh, dtab, DB, true, DCAP) != 0) return R_INVALID;
     return R_OK;
 }
 
+template <int LB = INF_LBITS, u32 LCAP = INF_LTAB, int DB = INF_DBITS, u32 DCAP = INF_DTAB>
 __device__ void fixed_tables(u8* lens, HuffLds* lh, u32* ltab, HuffLds* dh, u32* dtab) {
     const u32 tid = threadIdx.x, nth = blockDim.x;
     __syncthreads();
     for (u32 i = tid; i < 320; i += nth)
         lens[i] = i < 144 ? 8 : i < 256 ? 9 : i < 280 ? 7 : i < 288 ? 8 : 5;
     __syncthreads();
-    build_table(lens, 288, lh, ltab, INF_LBITS, false, INF_LTAB);
+    build_table(lens, 288, lh, ltab, LB, false, LCAP);
     // all 32 five-bit distance codes (30 and 31 decode as invalid), as zlib
     // builds the fixed table: the 30-symbol code alone would be incomplete
-    build_table(lens + 288, 32, dh, dtab, INF_DBITS, true, INF_DTAB);
+    build_table(lens + 288, 32, dh, dtab, DB, true, DCAP);
 }
 
 // Block header: 3 bits, then stored-length check / table construction.
 // *type receives BTYPE; for stored blocks *slen the LEN field.
+template <int LB = INF_LBITS, u32 LCAP = INF_LTAB, int DB = INF_DBITS, u32 DCAP = INF_DTAB>
 __device__ __attribute__((always_inline)) int read_block_header(BitIn& b, bool* last, u32* type, u32* slen, u8* lens, HuffLds* lh,
                                  u32* ltab, HuffLds* dh, u32* dtab) {
     if (!bi_has(b, 3)) return R_EXHAUSTED;
@@ -440,8 +445,8 @@ __device__ __attribute__((always_inline)) int read_block_header(BitIn& b, bool* 
         return R_OK;
     }
     if (*type == 3) return R_INVALID;  // "invalid block type"
-    if (*type == 1) { fixed_tables(lens, lh, ltab, dh, dtab); return R_OK; }
-    return read_dynamic(b, lens, lh, ltab, dh, dtab);
+    if (*type == 1) { fixed_tables<LB, LCAP, DB, DCAP>(lens, lh, ltab, dh, dtab); return R_OK; }
+    return read_dynamic<LB, LCAP, DB, DCAP>(b, lens, lh, ltab, dh, dtab);
 }
 
 // zlib keeps decoding after the output is full until it needs to emit a
@@ -449,6 +454,7 @@ __device__ __attribute__((always_inline)) int read_block_header(BitIn& b, bool* 
 // next literal/length code, length extra bits, distance code, distance
 // extra bits, and whole block headers are validated.  The input it was
 // given is the rest of flate2's current 32 KiB BufReader window.
+template <int LB = INF_LBITS, u32 LCAP = INF_LTAB, int DB = INF_DBITS, u32 DCAP = INF_DTAB>
 __device__ __attribute__((always_inline)) int inf_lookahead(BitIn& b, bool last, bool at_header, u8* lens, HuffLds* lh,
                              u32* ltab, HuffLds* dh, u32* dtab) {
     for (;;) {
@@ -456,7 +462,7 @@ __device__ __attribute__((always_inline)) int inf_lookahead(BitIn& b, bool last,
             at_header = false;
             if (last) return R_OK;
             u32 type = 0, slen = 0;
-            int r = read_block_header(b, &last, &type, &slen, lens, lh, ltab, dh, dtab);
+            int r = read_block_header<LB, LCAP, DB, DCAP>(b, &last, &type, &slen, lens, lh, ltab, dh, dtab);
             if (r != R_OK) return r;
             if (type == 0) {
                 if (slen != 0) return R_OK;
@@ -465,7 +471,7 @@ __device__ __attribute__((always_inline)) int inf_lookahead(BitIn& b, bool last,
             }
         }
         u32 e;
-        int r = decode_sym(b, ltab, INF_LBITS, &e);
+        int r = decode_sym(b, ltab, LB, &e);
         if (r != R_OK) return r;
         const u32 kind = (e >> 24) & 15;
         if (kind == K_LIT) return R_OK;
@@ -475,7 +481,7 @@ __device__ __attribute__((always_inline)) int inf_lookahead(BitIn& b, bool last,
             if (!bi_has(b, ex)) return R_EXHAUSTED;
             if (ex) bi_bits(b, ex);
             u32 de;
-            r = decode_sym(b, dtab, INF_DBITS, &de);
+            r = decode_sym(b, dtab, DB, &de);
             if (r != R_OK) return r;
             if (((de >> 24) & 15) != K_DIST) return R_INVALID;  // "invalid distance code"
             return R_OK;  // DISTEXT then MATCH: zlib leaves there (left == 0)
@@ -484,7 +490,7 @@ __device__ __attribute__((always_inline)) int inf_lookahead(BitIn& b, bool last,
         for (;;) {
             if (last) return R_OK;  // stream end
             u32 type = 0, slen = 0;
-            r = read_block_header(b, &last, &type, &slen, lens, lh, ltab, dh, dtab);
+            r = read_block_header<LB, LCAP, DB, DCAP>(b, &last, &type, &slen, lens, lh, ltab, dh, dtab);
             if (r != R_OK) return r;
             if (type != 0) break;         // decode symbols of the new block
             if (slen != 0) return R_OK;   // COPY with left == 0: leave

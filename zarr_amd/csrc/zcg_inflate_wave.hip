@@ -48,7 +48,7 @@
 #define ZIW_TCAP 768
 #endif
 #ifndef ZIW_WPE
-#define ZIW_WPE 3
+#define ZIW_WPE 4
 #endif
 #ifndef ZIW_EST_PCT
 #define ZIW_EST_PCT 108
@@ -91,30 +91,40 @@ constexpr u32 IE_VAL = 0xFF00u;
 constexpr u32 IE_FAR = 0x4000u;
 static_assert(IW_S <= IE_FAR && IE_FAR + 32768 <= IE_VAL, "stage entry encoding");
 
+// Table geometry: a 9-bit literal/length root (zlib's ENOUGH_LENS = 852
+// entries covers every complete code) and an 8-bit distance root, so the LDS
+// footprint allows 16 chunks per CU.
+constexpr int W_LB = 9;
+constexpr u32 W_LCAP = 852;
+constexpr int W_DB = 8;
+constexpr u32 W_DCAP = 432;  // >= enough(30, 8, 15) = 402
+
+constexpr u32 IW_NDBG = 20;
 __device__ unsigned long long g_iw_dbg[32];
-enum { IWD_ROUNDS, IWD_BLOCKS, IWD_STAGES, IWD_GROUPS, IWD_P1_IT, IWD_P2_IT, IWD_CHAIN, IWD_TOKENS,
-       IWD_BYTES, IWD_MRR, IWD_CAPS, IWD_NOEOB,
-       IWT_HDR = 16, IWT_P1, IWT_P2, IWT_CHAIN, IWT_HEADS, IWT_EXPAND, IWT_GATHER, IWT_JUMP, IWT_COMMIT,
-       IWT_TOTAL };
+enum { IWD_ROUNDS, IWD_BLOCKS, IWD_STAGES, IWD_GROUPS, IWD_P1_IT, IWD_P2_IT, IWD_CHAIN, IWD_MRR, IWD_CAPS,
+       IWD_NOEOB, IWT_HDR, IWT_P1, IWT_P2, IWT_CHAIN, IWT_HEADS, IWT_EXPAND, IWT_GATHER, IWT_JUMP,
+       IWT_COMMIT, IWT_TOTAL };
+static_assert(IWT_TOTAL < IW_NDBG, "debug slots");
 
 struct IwLds {
-    u32 ltab[INF_LTAB];
-    u32 dtab[INF_DTAB];
+    u32 ltab[W_LCAP];
+    u32 dtab[W_DCAP];
     union {
         struct {  // block headers and the look-ahead (wave-uniform reader)
             HuffLds lh, dh;
             u8 lens[320];
             u32 bcache[BI_CACHE_WORDS];
         } h;
-        struct {  // L phase: the stage ring and its token-start bits (one word per lane block)
+        u32 mlim[65];  // H round: marked extent (bits) of each segment
+        struct {       // L phase: the stage ring, its token-start bits (one word per lane block), the chain
             u16 ptr[IW_S];
             u32 head[IW_S / 32];
+            u16 ch_lane[65], ch_s[65], ch_e[65];  // chain members: lane, first valid token, list length
         } st;
     } u;
-    u16 ch_lane[65], ch_s[65], ch_e[65];  // chain members: lane, first valid token, list length
-    u32 mlim[65];                         // marked extent (bits) of each segment
-    u32 dbgc[32];
+    u32 dbgc[IW_NDBG];
 };
+static_assert(sizeof(IwLds) + 32 <= 10240, "16 chunks per CU");
 
 // wave-local ordering point for LDS (and the compiler): a wave's LDS
 // operations are performed in issue order, so a fence at wavefront scope is
@@ -211,15 +221,15 @@ __device__ __forceinline__ void gb_init(GBits& s, const u8* base, u32 nvec, u32 
 // Decode one token from >= 48 valid bits: both table lookups always run, so
 // lanes holding different token kinds do not serialise.
 __device__ __forceinline__ u32 iw_decode(const IwLds& L, u64 v, u32* adv) {
-    u32 e = L.ltab[(u32)v & ((1u << INF_LBITS) - 1)];
+    u32 e = L.ltab[(u32)v & ((1u << W_LB) - 1)];
     if (((e >> 24) & 15) == K_SUB)
-        e = L.ltab[(e & 0xFFFF) + (((u32)v >> INF_LBITS) & ((1u << ((e >> 16) & 0xFF)) - 1))];
+        e = L.ltab[(e & 0xFFFF) + (((u32)v >> W_LB) & ((1u << ((e >> 16) & 0xFF)) - 1))];
     const u32 l = e >> 28, kind = (e >> 24) & 15, ex = (e >> 16) & 0xFF;
     const u32 t = l + ex;
     const u64 vd = v >> t;
-    u32 de = L.dtab[(u32)vd & ((1u << INF_DBITS) - 1)];
+    u32 de = L.dtab[(u32)vd & ((1u << W_DB) - 1)];
     if (((de >> 24) & 15) == K_SUB)
-        de = L.dtab[(de & 0xFFFF) + (((u32)vd >> INF_DBITS) & ((1u << ((de >> 16) & 0xFF)) - 1))];
+        de = L.dtab[(de & 0xFFFF) + (((u32)vd >> W_DB) & ((1u << ((de >> 16) & 0xFF)) - 1))];
     const u32 dl = de >> 28, dex = (de >> 16) & 0xFF;
     const u32 len = (e & 0xFFFF) + ((u32)(v >> l) & ((1u << ex) - 1));
     const u32 dist = (de & 0xFFFF) + ((u32)(vd >> dl) & ((1u << dex) - 1));
@@ -309,18 +319,29 @@ __device__ __forceinline__ int iw_incl_max(int v) {
     return lane < 16 ? v : max(v, lane < 32 ? t0 : (lane < 48 ? t1 : t2));
 }
 
-__device__ __forceinline__ u32 e16(const u32x4* r, u32 k) {  // entry k of a lane block held in 4 x u32x4
-    const u32x4 q = r[k >> 3];
-    const u32 w = ((k >> 1) & 3) == 0 ? q.x : ((k >> 1) & 3) == 1 ? q.y : ((k >> 1) & 3) == 2 ? q.z : q.w;
-    return (k & 1) ? (w >> 16) : (w & 0xFFFF);
+__device__ __forceinline__ u32 swap_pos32(u32 p, const DType& t) {
+    if (!t.swap) return p;
+    const u32 m = t.es - 1;
+    return (p & ~m) | (m - (p & m));
 }
-__device__ __forceinline__ void e16_set(u32x4* r, u32 k, u32 v) {
-    u32x4 q = r[k >> 3];
-    const u32 j = (k >> 1) & 3;
-    u32 w = j == 0 ? q.x : j == 1 ? q.y : j == 2 ? q.z : q.w;
-    w = (k & 1) ? ((w & 0xFFFFu) | (v << 16)) : ((w & 0xFFFF0000u) | (v & 0xFFFFu));
-    if (j == 0) q.x = w; else if (j == 1) q.y = w; else if (j == 2) q.z = w; else q.w = w;
-    r[k >> 3] = q;
+
+// entry k of a lane block held as 16 u32 (two u16 entries each)
+__device__ __forceinline__ u32 e16(const u32* w, u32 k) { return (k & 1) ? (w[k >> 1] >> 16) : (w[k >> 1] & 0xFFFFu); }
+__device__ __forceinline__ void e16_set(u32* w, u32 k, u32 v) {
+    w[k >> 1] = (k & 1) ? ((w[k >> 1] & 0xFFFFu) | (v << 16)) : ((w[k >> 1] & 0xFFFF0000u) | (v & 0xFFFFu));
+}
+__device__ __forceinline__ void blk_load(u32* w, const u16* p) {
+    const u32x4* q = (const u32x4*)p;
+#pragma unroll
+    for (u32 i = 0; i < 4; i++) {
+        const u32x4 x = q[i];
+        w[4 * i] = x.x; w[4 * i + 1] = x.y; w[4 * i + 2] = x.z; w[4 * i + 3] = x.w;
+    }
+}
+__device__ __forceinline__ void blk_store(u16* p, const u32* w) {
+    u32x4* q = (u32x4*)p;
+#pragma unroll
+    for (u32 i = 0; i < 4; i++) q[i] = u32x4{w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]};
 }
 
 constexpr u32 IW_NSLOT_MAX = 8192;
@@ -347,7 +368,7 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
     const u64 n_in = ch.src_len;
     u64 h = 0;
     int st = gzip_header(s, n_in, &h);
-    if (st == ZCG_OK && n_in - h >= (1ull << 28)) st = ZCG_ERR_UNSUPPORTED;  // u32 bit positions
+    if (st == ZCG_OK && (n_in - h >= (1ull << 28) || D >= (1ull << 32))) st = ZCG_ERR_UNSUPPORTED;  // u32 positions
     if (st != ZCG_OK) { if (lane == 0) status[c] = st; return; }
 
     u8* dst = (u8*)ch.dst;
@@ -381,7 +402,7 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
     int r = R_OK;
     u32 est = IW_EST0;
     if (dbg) {
-        if (lane < 32) L.dbgc[lane] = 0;
+        if (lane < IW_NDBG) L.dbgc[lane] = 0;
         wsync();
     }
     u64 t_last = __builtin_readcyclecounter();
@@ -393,7 +414,8 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
         u32 type = 0, slen = 0;
         b.cbase = ~0ull;  // the reader's LDS cache shares storage with the stage
         wsync();
-        r = read_block_header(b, &last, &type, &slen, L.u.h.lens, &L.u.h.lh, L.ltab, &L.u.h.dh, L.dtab);
+        r = read_block_header<W_LB, W_LCAP, W_DB, W_DCAP>(b, &last, &type, &slen, L.u.h.lens, &L.u.h.lh, L.ltab,
+                                                          &L.u.h.dh, L.dtab);
         const u32 hdr_end = (u32)b.consumed;
         IW_T(IWT_HDR);
         if (r != R_OK) break;
@@ -478,18 +500,18 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
                 mk[cw + 2] = (u64)cpre << 32;
             }
             // marked extent: the whole segment, or up to where the lane stopped
-            L.mlim[lane] = !active ? 0u : nxt == S_NONE ? seg : (q - p) + (nxt == S_MARKER ? 1u : 0u);
-            if (lane == 0) L.mlim[64] = 0;
+            L.u.mlim[lane] = !active ? 0u : nxt == S_NONE ? seg : (q - p) + (nxt == S_MARKER ? 1u : 0u);
+            if (lane == 0) L.u.mlim[64] = 0;
             __syncthreads();  // every lane's marks and list are stored
             IW_T(IWT_P1);
             // pass 2: follow my path until it meets a token start a later lane marked
             u32 ks = lane + 1, pk = pend, it2 = 0;
-            u32 lim = L.mlim[ks];
+            u32 lim = L.u.mlim[ks];
             u32 cwi = 0xFFFFFFFFu;
             u64 cwv = 0;
             while (nxt == S_NONE) {
                 if (q >= round_hi) { nxt = S_ROUND_END; break; }
-                if (q >= pk + seg) { ks++; pk += seg; lim = L.mlim[ks]; cwi = 0xFFFFFFFFu; }
+                if (q >= pk + seg) { ks++; pk += seg; lim = L.u.mlim[ks]; cwi = 0xFFFFFFFFu; }
                 const u32 off = q - pk;
                 if (off < lim) {
                     const u32 wi = off >> 5;
@@ -530,7 +552,7 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
             for (;;) {
                 const u32 e = (u32)__builtin_amdgcn_readlane((int)nt, (int)cur);
                 const u32 nx = (u32)__builtin_amdgcn_readlane((int)nxt, (int)cur);
-                if (lane == 0) { L.ch_lane[ncm] = (u16)cur; L.ch_s[ncm] = (u16)sidx; L.ch_e[ncm] = (u16)e; }
+                if (lane == 0) { L.u.st.ch_lane[ncm] = (u16)cur; L.u.st.ch_s[ncm] = (u16)sidx; L.u.st.ch_e[ncm] = (u16)e; }
                 ncm++;
                 if (nx < 64) {
                     sidx = (u32)__builtin_amdgcn_readlane((int)give, (int)cur);
@@ -542,7 +564,7 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
             const u32 endq = (u32)__builtin_amdgcn_readlane((int)q, (int)cur);  // after the last member's list
             if ((u32)__builtin_amdgcn_readlane((int)nxt, (int)cur) == S_CAP && seg > IW_SEGMIN)
                 seg = (seg / 2 + 31) & ~31u;  // lists overflowed: shorter segments next round
-            if (lane == 0) { L.ch_lane[ncm] = 0; L.ch_s[ncm] = 0; L.ch_e[ncm] = 0; }
+            if (lane == 0) { L.u.st.ch_lane[ncm] = 0; L.u.st.ch_s[ncm] = 0; L.u.st.ch_e[ncm] = 0; }
             IW_ADD(IWD_CHAIN, ncm);
             // token lists of other lanes are read below: their stores must be done
             __syncthreads();
@@ -555,12 +577,12 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
             // lane's token at the cursor + lane (a member's list may end inside a group)
             auto fetch = [&](u32 cm0, u32 cj0) -> u32 {
                 u32 m = cm0, jj = cj0 + lane;
-                while (m < ncm && jj >= L.ch_e[m]) { jj = jj - L.ch_e[m] + L.ch_s[m + 1]; m++; }
-                return m < ncm ? (u32)gl[(u64)L.ch_lane[m] * IW_TCAP + jj] : (W_MARK | M_END);
+                while (m < ncm && jj >= L.u.st.ch_e[m]) { jj = jj - L.u.st.ch_e[m] + L.u.st.ch_s[m + 1]; m++; }
+                return m < ncm ? (u32)gl[(u64)L.u.st.ch_lane[m] * IW_TCAP + jj] : (W_MARK | M_END);
             };
             auto advance = [&](u32& cm0, u32& cj0, u32 k) {
                 cj0 += k;
-                while (cm0 < ncm && cj0 >= L.ch_e[cm0]) { cj0 = cj0 - L.ch_e[cm0] + L.ch_s[cm0 + 1]; cm0++; }
+                while (cm0 < ncm && cj0 >= L.u.st.ch_e[cm0]) { cj0 = cj0 - L.u.st.ch_e[cm0] + L.u.st.ch_s[cm0 + 1]; cm0++; }
             };
             u32 tk_next = fetch(cm, cj);
             bool round_done = false;
@@ -637,9 +659,8 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
                     int carry = iw_incl_max(lastpos);
                     carry = __shfl_up(carry, 1, 64);
                     if (lane == 0) carry = INT_MIN;
-                    u32x4 ev[4];
-                    const u32x4* lp = (const u32x4*)(L.u.st.ptr + rb);
-                    ev[0] = lp[0]; ev[1] = lp[1]; ev[2] = lp[2]; ev[3] = lp[3];
+                    u32 ev[16];
+                    blk_load(ev, L.u.st.ptr + rb);
                     int mo = 0;
                     u32 md = 0, mj = 0;
                     bool in_match = false;
@@ -672,50 +693,56 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
                     IW_T(IWT_EXPAND);
                     // far codes: bytes before the stage, from the committed output
                     if (__ballot(nfar != 0)) {
+                        const gu8* gd = (const gu8*)dst;
+                        const u32 S32 = (u32)S;
 #pragma unroll
-                        for (u32 half = 0; half < 2; half++) {
-                            u32 bv[16];
+                        for (u32 qt = 0; qt < 4; qt++) {
+                            u32 bv[8];
 #pragma unroll
-                            for (u32 u = 0; u < 16; u++) {
-                                const u32 v = e16(ev, half * 16 + u);
-                                const int xr = xr0 + (int)(half * 16 + u);
+                            for (u32 u = 0; u < 8; u++) {
+                                const u32 v = e16(ev, qt * 8 + u);
+                                const int xr = xr0 + (int)(qt * 8 + u);
                                 bv[u] = 0;
                                 if (xr >= 0 && xr < (int)emit && v >= IE_FAR && v < IE_VAL)
-                                    bv[u] = ((const gu8*)dst)[swap_pos(S - (v - IE_FAR + 1), tw)];
+                                    bv[u] = gd[swap_pos32(S32 - (v - IE_FAR + 1), tw)];
                             }
 #pragma unroll
-                            for (u32 u = 0; u < 16; u++) {
-                                const u32 v = e16(ev, half * 16 + u);
-                                const int xr = xr0 + (int)(half * 16 + u);
+                            for (u32 u = 0; u < 8; u++) {
+                                const u32 v = e16(ev, qt * 8 + u);
+                                const int xr = xr0 + (int)(qt * 8 + u);
                                 if (xr >= 0 && xr < (int)emit && v >= IE_FAR && v < IE_VAL)
-                                    e16_set(ev, half * 16 + u, IE_VAL | bv[u]);
+                                    e16_set(ev, qt * 8 + u, IE_VAL | bv[u]);
                             }
                         }
                     }
-                    u32x4* wp = (u32x4*)(L.u.st.ptr + rb);
-                    wp[0] = ev[0]; wp[1] = ev[1]; wp[2] = ev[2]; wp[3] = ev[3];
+                    blk_store(L.u.st.ptr + rb, ev);
                     wsync();
                     IW_T(IWT_GATHER);
                     // pointer jumping: every pointer points strictly backwards, so
                     // log2(IW_S) passes resolve any stage (the cap guards the invariant)
                     for (u32 pass = 0;; pass++) {
                         bool pending = false;
-                        u32 nw[32];
 #pragma unroll
-                        for (u32 k = 0; k < 32; k++) {
-                            const u32 v = e16(ev, k);
-                            const int xr = xr0 + (int)k;
-                            nw[k] = (xr >= 0 && xr < (int)emit && v < IW_S) ? (u32)L.u.st.ptr[v] : v;
-                        }
+                        for (u32 half = 0; half < 2; half++) {
+                            u32 nw[16];
 #pragma unroll
-                        for (u32 k = 0; k < 32; k++) {
-                            const int xr = xr0 + (int)k;
-                            if (xr >= 0 && xr < (int)emit && e16(ev, k) < IW_S) {
-                                e16_set(ev, k, nw[k]);
-                                pending |= nw[k] < IW_S;
+                            for (u32 u = 0; u < 16; u++) {
+                                const u32 k = half * 16 + u;
+                                const u32 v = e16(ev, k);
+                                const int xr = xr0 + (int)k;
+                                nw[u] = (xr >= 0 && xr < (int)emit && v < IW_S) ? (u32)L.u.st.ptr[v] : v;
+                            }
+#pragma unroll
+                            for (u32 u = 0; u < 16; u++) {
+                                const u32 k = half * 16 + u;
+                                const int xr = xr0 + (int)k;
+                                if (xr >= 0 && xr < (int)emit && e16(ev, k) < IW_S) {
+                                    e16_set(ev, k, nw[u]);
+                                    pending |= nw[u] < IW_S;
+                                }
                             }
                         }
-                        wp[0] = ev[0]; wp[1] = ev[1]; wp[2] = ev[2]; wp[3] = ev[3];
+                        blk_store(L.u.st.ptr + rb, ev);
                         IW_ADD(IWD_MRR, 1);
                         wsync();
                         if (__ballot(pending) == 0) break;
@@ -725,8 +752,7 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
                     if (r != R_OK) break;
                     iw_commit(L, dst, S, S + emit, tw);
                     P = S + emit;
-                    IW_ADD(IWD_BYTES, emit);
-                    IW_T(IWT_COMMIT);
+                                        IW_T(IWT_COMMIT);
                 }
                 if (why == 1) {
                     // output full: zlib's look-ahead continues at the first untaken token
@@ -735,7 +761,7 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
                     round_done = true;
                     if (boundary) {
                         u32 qn = endq;
-                        if (cm < ncm) qn = iw_pos(gl, L.ch_lane[cm], cj, R0 + L.ch_lane[cm] * seg);
+                        if (cm < ncm) qn = iw_pos(gl, L.u.st.ch_lane[cm], cj, R0 + L.u.st.ch_lane[cm] * seg);
                         b.cbase = ~0ull;
                         bi_seek(b, qn);
                     }
@@ -750,7 +776,7 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
                         u32 sg = (rem / 64 + 31) & ~31u;
                         seg = sg < IW_SEGMIN ? IW_SEGMIN : sg > IW_SEGMAX ? IW_SEGMAX : sg;
                     } else if (mcode == M_EOB) {
-                        const u32 lm = L.ch_lane[cm];
+                        const u32 lm = L.u.st.ch_lane[cm];
                         const u32 qe = iw_pos(gl, lm, cj + 1, R0 + lm * seg);  // after the EOB code
                         block_end = true;
                         b.cbase = ~0ull;
@@ -774,7 +800,8 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
         b.cbase = ~0ull;
         wsync();
         if (b.limit >= b.consumed) {
-            const int la = inf_lookahead(b, last, after_stored, L.u.h.lens, &L.u.h.lh, L.ltab, &L.u.h.dh, L.dtab);
+            const int la = inf_lookahead<W_LB, W_LCAP, W_DB, W_DCAP>(b, last, after_stored, L.u.h.lens, &L.u.h.lh,
+                                                                     L.ltab, &L.u.h.dh, L.dtab);
             if (la == R_INVALID) r = R_INVALID;
         }
     }
@@ -784,7 +811,7 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
     if (dbg) {
         if (lane == 0) L.dbgc[IWT_TOTAL] = (u32)(__builtin_readcyclecounter() - t_start);
         wsync();
-        if (lane < 32 && L.dbgc[lane]) atomicAdd(&g_iw_dbg[lane], (unsigned long long)L.dbgc[lane]);
+        if (lane < IW_NDBG && L.dbgc[lane]) atomicAdd(&g_iw_dbg[lane], (unsigned long long)L.dbgc[lane]);
     }
     __syncthreads();  // every workspace access of this wave is done
     if (lane == 0) {
