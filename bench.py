@@ -56,7 +56,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
 GIB = float(1 << 30)
 # The kernels one zcg_decode_batch call launches (kernel_ms and roofline.traffic
 # cover the whole sequence: HIP events around the call, PMC summed per call).
-KERNEL = {"gzip": "zcg::inflate_par_kernel", "lz4": "zcg::lz4_{frames,lanes,finish}_kernel",
+KERNEL = {"gzip": "zcg::inflate_wave_kernel", "lz4": "zcg::lz4_{frames,lanes,finish}_kernel",
           "raw": "zcg::raw_kernel", "xz": "zcg::xz_decode_kernel<{7990,14134}u, 4096u>",
           "bzip2": "zcg::bz2_{init,stage_a,stage_bc,decode}_kernel"}
 # per-codec leg shapes: pool of distinct chunks, chunks per rank (weak) or per job (strong)
