@@ -61,7 +61,11 @@ constexpr u32 IW_BLK = IW_S / 64;
 constexpr u32 IW_TCAP = ZIW_TCAP;
 constexpr u32 IW_SEGMIN = 128;   // bits per lane segment
 constexpr u32 IW_SEGMAX = 4096;
-constexpr u32 IW_MWORDS = IW_SEGMAX / 32 + 3;  // mark words per segment (+ the tail of the last token)
+constexpr u32 IW_K = 4;          // decode steps between staged-token / mark flushes
+constexpr u32 IW_KH = 2;         // flush periods per outer step (reader loads at its top, absorbs at its bottom)
+constexpr u32 IW_TSTR = IW_TCAP + IW_K;          // token list stride (a flush writes IW_K words)
+constexpr u32 IW_MWIN = 8;                       // mark words a lane keeps in LDS between flushes
+constexpr u32 IW_MWORDS = IW_SEGMAX / 32 + 2 + IW_MWIN;  // mark words per segment (bitmap, u32)
 constexpr u32 IW_EST0 = 64 * 3072;  // first block's body estimate (zlib-6 blocks: ~195 Kbit)
 static_assert(IW_S == 2048 && IW_BLK == 32, "the L phase keeps one 32-entry block per lane in registers");
 
@@ -115,7 +119,11 @@ struct IwLds {
             u8 lens[320];
             u32 bcache[BI_CACHE_WORDS];
         } h;
-        u32 mlim[65];  // H round: marked extent (bits) of each segment
+        struct {       // H round: marked extent (bits) of each segment, staged tokens, mark windows
+            u32 mlim[65];
+            u32 tst[IW_K][64];
+            u32 mwin[IW_MWIN][64];
+        } hr;
         struct {       // L phase: the stage ring, its token-start bits (one word per lane block), the chain
             u16 ptr[IW_S];
             u32 head[IW_S / 32];
@@ -152,29 +160,41 @@ __device__ __forceinline__ u32 iw_wave_sum(u32 v) {
     return (u32)__builtin_amdgcn_readlane((int)x, 63);
 }
 
-// ---- per-lane bit reader straight from HBM --------------------------------------------
+// ---- per-lane bit reader straight from HBM, refilled at wave-uniform points ----------
 // The stream is read as aligned 16-byte vectors from base = ds & ~15 (an
 // aligned vector holding any stream byte is readable; bytes outside the
 // stream are don't-care: a token that needs bits past the end becomes the
-// input-exhausted marker).  A 96-bit window (lo:hi) holds the next nb bits;
-// words are appended from `cur`, and `nxt` is in flight one vector ahead.
-struct GBits {
+// input-exhausted marker, and an index past the stream re-reads the last
+// vector).  A 96-bit window (lo:hi) holds the next nb bits; words are
+// appended from the two resident vectors A:B (8 words).
+// Loads are issued only at wave-uniform points: every lane loads the two
+// vectors after B at the top of an outer step (IW_K2 decode steps) and
+// absorbs them at its bottom (gr_absorb), so no load is in flight across a
+// loop back edge.  The memory counters are per wave, not per lane: a load
+// issued in a divergent step (when one lane's vector runs out) is waited for
+// by the whole wave as soon as any lane touches that register, i.e. at about
+// every step; a loop-carried register in flight is copied at the loop header,
+// which waits as well; and a flat (generic) load would also hold every LDS
+// table lookup.
+struct GRd {
     u64 lo;
     u32 hi;
     u32 nb;
-    u32x4 cur;
-    u32x4 nxt;
-    u32 wi;  // next word of cur
-    u32 vn;  // vector index to load after nxt
+    u32x4 A, B;
+    u32 wi;  // next word of A:B to append (0..8)
+    u32 vc;  // vector index after B
 };
 
-__device__ __forceinline__ u32x4 gb_vec(const u8* base, u32 nvec, u32 v) {
-    if (v < nvec) return *(const u32x4*)(base + 16ull * v);
-    return u32x4{0u, 0u, 0u, 0u};
+typedef __attribute__((address_space(1))) u32x4 gu32x4;
+__device__ __forceinline__ u32x4 gr_vec(const u8* base, u32 nvec, u32 v) {
+    const u32 vc = v < nvec ? v : (nvec ? nvec - 1 : 0u);
+    return *(const gu32x4*)((const gu8*)base + 16ull * vc);
 }
 
-__device__ __forceinline__ void gb_word(GBits& s, const u8* base, u32 nvec) {
-    const u32 w = s.wi == 0 ? s.cur.x : s.wi == 1 ? s.cur.y : s.wi == 2 ? s.cur.z : s.cur.w;
+__device__ __forceinline__ void gr_word(GRd& s) {
+    const u32x4 X = s.wi < 4 ? s.A : s.B;
+    const u32 k = s.wi & 3;
+    const u32 w = k == 0 ? X.x : k == 1 ? X.y : k == 2 ? X.z : X.w;
     if (s.nb < 64) {
         s.lo |= (u64)w << s.nb;
         s.hi = s.nb > 32 ? w >> (64 - s.nb) : 0u;
@@ -182,40 +202,48 @@ __device__ __forceinline__ void gb_word(GBits& s, const u8* base, u32 nvec) {
         s.hi = w;
     }
     s.nb += 32;
-    if (++s.wi == 4) {
-        s.cur = s.nxt;
-        s.nxt = gb_vec(base, nvec, s.vn++);
-        s.wi = 0;
-    }
+    s.wi++;
 }
 
-// >= 48 valid bits in lo afterwards (one token's worst case)
-__device__ __forceinline__ void gb_fill(GBits& s, const u8* base, u32 nvec) {
-    if (s.nb <= 64) gb_word(s, base, nvec);
-    if (s.nb < 48) gb_word(s, base, nvec);
+// >= 48 valid bits in lo afterwards (one token's worst case), unless A:B ran
+// dry: then the lane sits out the steps until the next refill
+__device__ __forceinline__ bool gr_fill(GRd& s) {
+    if (s.nb <= 64 && s.wi < 8) gr_word(s);
+    if (s.nb < 48 && s.wi < 8) gr_word(s);
+    return s.nb >= 48;
 }
 
-__device__ __forceinline__ void gb_drop(GBits& s, u32 k) {  // 0 < k <= 48
+__device__ __forceinline__ void gr_drop(GRd& s, u32 k) {  // 0 < k <= 48
     s.lo = (s.lo >> k) | ((u64)s.hi << (64 - k));
     s.hi = k >= 32 ? 0u : (s.hi >> k);
     s.nb -= k;
 }
 
-// qa = bit position relative to base
-__device__ __forceinline__ void gb_init(GBits& s, const u8* base, u32 nvec, u32 qa) {
+// every lane, wave-uniform, branch-free: C, D = the two vectors after B
+// (loaded at the top of the outer step) replace the used-up vectors of A:B
+__device__ __forceinline__ void gr_absorb(GRd& s, const u32x4& C, const u32x4& D) {
+    const u32 sh = s.wi >= 8 ? 2u : s.wi >= 4 ? 1u : 0u;
+    s.A = sh == 2 ? C : sh == 1 ? s.B : s.A;
+    s.B = sh == 2 ? D : sh == 1 ? C : s.B;
+    s.vc += sh;
+    s.wi -= 4 * sh;
+}
+
+// qa = bit position relative to base (every lane; waits for its first vectors)
+__device__ __forceinline__ void gr_init(GRd& s, const u8* base, u32 nvec, u32 qa) {
     const u32 v0 = qa >> 7;
-    s.cur = gb_vec(base, nvec, v0);
-    s.nxt = gb_vec(base, nvec, v0 + 1);
-    s.vn = v0 + 2;
+    s.A = gr_vec(base, nvec, v0);
+    s.B = gr_vec(base, nvec, v0 + 1);
+    s.vc = v0 + 2;
     s.wi = (qa >> 5) & 3;
     s.lo = 0;
     s.hi = 0;
     s.nb = 0;
-    gb_word(s, base, nvec);
-    gb_word(s, base, nvec);
-    gb_word(s, base, nvec);
+    gr_word(s);
+    gr_word(s);
+    gr_word(s);
     const u32 k = qa & 31;
-    if (k) gb_drop(s, k);
+    if (k) gr_drop(s, k);
 }
 
 // Decode one token from >= 48 valid bits: both table lookups always run, so
@@ -247,10 +275,21 @@ __device__ __forceinline__ u32 iw_decode(const IwLds& L, u64 v, u32* adv) {
     return tk;
 }
 
+typedef __attribute__((address_space(1))) u32x4 gu32x4_a4 __attribute__((aligned(4)));
+
+// tokens of a lane's list that start before word wi of its bitmap, plus the
+// marks in `part` (the bits of word wi below the position)
+__device__ __forceinline__ u32 iw_rank(const gu32* mw, u32 wi, u32 part) {
+    u32 c = __popc(part);
+#pragma unroll 8
+    for (u32 w = 0; w < wi; w++) c += __popc(mw[w]);
+    return c;
+}
+
 // stream bit of token j of the list of `lm` (segment start + bits before it)
 __device__ __forceinline__ u32 iw_pos(const gu32* gl, u32 lm, u32 j, u32 seg0) {
     const u32 lane = (u32)lane_id();
-    const gu32* lst = gl + (u64)lm * IW_TCAP;
+    const gu32* lst = gl + (u64)lm * IW_TSTR;
     u32 s = 0;
     for (u32 x = lane; x < j; x += 64) s += w_bits(lst[x]);
     return seg0 + iw_wave_sum(s);
@@ -345,8 +384,8 @@ __device__ __forceinline__ void blk_store(u16* p, const u32* w) {
 }
 
 constexpr u32 IW_NSLOT_MAX = 8192;
-constexpr u64 IW_LIST_WORDS = 64ull * IW_TCAP;              // token lists of a slot (u32)
-constexpr u64 IW_MARK_WORDS = 64ull * IW_MWORDS * 2;        // mark words of a slot (u64 as 2 x u32)
+constexpr u64 IW_LIST_WORDS = 64ull * IW_TSTR;              // token lists of a slot (u32)
+constexpr u64 IW_MARK_WORDS = 64ull * IW_MWORDS;            // token-start bitmaps of a slot (u32)
 constexpr u64 IW_SLOT_WORDS = IW_LIST_WORDS + IW_MARK_WORDS;
 constexpr u64 IW_OWNER_BYTES = IW_NSLOT_MAX * 4;
 
@@ -389,11 +428,10 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
         slot = sl;
     }
     slot = __builtin_amdgcn_readfirstlane(slot);
-    gu32* const gl = pools + (u64)slot * IW_SLOT_WORDS;                 // token lists [lane][IW_TCAP]
-    gu32* const my = gl + (u64)lane * IW_TCAP;
-    typedef __attribute__((address_space(1))) u64 gu64;
-    gu64* const marks = (gu64*)(gl + IW_LIST_WORDS);                    // mark words [lane][IW_MWORDS]
-    gu64* const mk = marks + (u64)lane * IW_MWORDS;
+    gu32* const gl = pools + (u64)slot * IW_SLOT_WORDS;                 // token lists [lane][IW_TSTR]
+    gu32* const my = gl + (u64)lane * IW_TSTR;
+    gu32* const marks = gl + IW_LIST_WORDS;                             // token-start bitmaps [lane][IW_MWORDS]
+    gu32* const mk = marks + (u64)lane * IW_MWORDS;
 
     BitIn b;
     bi_init(b, ds, n_ds, L.u.h.bcache);
@@ -456,88 +494,115 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
             const u32 p = R0 + lane * seg;
             const u32 pend = p + seg;
             u32 q = p, nt = 0, nxt = S_NONE, give = 0;
-            u32 cw = 0, cb = 0, cpre = 0;  // current mark word, its bits, marks before it
             const bool active = p < total_bits;
-            GBits bs;
-            if (active) {
-                gb_init(bs, vbase, nvec, p + a0b);
-            } else if (lane == 0) {  // the block body starts at the stream end
-                my[0] = W_MARK | M_EXH;
-                nt = 1;
-                nxt = S_MARKER;
-            } else {
-                nxt = S_ROUND_END;  // (never on the chain: the lane before it ends in EXH)
-            }
-            u32 it1 = 0;
-            // pass 1: my segment; markers other than EXH do not stop it.  Token
-            // starts are marked in u64 words {bits, marks before the word}.
-            while (nxt == S_NONE && q < pend) {
-                gb_fill(bs, vbase, nvec);
-                u32 adv;
-                u32 tk = iw_decode(L, bs.lo, &adv);
-                if (q + adv > total_bits) tk = W_MARK | M_EXH;
-                if (nt == IW_TCAP) { nxt = S_CAP; break; }
-                my[nt] = tk;
-                nt++;
-                const u32 off = q - p, wi = off >> 5;
-                if (wi != cw) {  // (a token is <= 48 bits: at most one word skipped)
-                    mk[cw] = (u64)cb | ((u64)cpre << 32);
-                    cpre += __popc(cb);
-                    if (wi > cw + 1) mk[cw + 1] = (u64)cpre << 32;
-                    cw = wi;
-                    cb = 0;
+            GRd bs;
+            gr_init(bs, vbase, nvec, (active ? p : 0u) + a0b);
+            if (!active) {
+                if (lane == 0) {  // the block body starts at the stream end
+                    my[0] = W_MARK | M_EXH;
+                    nt = 1;
+                    nxt = S_MARKER;
+                } else {
+                    nxt = S_ROUND_END;  // (never on the chain: the lane before it ends in EXH)
                 }
-                cb |= 1u << (off & 31);
-                if (tk == (W_MARK | M_EXH)) { nxt = S_MARKER; break; }
-                gb_drop(bs, adv);
-                q += adv;
-                it1++;
             }
-            if (active) {  // the last word and the words the last token spans
-                mk[cw] = (u64)cb | ((u64)cpre << 32);
-                cpre += __popc(cb);
-                mk[cw + 1] = (u64)cpre << 32;
-                mk[cw + 2] = (u64)cpre << 32;
+            // pass 1: my segment; markers other than EXH do not stop it.  Each
+            // step stages its token and sets its start bit in an LDS window of
+            // IW_MWIN mark words; every IW_K steps all lanes flush both to the
+            // workspace with unconditional stores and refill the reader.
+            u32 it1 = 0, w0 = 0, nt0 = nt;
+#pragma unroll
+            for (u32 j = 0; j < IW_MWIN; j++) L.u.hr.mwin[j][lane] = 0;
+            bool run = nxt == S_NONE;
+            while (__ballot(run) != 0) {
+              const u32x4 vC = gr_vec(vbase, nvec, bs.vc), vD = gr_vec(vbase, nvec, bs.vc + 1);
+              for (u32 kh = 0; kh < IW_KH; kh++) {
+                for (u32 k = 0; k < IW_K; k++) {
+                    if (!run || !gr_fill(bs)) continue;
+                    u32 adv;
+                    u32 tk = iw_decode(L, bs.lo, &adv);
+                    if (q + adv > total_bits) tk = W_MARK | M_EXH;
+                    if (nt == IW_TCAP) { nxt = S_CAP; run = false; continue; }
+                    L.u.hr.tst[nt - nt0][lane] = tk;
+                    nt++;
+                    const u32 off = q - p;  // (<= 5 words past w0 within one flush period)
+                    atomicOr(&L.u.hr.mwin[(off >> 5) - w0][lane], 1u << (off & 31));
+                    if (tk == (W_MARK | M_EXH)) { nxt = S_MARKER; run = false; continue; }
+                    gr_drop(bs, adv);
+                    q += adv;
+                    it1++;
+                    if (q >= pend) run = false;
+                }
+                // flush: IW_K staged words (those past nt are overwritten later)
+                // and the mark window (words past my position are still zero)
+                *(gu32x4_a4*)(my + nt0) = u32x4{L.u.hr.tst[0][lane], L.u.hr.tst[1][lane], L.u.hr.tst[2][lane],
+                                                 L.u.hr.tst[3][lane]};
+                nt0 = nt;
+                u32 mv[IW_MWIN];
+#pragma unroll
+                for (u32 j = 0; j < IW_MWIN; j++) mv[j] = L.u.hr.mwin[j][lane];
+                *(gu32x4_a4*)(mk + w0) = u32x4{mv[0], mv[1], mv[2], mv[3]};
+                *(gu32x4_a4*)(mk + w0 + 4) = u32x4{mv[4], mv[5], mv[6], mv[7]};
+                // slide the window to the word of my next token start (< 8 words on)
+                const u32 w1 = (q - p) >> 5, dw = w1 - w0;
+#pragma unroll
+                for (u32 sb = 1; sb < IW_MWIN; sb <<= 1) {
+                    const bool t = (dw & sb) != 0;
+#pragma unroll
+                    for (u32 j = 0; j < IW_MWIN; j++) mv[j] = t ? (j + sb < IW_MWIN ? mv[j + sb] : 0u) : mv[j];
+                }
+#pragma unroll
+                for (u32 j = 0; j < IW_MWIN; j++) L.u.hr.mwin[j][lane] = mv[j];
+                w0 = w1;
+              }
+              gr_absorb(bs, vC, vD);
             }
+            static_assert(IW_K == 4 && IW_MWIN == 8, "flush layout");
             // marked extent: the whole segment, or up to where the lane stopped
-            L.u.mlim[lane] = !active ? 0u : nxt == S_NONE ? seg : (q - p) + (nxt == S_MARKER ? 1u : 0u);
-            if (lane == 0) L.u.mlim[64] = 0;
+            L.u.hr.mlim[lane] = !active ? 0u : nxt == S_NONE ? seg : (q - p) + (nxt == S_MARKER ? 1u : 0u);
+            if (lane == 0) L.u.hr.mlim[64] = 0;
             __syncthreads();  // every lane's marks and list are stored
             IW_T(IWT_P1);
             // pass 2: follow my path until it meets a token start a later lane marked
             u32 ks = lane + 1, pk = pend, it2 = 0;
-            u32 lim = L.u.mlim[ks];
-            u32 cwi = 0xFFFFFFFFu;
-            u64 cwv = 0;
-            while (nxt == S_NONE) {
-                if (q >= round_hi) { nxt = S_ROUND_END; break; }
-                if (q >= pk + seg) { ks++; pk += seg; lim = L.u.mlim[ks]; cwi = 0xFFFFFFFFu; }
-                const u32 off = q - pk;
-                if (off < lim) {
-                    const u32 wi = off >> 5;
-                    if (wi != cwi) { cwv = marks[(u64)ks * IW_MWORDS + wi]; cwi = wi; }
-                    const u32 bits = (u32)cwv;
-                    if ((bits >> (off & 31)) & 1u) {
-                        give = (u32)(cwv >> 32) + __popc(bits & ((1u << (off & 31)) - 1u));
-                        nxt = ks;
-                        break;
+            u32 lim = L.u.hr.mlim[ks];
+            u32 cwi = 0xFFFFFFFFu, cwv = 0;
+            bool run2 = nxt == S_NONE;
+            while (__ballot(run2) != 0) {
+                const u32x4 vC = gr_vec(vbase, nvec, bs.vc), vD = gr_vec(vbase, nvec, bs.vc + 1);
+                for (u32 k = 0; k < IW_K * IW_KH; k++) {
+                    if (!run2) continue;
+                    if (q >= round_hi) { nxt = S_ROUND_END; run2 = false; continue; }
+                    if (q >= pk + seg) { ks++; pk += seg; lim = L.u.hr.mlim[ks]; cwi = 0xFFFFFFFFu; }
+                    const u32 off = q - pk;
+                    if (off < lim) {
+                        const u32 wi = off >> 5;
+                        if (wi != cwi) { cwv = marks[(u64)ks * IW_MWORDS + wi]; cwi = wi; }
+                        if ((cwv >> (off & 31)) & 1u) {
+                            give = iw_rank(marks + (u64)ks * IW_MWORDS, wi, cwv & ((1u << (off & 31)) - 1u));
+                            nxt = ks;
+                            run2 = false;
+                            continue;
+                        }
                     }
+                    if (!gr_fill(bs)) continue;  // A:B ran dry: wait for the refill
+                    u32 adv;
+                    u32 tk = iw_decode(L, bs.lo, &adv);
+                    if (q + adv > total_bits) tk = W_MARK | M_EXH;
+                    if (nt == IW_TCAP) { nxt = S_CAP; run2 = false; continue; }
+                    my[nt] = tk;
+                    nt++;
+                    it2++;
+                    if (w_marker(tk)) {
+                        if (tk != (W_MARK | M_EXH)) q += adv;
+                        nxt = S_MARKER;
+                        run2 = false;
+                        continue;
+                    }
+                    gr_drop(bs, adv);
+                    q += adv;
                 }
-                gb_fill(bs, vbase, nvec);
-                u32 adv;
-                u32 tk = iw_decode(L, bs.lo, &adv);
-                if (q + adv > total_bits) tk = W_MARK | M_EXH;
-                if (nt == IW_TCAP) { nxt = S_CAP; break; }
-                my[nt] = tk;
-                nt++;
-                it2++;
-                if (w_marker(tk)) {
-                    if (tk != (W_MARK | M_EXH)) q += adv;
-                    nxt = S_MARKER;
-                    break;
-                }
-                gb_drop(bs, adv);
-                q += adv;
+                gr_absorb(bs, vC, vD);
             }
             if (dbg) {
                 const u32 m1 = iw_wave_sum(it1), m2 = iw_wave_sum(it2);
@@ -578,7 +643,7 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
             auto fetch = [&](u32 cm0, u32 cj0) -> u32 {
                 u32 m = cm0, jj = cj0 + lane;
                 while (m < ncm && jj >= L.u.st.ch_e[m]) { jj = jj - L.u.st.ch_e[m] + L.u.st.ch_s[m + 1]; m++; }
-                return m < ncm ? (u32)gl[(u64)L.u.st.ch_lane[m] * IW_TCAP + jj] : (W_MARK | M_END);
+                return m < ncm ? (u32)gl[(u64)L.u.st.ch_lane[m] * IW_TSTR + jj] : (W_MARK | M_END);
             };
             auto advance = [&](u32& cm0, u32& cj0, u32 k) {
                 cj0 += k;
