@@ -146,7 +146,11 @@ int zcg_codec_on_gpu(int32_t codec, int encode);
  * are device arrays of n entries.  Asynchronous on `stream`; returns a
  * zcg_status for argument/launch errors only — per-chunk results land in
  * d_status.  Workspace is grown on first use of a given batch shape
- * (hipMalloc), so steady-state calls do no allocation and are capturable. */
+ * (hipMalloc), so steady-state calls do no allocation and are capturable.
+ * The workspace is kept per stream (gzip decode: ~100 MiB at full batch,
+ * zcg_workspace_bytes gives the figure); a context keeps at most 4 streams'
+ * workspaces and frees the least recently used one (after a device-wide
+ * synchronize) when a fifth stream arrives. */
 int zcg_decode_batch(zcg_ctx* ctx, const zcg_array* array, const zcg_chunk* d_chunks,
                      uint32_t n, int32_t* d_status, void* stream);
 

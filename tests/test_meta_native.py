@@ -92,6 +92,25 @@ def test_codec_defaults_and_configuration():
     assert st == _native.INVALID_DATA
 
 
+@pytest.mark.parametrize("codec,key", [("https://purl.org/zarr/spec/codec/gzip/1.0", "level"),
+                                       ("lz4", "blockSize"), ("xz", "preset")])
+def test_codec_configuration_outside_i32(codec, key):
+    # the reference's configuration fields are i32: serde rejects values outside it
+    for v in (2 ** 31, -(2 ** 31) - 1, 2 ** 40):
+        st, _, _ = native(_doc(compressor={"codec": codec, "configuration": {key: v}}))
+        assert st == _native.INVALID_DATA, (codec, v)
+    st, _, _ = native(_doc(compressor={"codec": codec, "configuration": {key: 2 ** 31 - 1}}))
+    assert st == _native.OK
+
+
+def test_chunk_shape_product_overflow():
+    st, _, err = native(_doc(chunk_grid={"type": "regular", "chunk_shape": [2 ** 32 - 1] * 3, "separator": "/"}))
+    assert st == _native.INVALID_DATA and "overflow" in err
+    st, m, _ = native(_doc(chunk_grid={"type": "regular", "chunk_shape": [2 ** 32 - 1, 2 ** 32 - 1],
+                                       "separator": "/"}))
+    assert st == _native.OK and m.array.chunk_num_elements == (2 ** 32 - 1) ** 2
+
+
 def test_extended_types_and_extensions():
     ext = {"extension": "https://example.org/dt/complex", "type": "complex128", "fallback": ">u8"}
     st, m, err = native(_doc(data_type=ext))

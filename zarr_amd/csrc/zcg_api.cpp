@@ -24,12 +24,17 @@ struct zcg_ctx {
     std::string err;
     // device workspace of the batch kernels, one per stream, so batches
     // enqueued on different streams of one ctx never share scratch
+    // (at most WS_MAX of them: the least recently used one is freed when a
+    // new stream needs one; a gzip workspace is ~100 MiB)
     struct Ws {
         void* stream;
         void* p;
         size_t bytes;
+        uint64_t used;
     };
+    static constexpr size_t WS_MAX = 4;
     std::vector<Ws> ws;
+    uint64_t ws_tick = 0;
     // host-convenience staging
     void* d_buf = nullptr;
     size_t d_buf_bytes = 0;
@@ -99,9 +104,20 @@ int stream_ws(zcg_ctx* ctx, void* stream, size_t need, zcg_ctx::Ws** out) {
     for (auto& x : ctx->ws)
         if (x.stream == stream) w = &x;
     if (!w) {
-        ctx->ws.push_back({stream, nullptr, 0});
+        if (ctx->ws.size() >= zcg_ctx::WS_MAX) {
+            // evict the least recently used stream's workspace; that stream may
+            // already be destroyed by the caller, so wait for the whole device
+            size_t v = 0;
+            for (size_t i = 1; i < ctx->ws.size(); i++)
+                if (ctx->ws[i].used < ctx->ws[v].used) v = i;
+            (void)hipDeviceSynchronize();
+            if (ctx->ws[v].p) (void)hipFree(ctx->ws[v].p);
+            ctx->ws.erase(ctx->ws.begin() + (long)v);
+        }
+        ctx->ws.push_back({stream, nullptr, 0, 0});
         w = &ctx->ws.back();
     }
+    w->used = ++ctx->ws_tick;
     if (w->bytes < need) (void)hipStreamSynchronize((hipStream_t)stream);  // old scratch may be in use
     const int r = ensure_dev(ctx, &w->p, &w->bytes, need);
     *out = w;

@@ -147,7 +147,7 @@ static_assert(sizeof(ParLds) <= 53 * 1024, "ParLds must leave room for three wor
 // token words, token j of lane i at [j * PI_NL + i].  A workgroup takes a
 // free slot when it starts (owner word 0 -> 1) and frees it when it ends; the
 // launcher zeroes the owner words before each launch.
-constexpr u32 PI_NSLOT = 1024;  // > the 512 workgroups two per CU can keep resident
+constexpr u32 PI_NSLOT = 1024;  // > the 768 workgroups three per CU (256 CUs) keep resident
 constexpr u64 PI_SLOT_WORDS = (u64)PI_TMAX * PI_NL;
 constexpr u64 PI_OWNER_BYTES = PI_NSLOT * 4;
 

@@ -324,6 +324,9 @@ int64_t cfg_int(const JVal* conf, const char* key, int64_t def, bool& bad) {
     const JVal* x = conf->get(key);
     if (!x) return def;
     if (x->kind != JVal::NUM || !x->is_int) { bad = true; return def; }
+    // the configuration fields are i32 in the reference (serde rejects a value
+    // outside the type's range with InvalidData)
+    if (x->neg ? x->mag > 0x80000000ull : x->mag > 0x7FFFFFFFull) { bad = true; return def; }
     return x->neg ? -(int64_t)x->mag : (int64_t)x->mag;
 }
 
@@ -371,6 +374,7 @@ int parse_meta(const char* json, uint64_t len, zcg_array_meta* out, std::string&
             return ZCG_ERR_INVALID_DATA;
         }
         out->chunk_shape[i] = x.mag;
+        if (x.mag && nel > UINT64_MAX / x.mag) { err = "chunk_shape product overflows u64"; return ZCG_ERR_INVALID_DATA; }
         nel *= x.mag;
     }
     out->chunk_ndim = (uint32_t)cshape.arr.size();

@@ -4,9 +4,10 @@
 // transform of read_data (byte reversal for '>' types, bool != 0).
 // Encode = write_data's serialisation (chunk.rs:118-140): the same map.
 //
-// Pure HBM copy: each 256-thread workgroup moves one 16 KiB tile of one
-// chunk with 16 B per lane per access (4 x global_load_dwordx4 in flight per
-// lane), so the kernel is bound by the HBM copy roofline.  Algorithmic bytes
+// Pure HBM copy: each 256-thread workgroup moves one 4 KiB tile of one
+// chunk, one 16-B load and one 16-B store per lane (a grid past the launch
+// limit strides over the tiles), so the kernel is bound by the HBM copy
+// roofline.  Algorithmic bytes
 // per chunk: 2*N*size (read once, write once).
 #include "zcg_common.h"
 
