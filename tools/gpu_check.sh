@@ -21,7 +21,7 @@ run_bench() {
 run_prof() {
   [ -n "$SKIP_PROF" ] && return 0
   cd /tmp && timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof" -o run -- \
-    python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-} > "$R/gpurun_out/prof.log" 2>&1
+    python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-} > "$R/gpurun_out/prof.log" 2>&1 && grep "^{" "$R/gpurun_out/prof.log" > "$R/gpurun_out/prof_bench.json"
 }
 run_tests && run_bench && run_prof
 rc=$?
