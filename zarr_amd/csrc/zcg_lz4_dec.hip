@@ -780,6 +780,9 @@ struct LaneRing {
     __device__ __forceinline__ void wr32(u32 a, u32 v) { *(lu32*)(R + (a & LZ_LRM)) = v; }
     __device__ __forceinline__ u32 rd32(u32 a) const { return *(const lu32*)(R + (a & LZ_LRM)); }
     __device__ __forceinline__ void store_piece(u32 a) {
+#ifdef ZCG_LZ4_DIAG_NOSTORE  // timing diagnostic only: no output stores
+        if (a < 0x7FFFFFFFu) return;
+#endif
         if (a >= lim) return;
         const lu8* p = R + (a & LZ_LRM);
         if (a + LZ_LPC <= lim) {
@@ -853,7 +856,11 @@ __device__ __forceinline__ u32x4 lz_pattern(u32x4 v, u32 off) {
 // the 4 covering the stale tail of the last written dword), else from HBM
 __device__ __forceinline__ u32x4 lz_src16(const LaneRing& O, u32 op, u32 off) {
     const u32 p = op - off;
+#ifdef ZCG_LZ4_DIAG_NOFAR  // timing diagnostic only (wrong bytes): every source from the ring
+    if (true) {
+#else
     if (off < LZ_LRB - 4) {
+#endif
         const u32x4 v = O.rd16(p);
         return off < 16 ? lz_pattern(v, off) : v;
     }
@@ -994,6 +1001,230 @@ __device__ __forceinline__ int lz4_lane_block(const u8* __restrict__ src, u32 ie
     return ZCG_OK;
 }
 
+// ---- the same decode with the sequence parse running QK sequences ahead ------
+// A lane's decode is a chain of dependent steps, and at 2-4 waves per SIMD
+// the exposed latency of each step's memory reads (the match source from HBM
+// for 70 % of C4 sequences, a new input line every ~14) is what bounds it.
+// The parse of a sequence (token, lengths, offset, and every check of
+// LZ4_decompress_safe: they need only ip, op and the lengths) does not depend
+// on the output, so it runs QK sequences ahead of the execution:
+//  * parsing sequence s+QK issues the loads that sequence will need — its
+//    first 16 literal bytes, and, when its match source is already in HBM
+//    (offset past the ring and the source below the flushed mark), the first
+//    16 source bytes — into the queue slot that sequence s just left;
+//  * the loads are issued on every step whatever the sequence needs (a dummy
+//    address otherwise), so the compiler can count the vector-memory
+//    operations between a slot's loads and their use and wait for those
+//    alone (vmcnt counts loads and stores together, in issue order);
+//  * the input is two 64-byte register buffers, the next one loaded as soon
+//    as the parse enters the current one.
+// The queue is QK named slots in a QK-times unrolled loop, so a slot's loads
+// stay in flight in place across the loop's back edge (no register copies).
+#ifndef ZCG_LZ4_Q
+#define ZCG_LZ4_Q 0
+#endif
+#ifndef ZCG_LZ4_QK
+#define ZCG_LZ4_QK 4
+#endif
+
+// win_load for a global pointer (global_load, not flat: a flat load makes
+// every later wait a full vmcnt(0) + lgkmcnt(0))
+__device__ __forceinline__ u32x4 gwin_load(const gu8* __restrict__ src, u32 q, u32 avail) {
+    if (q + 16 <= avail) return *(const gu32x4_ua*)(src + q);
+    u64 lo = 0, hi = 0;
+    for (u32 k = 0; k < 16; k++) {
+        const u64 b = (q + k < avail) ? (u64)src[q + k] : 0ull;
+        if (k < 8) lo |= b << (8 * k);
+        else hi |= b << (8 * (k - 8));
+    }
+    return u32x4{(u32)lo, (u32)(lo >> 32), (u32)hi, (u32)(hi >> 32)};
+}
+
+struct LzIn2 {
+    const gu8* src;
+    u32 avail;            // readable bytes from src (>= 64 on this path)
+    u32x4 b0, b1, b2, b3;  // [bb, bb + 64)
+    u32x4 n0, n1, n2, n3;  // [bb + 64, bb + 128), in flight until first used
+    u32 bb;
+    u32x4 w;  // [wb, wb + 16)
+    u32 wb;
+    // 16 bytes at q; near the stream end the last 16 readable bytes are
+    // loaded and shifted into place (zero fill past avail)
+    __device__ __forceinline__ u32x4 vec(u32 q) const {
+        const u32 a = q + 16 <= avail ? q : avail - 16;
+        const u32x4 v = *(const gu32x4_ua*)(src + a);
+        return a == q ? v : (q - a >= 16 ? u32x4{0u, 0u, 0u, 0u} : win_shift(v, q - a));
+    }
+    __device__ __forceinline__ void load_at(u32 q) {
+        bb = q & ~15u;
+        b0 = vec(bb); b1 = vec(bb + 16); b2 = vec(bb + 32); b3 = vec(bb + 48);
+        n0 = vec(bb + 64); n1 = vec(bb + 80); n2 = vec(bb + 96); n3 = vec(bb + 112);
+    }
+    __device__ __forceinline__ void at(u32 q) {
+        u32 d = q - bb;
+        if (d >= 64) {
+            if (d < 128) {
+                b0 = n0; b1 = n1; b2 = n2; b3 = n3;
+                bb += 64;
+                n0 = vec(bb + 64); n1 = vec(bb + 80); n2 = vec(bb + 96); n3 = vec(bb + 112);
+            } else {
+                load_at(q);
+            }
+            d = q - bb;
+        }
+        const u32 qd = d >> 4;
+        u32x4 c0 = b0, c1 = b1, c2 = b2, c3 = b3, c4 = n0;
+        asm volatile("" : "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3), "+v"(c4));
+        const u32x4 lo = qd == 0 ? c0 : qd == 1 ? c1 : qd == 2 ? c2 : c3;
+        const u32x4 hi = qd == 0 ? c1 : qd == 1 ? c2 : qd == 2 ? c3 : c4;
+        const u32 s4 = (d >> 2) & 3, sb = d & 3;
+        const u32 y0 = sel4(s4, lo.x, lo.y, lo.z, lo.w), y1 = sel4(s4, lo.y, lo.z, lo.w, hi.x);
+        const u32 y2 = sel4(s4, lo.z, lo.w, hi.x, hi.y), y3 = sel4(s4, lo.w, hi.x, hi.y, hi.z);
+        const u32 y4 = sel4(s4, hi.x, hi.y, hi.z, hi.w);
+        w = sb ? u32x4{__builtin_amdgcn_alignbyte(y1, y0, sb), __builtin_amdgcn_alignbyte(y2, y1, sb),
+                       __builtin_amdgcn_alignbyte(y3, y2, sb), __builtin_amdgcn_alignbyte(y4, y3, sb)}
+               : u32x4{y0, y1, y2, y3};
+        wb = q;
+    }
+    __device__ __forceinline__ u32 byte(u32 q) {
+        u32 d = q - wb;
+        if (d >= 16) { at(q); d = 0; }
+        return win_byte(w, d);
+    }
+};
+
+struct LzQSeq {
+    u32 lit, lip;  // literal count and their input position
+    u32 ofs;       // offset | Q_PRE (first source vector prefetched) | Q_LAST | Q_VALID
+    u32 ml;        // match length (incl. the 4)
+    u32x4 lv, fv;  // first 16 literal bytes, first 16 match-source bytes
+};
+constexpr u32 Q_PRE = 1u << 16, Q_LAST = 1u << 17, Q_VALID = 1u << 18;
+
+// parse the sequence at ip (output position opp) into q; returns false on
+// corrupt input (LZ4_decompress_safe's checks, in lz4_lane_block's order)
+__device__ __forceinline__ bool lzq_parse(LzIn2& in, u32& ip, u32& opp, u32 iend, u32 cap, const LaneRing& O,
+                                          LzQSeq& q, bool& pdone, u32& la, u32& fa) {
+    if (ip >= iend) return false;
+    if (ip - in.wb > 8) in.at(ip);
+    const u32 token = in.byte(ip++);
+    u32 lit = token >> 4;
+    if (lit == 15) {
+        if ((i64)ip >= (i64)iend - 15) return false;
+        u32 s;
+        do {
+            s = in.byte(ip++);
+            lit += s;
+        } while (s == 255 && (i64)ip < (i64)iend - 15);
+    }
+    const u64 cpy = (u64)opp + lit;
+    const bool last = cpy + 12 > cap || (i64)ip + lit > (i64)iend - 8;
+    if (last && ((u64)ip + lit != iend || cpy > cap)) return false;
+    q.lit = lit;
+    q.lip = ip;
+    la = ip;
+    ip += lit;
+    opp += lit;
+    if (last) {
+        q.ofs = Q_VALID | Q_LAST;
+        q.ml = 0;
+        pdone = true;
+        return true;
+    }
+    const u32 off = in.byte(ip) | (in.byte(ip + 1) << 8);
+    ip += 2;
+    u32 ml = token & 15;
+    if (ml == 15) {
+        u32 s;
+        do {
+            s = in.byte(ip++);
+            ml += s;
+            if ((i64)ip >= (i64)iend - 4) return false;
+        } while (s == 255);
+    }
+    ml += 4;
+    if (opp < off) return false;
+    if ((u64)opp + ml + 5 > cap) return false;
+    // the source is in HBM already: prefetch its first vector
+    const bool pre = off >= LZ_LRB - 4 && opp - off + 16 <= O.fl && opp - off + 16 <= O.lim;
+    if (pre) fa = opp - off;
+    q.ofs = Q_VALID | off | (pre ? Q_PRE : 0u);
+    q.ml = ml;
+    opp += ml;
+    return true;
+}
+
+__device__ __forceinline__ void lzq_exec(const gu8* src, u32 avail, LaneRing& O, u32& op, const LzQSeq& q) {
+    const u32 lit = q.lit;
+    if (lit) {
+        const u32x4 v = q.lip + 16 <= avail ? q.lv : gwin_load(src, q.lip, avail);
+        const u32 k = lit < 16 ? lit : 16;
+        O.append16(op, v, k);
+        O.flush(op);
+        for (u32 j0 = 16; j0 < lit; j0 += 16) {
+            const u32 k2 = lit - j0 < 16 ? lit - j0 : 16;
+            O.append16(op, gwin_load(src, q.lip + j0, avail), k2);
+            O.flush(op);
+        }
+    }
+    if (q.ofs & Q_LAST) return;
+    const u32 off = q.ofs & 0xFFFFu;
+    u32 r = q.ml;
+    {
+        const u32 k = r < 16 ? r : 16;
+        const u32x4 v = (q.ofs & Q_PRE) ? q.fv : (off ? lz_src16(O, op, off) : u32x4{0u, 0u, 0u, 0u});
+        O.append16(op, v, k);
+        O.flush(op);
+        r -= k;
+    }
+    while (r > 0) {
+        const u32 k = r < 16 ? r : 16;
+        const u32x4 v = off ? lz_src16(O, op, off) : u32x4{0u, 0u, 0u, 0u};
+        O.append16(op, v, k);
+        O.flush(op);
+        r -= k;
+    }
+}
+
+__device__ __forceinline__ int lz4_lane_block_q(const u8* __restrict__ src8, u32 iend, u32 avail, LaneRing& O,
+                                                u32 cap, u32* out_n) {
+    const gu8* src = (const gu8*)src8;
+    LzIn2 in;
+    in.src = src;
+    in.avail = avail;
+    in.load_at(0);
+    in.wb = 0x80000000u;  // no window yet
+    u32 ip = 0, opp = 0, op = 0;
+    bool pdone = false;
+    LzQSeq q0, q1, q2, q3;
+    q0.ofs = q1.ofs = q2.ofs = q3.ofs = 0;
+    // one queue step on slot q: run the sequence it holds, refill it
+#define LZQ_STEP(q)                                                                              \
+    {                                                                                            \
+        if (q.ofs & Q_VALID) {                                                                   \
+            lzq_exec(src, avail, O, op, q);                                                      \
+            if (q.ofs & Q_LAST) { *out_n = op; return ZCG_OK; }                                  \
+        }                                                                                        \
+        u32 la = ip, fa = 0;                                                                     \
+        q.ofs = 0;                                                                               \
+        if (!pdone && !lzq_parse(in, ip, opp, iend, cap, O, q, pdone, la, fa))                   \
+            return ZCG_ERR_INVALID_DATA;                                                         \
+        const u32 la2 = la + 16 <= avail ? la : avail - 16;                                      \
+        q.lv = *(const gu32x4_ua*)(src + la2);                                                   \
+        q.fv = *(const gu32x4_ua*)((q.ofs & Q_PRE) ? (const gu8*)O.dst + fa : src + la2);        \
+    }
+    static_assert(ZCG_LZ4_QK == 3 || ZCG_LZ4_QK == 4, "three or four named queue slots");
+    for (;;) {
+        LZQ_STEP(q0);
+        LZQ_STEP(q1);
+        LZQ_STEP(q2);
+#if ZCG_LZ4_QK == 4
+        LZQ_STEP(q3);
+#endif
+    }
+#undef LZQ_STEP
+}
+
 #ifndef ZCG_LZ4_WPE
 #define ZCG_LZ4_WPE 1
 #endif
@@ -1030,7 +1261,11 @@ __global__ __launch_bounds__(LZ_LWG, ZCG_LZ4_WPE) void lz4_lanes_kernel(const zc
             got = cs;
         } else {
             LaneRing O{(lu8*)(rings + threadIdx.x * LZ_LRB), dst, lb, 0, 0};
-            st = lz4_lane_block(s, cs, ch.src_len - so, O, ci.bmax, &got);
+            const u64 avail = ch.src_len - so;
+            if (ZCG_LZ4_Q && avail >= 64)
+                st = lz4_lane_block_q(s, cs, avail < 0xFFFFFFF0ull ? (u32)avail : 0xFFFFFFF0u, O, ci.bmax, &got);
+            else
+                st = lz4_lane_block(s, cs, avail, O, ci.bmax, &got);
             if (st == ZCG_OK) O.finish(got);
         }
     }
