@@ -35,6 +35,7 @@ def main():
     ap.add_argument("--chunks", type=int, default=1024)
     ap.add_argument("--pool", type=int, default=32)
     ap.add_argument("--threads", type=int, default=16)
+    ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--dir", default=os.path.join(os.environ.get("TMPDIR", "/tmp"), "zcg_e2e_store"))
     args = ap.parse_args()
     meta0, gen, desc = workload(args.codec)
@@ -53,9 +54,13 @@ def main():
     tw = time.time() - t0
     comp = sum(os.path.getsize(h.chunk_path("a", meta, c)) for c in coords)
     h.read_chunks("a", meta, coords[:8], vals[0].dtype, io_threads=args.threads)
-    t0 = time.time()
-    got = h.read_chunks("a", meta, coords, vals[0].dtype, io_threads=args.threads)
-    tr = time.time() - t0
+    trs = []
+    for _ in range(args.reps):  # the first read also pays the pinned destination's allocation
+        got = None
+        t0 = time.time()
+        got = h.read_chunks("a", meta, coords, vals[0].dtype, io_threads=args.threads)
+        trs.append(time.time() - t0)
+    tr = min(trs)
     for i in range(0, args.chunks, max(1, args.chunks // 32)):
         assert np.array_equal(got[i].get_data(), vals[i % args.pool]), i
     fs = os.statvfs(args.dir)
@@ -65,7 +70,8 @@ def main():
     print(json.dumps(dict(common, direction="write_chunks (elements -> files)",
                           gib_s=round(args.chunks * D / tw / GIB, 3), seconds=round(tw, 3))))
     print(json.dumps(dict(common, direction="read_chunks (files -> elements, page cache)",
-                          gib_s=round(args.chunks * D / tr / GIB, 3), seconds=round(tr, 3))))
+                          gib_s=round(args.chunks * D / tr / GIB, 3), seconds=round(tr, 3),
+                          first_read_gib_s=round(args.chunks * D / trs[0] / GIB, 3))))
     shutil.rmtree(args.dir, ignore_errors=True)
 
 

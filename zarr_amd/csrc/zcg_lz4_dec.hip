@@ -771,6 +771,30 @@ constexpr u32 LZ_LRM = LZ_LRB - 1;
 #endif
 constexpr u32 LZ_LWG = ZCG_LZ4_LWG;  // lanes (blocks) per workgroup
 
+// ZCG_LZ4_ULDS: the ring is written and read with byte-unaligned
+// ds_write_b128 / ds_read_b128 (gfx950 LDS in the unaligned alignment mode
+// the ROCm driver sets; tools/probe/lds_unaligned checks it).  The lane's
+// LDS block is [16-byte front pad | LZ_LRB ring | 16-byte mirror]: a vector
+// that crosses the ring end is written a second time LZ_LRB bytes lower, and
+// one that touches the ring's first 16 bytes a second time LZ_LRB higher, so
+// any 16 ring bytes are contiguous in the block.
+#ifndef ZCG_LZ4_ULDS
+#define ZCG_LZ4_ULDS 0
+#endif
+constexpr u32 LZ_LSTRIDE = ZCG_LZ4_ULDS ? ZCG_LZ4_LRB + 32 : ZCG_LZ4_LRB;  // LDS bytes per lane
+typedef __attribute__((ext_vector_type(4))) u32 lz_v4;
+__device__ __forceinline__ void lds_st16_ua(lu8* p, const u32x4& v) {
+    const u32 a = (u32)(uintptr_t)p;
+    const lz_v4 w = {v.x, v.y, v.z, v.w};
+    asm volatile("ds_write_b128 %0, %1" ::"v"(a), "v"(w) : "memory");
+}
+__device__ __forceinline__ u32x4 lds_ld16_ua(const lu8* p) {
+    const u32 a = (u32)(uintptr_t)p;
+    lz_v4 r;
+    asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(r) : "v"(a) : "memory");
+    return u32x4{r.x, r.y, r.z, r.w};
+}
+
 struct LaneRing {
     lu8* R;      // this lane's ring (16-byte aligned)
     gu8* dst;    // the block's output
@@ -807,6 +831,19 @@ struct LaneRing {
         flush(op);
         for (u32 i = fl; i < op && i < lim; i++) dst[i] = R[i & LZ_LRM];
     }
+#if ZCG_LZ4_ULDS
+    // append the first k (1..16) bytes of v at op: one unaligned 16-byte
+    // write (bytes past op + k are stale and overwritten later), a second
+    // one when it crosses the ring end or covers its first 16 bytes
+    __device__ __forceinline__ void append16(u32& op, const u32x4& v, u32 k) {
+        const u32 w = op & LZ_LRM;
+        lds_st16_ua(R + w, v);
+        if (w > LZ_LRB - 16) lds_st16_ua(R + w - LZ_LRB, v);
+        else if (w < 16) lds_st16_ua(R + w + LZ_LRB, v);
+        op += k;
+    }
+    __device__ __forceinline__ u32x4 rd16(u32 p) const { return lds_ld16_ua(R + (p & LZ_LRM)); }
+#else
     // append the first k (1..16) bytes of v at op: up to five dword writes
     // (v_alignbyte merges), the dword holding the new op is kept in tw
     __device__ __forceinline__ void append16(u32& op, const u32x4& v, u32 k) {
@@ -834,6 +871,7 @@ struct LaneRing {
         return u32x4{__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
                      __builtin_amdgcn_alignbyte(w3, w2, sh), __builtin_amdgcn_alignbyte(w4, w3, sh)};
     }
+#endif
 };
 
 // v with its first `off` (1..15) bytes repeated: byte j = byte (j mod off)
@@ -1232,7 +1270,7 @@ __global__ __launch_bounds__(LZ_LWG, ZCG_LZ4_WPE) void lz4_lanes_kernel(const zc
                                                            u32 S, u32 vflags,
                                                            const Lz4ChunkInfo* __restrict__ info,
                                                            Lz4Slot* __restrict__ slots) {
-    __shared__ __attribute__((aligned(16))) u8 rings[LZ_LWG * LZ_LRB + ZCG_LZ4_LDS_PAD];
+    __shared__ __attribute__((aligned(16))) u8 rings[LZ_LWG * LZ_LSTRIDE + ZCG_LZ4_LDS_PAD];
     const u64 g = (u64)blockIdx.x * LZ_LWG + threadIdx.x;
     const u32 c = (u32)(g / S);
     const u32 k = (u32)(g - (u64)c * S);
@@ -1260,7 +1298,7 @@ __global__ __launch_bounds__(LZ_LWG, ZCG_LZ4_WPE) void lz4_lanes_kernel(const zc
             for (; i < m; i++) dst[i] = s[i];
             got = cs;
         } else {
-            LaneRing O{(lu8*)(rings + threadIdx.x * LZ_LRB), dst, lb, 0, 0};
+            LaneRing O{(lu8*)(rings + threadIdx.x * LZ_LSTRIDE + (ZCG_LZ4_ULDS ? 16 : 0)), dst, lb, 0, 0};
             const u64 avail = ch.src_len - so;
             if (ZCG_LZ4_Q && avail >= 64)
                 st = lz4_lane_block_q(s, cs, avail < 0xFFFFFFF0ull ? (u32)avail : 0xFFFFFFF0u, O, ci.bmax, &got);

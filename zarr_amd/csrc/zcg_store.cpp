@@ -191,6 +191,19 @@ size_t store_batch_bytes(const zcg_array* a) {
     const int32_t c = a->compression.codec;
     return (c == ZCG_CODEC_XZ || c == ZCG_CODEC_BZIP2) ? 4 * STORE_BATCH_BYTES : STORE_BATCH_BYTES;
 }
+// Chunks per read sub-batch.  Gzip, xz and bzip2 decode one chunk per wave
+// (or workgroup), and a wave's time does not depend on how many run beside
+// it up to 16 per CU: a sub-batch needs >= 2 048 chunks (4 096 in flight over
+// the two pipeline slots) to run at the device rate, whatever D is.
+uint64_t store_read_batch_chunks(const zcg_array* a, uint64_t D) {
+    const int32_t c = a->compression.codec;
+    uint64_t per = D ? store_batch_bytes(a) / D : ~0ull;
+    if (c == ZCG_CODEC_GZIP || c == ZCG_CODEC_XZ || c == ZCG_CODEC_BZIP2) {
+        const uint64_t cap = D ? (4ull << 30) / D : ~0ull;  // <= 4 GiB of decoded bytes per slot
+        per = std::max<uint64_t>(per, std::min<uint64_t>(2048, cap));
+    }
+    return std::max<uint64_t>(per, 1);
+}
 
 // true when every pointer is page-locked host memory the GPU can copy into
 bool all_pinned(void* const* p, uint32_t n) {
@@ -253,7 +266,7 @@ int store_read_impl(zcg_ctx* ctx, const zcg_array* a, uint32_t n, const char* co
     IoPool& pool = S->pool;
     const uint64_t D = a->chunk_num_elements * (uint64_t)a->dtype.elem_size;
     const Dst mode = device_dsts ? Dst::Device : (all_pinned(dsts, n) ? Dst::HostPinned : Dst::HostStaged);
-    const uint32_t per = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(n, D ? store_batch_bytes(a) / D : n));
+    const uint32_t per = (uint32_t)std::min<uint64_t>(n, store_read_batch_chunks(a, D));
     const uint32_t nb = (n + per - 1) / per;
     std::vector<int32_t> fst[2];  // per sub-batch slot: file status (OK / ABSENT / IO)
     int rc = ZCG_OK;
