@@ -67,7 +67,9 @@ LEG = {"gzip": {"pool": 64, "batch": 4096, "strong": False},
        "bzip2": {"pool": 64, "batch": 4096, "strong": False}}
 # encode legs: chunks per rank, timed steps
 ENCODE_LEG = {"gzip": (512, 2), "lz4": (1024, 3), "xz": (1024, 2), "bzip2": (512, 2)}
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r02_pmc_traffic.json")
+# committed PMC traffic passes, newest first: a leg takes the first file that
+# measured it at the bench's own batch (kernels change between rounds)
+TRAFFIC_FILES = [os.path.join(ROOT, "profiles", f) for f in ("r03_pmc_traffic.json", "r02_pmc_traffic.json")]
 
 
 # ---------------------------------------------------------------- inputs ----
@@ -289,11 +291,22 @@ def pmc_traffic(leg, n):
     batch n, from the committed rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE passes
     over this same leg (tools/pmc_traffic.sh -> tools/pmc_traffic.py).  None
     unless the pass was taken at this batch (no scaling between batches)."""
-    try:
-        e = json.load(open(TRAFFIC_FILE))["legs"][leg]
-    except (OSError, KeyError, ValueError):
+    f = traffic_file(leg)
+    if f is None:
         return None
+    e = json.load(open(f))["legs"][leg]
     return int(e["traffic_bytes"]) if int(e["batch_per_gpu"]) == int(n) else None
+
+
+def traffic_file(leg):
+    """The newest committed traffic file that measured `leg`."""
+    for f in TRAFFIC_FILES:
+        try:
+            if leg in json.load(open(f))["legs"]:
+                return f
+        except (OSError, KeyError, ValueError):
+            continue
+    return None
 
 
 # ------------------------------------------------------------------ legs ----
@@ -361,7 +374,7 @@ def decode_leg(codec, batch, strong, steps, warmup, pool, rank, world, dev, thre
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                      "traffic": pmc_traffic(codec, n),
-                     "traffic_source": os.path.relpath(TRAFFIC_FILE, ROOT) +
+                     "traffic_source": os.path.relpath(traffic_file(codec) or TRAFFIC_FILES[-1], ROOT) +
                                        " (2*FETCH_SIZE + WRITE_SIZE per launch, same leg and batch)",
                      "kernel": KERNEL[codec], "kernel_ms": round(kern_ms, 4),
                      "algorithmic_bytes_per_launch": algo_bytes},
@@ -411,7 +424,7 @@ def encode_leg(codec, n, steps, warmup, pool, rank, world, dev, cpu_seconds=0.0,
            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                         "traffic": pmc_traffic(f"{codec}_encode", n),
-                        "traffic_source": os.path.relpath(TRAFFIC_FILE, ROOT) +
+                        "traffic_source": os.path.relpath(traffic_file(f"{codec}_encode") or TRAFFIC_FILES[-1], ROOT) +
                                           " (all encode kernels per call, same leg and batch)",
                         "algorithmic_bytes_per_launch": n * D + out_bytes}}
     del elems, dst, desc, out_len, status

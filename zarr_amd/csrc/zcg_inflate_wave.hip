@@ -59,6 +59,10 @@ namespace zcg {
 constexpr u32 IW_S = ZIW_S;            // stage ring entries: 64 lane blocks of IW_BLK
 constexpr u32 IW_BLK = IW_S / 64;
 constexpr u32 IW_TCAP = ZIW_TCAP;
+#ifndef ZIW_G2
+#define ZIW_G2 1
+#endif
+constexpr u32 IW_GK = 3;       // token groups in flight in the L phase (named slots)  // far-byte loads in flight per lane (gather)
 constexpr u32 IW_SEGMIN = 128;   // bits per lane segment
 constexpr u32 IW_SEGMAX = 4096;
 constexpr u32 IW_K = 4;          // decode steps between staged-token / mark flushes
@@ -127,7 +131,6 @@ struct IwLds {
         struct {       // L phase: the stage ring, its token-start bits (one word per lane block), the chain
             u16 ptr[IW_S];
             u32 head[IW_S / 32];
-            u16 ch_lane[65], ch_s[65], ch_e[65];  // chain members: lane, first valid token, list length
         } st;
     } u;
     u32 dbgc[IW_NDBG];
@@ -153,6 +156,16 @@ __device__ __forceinline__ u32 iw_incl_scan(u32 v) {
     const u32 t2 = t1 + (u32)__builtin_amdgcn_readlane((int)v, 47);
     const u32 lane = (u32)lane_id();
     return v + (lane < 16 ? 0u : (lane < 32 ? t0 : (lane < 48 ? t1 : t2)));
+}
+
+// OR over the wave (DPP row shifts, then the four row results), wave-uniform
+__device__ __forceinline__ u32 iw_wave_or(u32 v) {
+    v |= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
+    v |= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
+    v |= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
+    v |= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
+    return (u32)(__builtin_amdgcn_readlane((int)v, 15) | __builtin_amdgcn_readlane((int)v, 31) |
+                 __builtin_amdgcn_readlane((int)v, 47) | __builtin_amdgcn_readlane((int)v, 63));
 }
 
 __device__ __forceinline__ u32 iw_wave_sum(u32 v) {
@@ -383,6 +396,122 @@ __device__ __forceinline__ void blk_store(u16* p, const u32* w) {
     for (u32 i = 0; i < 4; i++) q[i] = u32x4{w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]};
 }
 
+// ---- dynamic block header, wave-parallel ------------------------------------
+// Same results, validity rules and order as read_dynamic
+// (zcg_inflate_common.h).  The code-length symbols are decoded at 64 bit
+// positions at once (lane i at window bit w0 + i: symbol, code bits, extra
+// bits, repeat count), and the true chain is walked through the window with
+// v_readlane on wave-uniform positions, so a symbol costs a few scalar
+// instructions instead of two dependent LDS round trips.
+#ifndef ZIW_PHDR
+#define ZIW_PHDR 1
+#endif
+template <int LB, u32 LCAP, int DB, u32 DCAP>
+__device__ __attribute__((always_inline)) int read_dynamic_wave(BitIn& b, u8* lens, HuffLds* lh, u32* ltab,
+                                                                HuffLds* dh, u32* dtab) {
+    const u32 lane = (u32)lane_id();
+    if (!bi_has(b, 14)) return R_EXHAUSTED;
+    const u32 nlen = bi_bits(b, 5) + 257, ndist = bi_bits(b, 5) + 1, ncode = bi_bits(b, 4) + 4;
+    if (nlen > 286 || ndist > 30) return R_INVALID;  // "too many length or distance symbols"
+    if (!bi_has(b, 3 * ncode)) return R_EXHAUSTED;
+    const gu8* src = (const gu8*)b.src;
+    const u64 nbytes = b.n;
+    // 32 stream bits from absolute bit q (bytes past the input read as 0)
+    auto bits32 = [&](u64 q) -> u32 {
+        const u64 by = q >> 3;
+        u64 w = 0;
+        if (by + 8 <= nbytes) {
+            w = *(const __attribute__((address_space(1))) u64 __attribute__((aligned(1)))*)(src + by);
+        } else {
+            for (u32 k = 0; k < 8; k++)
+                if (by + k < nbytes) w |= (u64)src[by + k] << (8 * k);
+        }
+        return (u32)(w >> (q & 7));
+    };
+    // the 3-bit code-length code lengths: lane i < ncode reads its own field
+    const u64 c0 = b.consumed;
+    const u32 mycl = lane < ncode ? bits32(c0 + 3 * lane) & 7 : 0u;
+    {  // code-length code must be complete ("invalid code lengths set")
+        int left = 1;
+        for (u32 l = 1; l <= 7; l++) {
+            const u32 cnt = (u32)__popcll(__ballot(lane < ncode && mycl == l));
+            left <<= 1;
+            left -= (int)cnt;
+            if (left < 0) break;
+        }
+        if (left != 0) return R_INVALID;
+    }
+    __syncthreads();
+    if (lane < 19) lens[lane] = 0;
+    __syncthreads();
+    if (lane < ncode) lens[c_clen_order[lane]] = (u8)mycl;
+    __syncthreads();
+    build_table(lens, 19, lh, ltab, 7, false, LCAP);
+    const u32 total = nlen + ndist;
+    const u64 lim = b.limit;
+    u64 pos = c0 + 3 * ncode;  // wave-uniform reader position
+    u32 idx = 0, prev = 0;
+    int r = R_OK;
+    while (idx < total) {
+        // records of the 64 bit positions [pos, pos + 64): adv | l << 4 | sym << 8 | cnt << 16
+        const u64 q = pos + lane;
+        const u32 v = bits32(q);
+        const u32 e = ltab[v & 127];
+        const u32 l = e >> 28, sym = e & 0x1F;
+        const u32 x = v >> l;
+        const u32 adv = sym == 16 ? l + 2 : sym == 17 ? l + 3 : sym == 18 ? l + 7 : l;
+        const u32 cnt = sym == 16 ? 3 + (x & 3) : sym == 17 ? 3 + (x & 7) : sym == 18 ? 11 + (x & 127) : 1;
+        const u32 rec = adv | (l << 4) | (sym << 8) | (cnt << 16);
+        u32 rel = 0;
+        while (rel < 64 && idx < total) {
+            const u32 f = (u32)__builtin_amdgcn_readlane((int)rec, (int)rel);
+            const u32 fa = f & 15, fl = (f >> 4) & 15, fs = (f >> 8) & 31, fc = f >> 16;
+            const u64 at = pos + rel;
+            // zlib's checks in read_dynamic's order: code bits, repeat at 0, extra bits, overflow
+            if (at + fl > lim) { r = R_EXHAUSTED; break; }
+            if (fs == 16 && idx == 0) { r = R_INVALID; break; }
+            if (at + fa > lim) { r = R_EXHAUSTED; break; }
+            if (idx + fc > total) { r = R_INVALID; break; }
+            const u32 val = fs < 16 ? fs : fs == 16 ? prev : 0u;
+            for (u32 k = lane; k < fc; k += 64) lens[idx + k] = (u8)val;
+            prev = val;
+            idx += fc;
+            rel += fa;
+        }
+        if (r != R_OK) return r;
+        pos += rel;
+    }
+    b.cbase = ~0ull;
+    bi_seek(b, pos);
+    __syncthreads();
+    u8 dl = 0;
+    if (lane < ndist) dl = lens[nlen + lane];
+    __syncthreads();
+    for (u32 i = nlen + lane; i < 288; i += 64) lens[i] = 0;
+    if (lane < 32) lens[288 + lane] = lane < ndist ? dl : 0;
+    __syncthreads();
+    if (lens[256] == 0) return R_INVALID;  // "invalid code -- missing end-of-block"
+    if (build_table(lens, 288, lh, ltab, LB, false, LCAP) != 0) return R_INVALID;
+    if (build_table(lens + 288, 30, dh, dtab, DB, true, DCAP) != 0) return R_INVALID;
+    return R_OK;
+}
+
+template <int LB, u32 LCAP, int DB, u32 DCAP>
+__device__ __attribute__((always_inline)) int read_block_header_wave(BitIn& b, bool* last, u32* type, u32* slen,
+                                                                     u8* lens, HuffLds* lh, u32* ltab, HuffLds* dh,
+                                                                     u32* dtab) {
+    if (!bi_has(b, 3)) return R_EXHAUSTED;
+    const u32 hdr = bi_bits(b, 3);
+    *last = hdr & 1;
+    *type = hdr >> 1;
+    if (*type != 2) {  // stored / fixed / invalid: the serial reader's rules
+        b.cbase = ~0ull;
+        bi_seek(b, b.consumed - 3);
+        return read_block_header<LB, LCAP, DB, DCAP>(b, last, type, slen, lens, lh, ltab, dh, dtab);
+    }
+    return read_dynamic_wave<LB, LCAP, DB, DCAP>(b, lens, lh, ltab, dh, dtab);
+}
+
 constexpr u32 IW_NSLOT_MAX = 8192;
 constexpr u64 IW_LIST_WORDS = 64ull * IW_TSTR;              // token lists of a slot (u32)
 constexpr u64 IW_MARK_WORDS = 64ull * IW_MWORDS;            // token-start bitmaps of a slot (u32)
@@ -452,8 +581,13 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
         u32 type = 0, slen = 0;
         b.cbase = ~0ull;  // the reader's LDS cache shares storage with the stage
         wsync();
+#if ZIW_PHDR
+        r = read_block_header_wave<W_LB, W_LCAP, W_DB, W_DCAP>(b, &last, &type, &slen, L.u.h.lens, &L.u.h.lh, L.ltab,
+                                                               &L.u.h.dh, L.dtab);
+#else
         r = read_block_header<W_LB, W_LCAP, W_DB, W_DCAP>(b, &last, &type, &slen, L.u.h.lens, &L.u.h.lh, L.ltab,
                                                           &L.u.h.dh, L.dtab);
+#endif
         const u32 hdr_end = (u32)b.consumed;
         IW_T(IWT_HDR);
         if (r != R_OK) break;
@@ -613,11 +747,16 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
             }
             IW_T(IWT_P2);
             // ---- chain: lane 0 is true; follow the sync targets (wave-uniform walk) ----
+            // chain member m lives in lane m's chL/chS/chE (its lane, first valid
+            // token, list length): a sync target is always a later lane, so a
+            // chain has <= 64 members, and the wave-uniform cursor reads them
+            // with v_readlane instead of dependent LDS reads
             u32 ncm = 0, cur = 0, sidx = 0;
+            u32 chL = 0, chS = 0, chE = 0;
             for (;;) {
                 const u32 e = (u32)__builtin_amdgcn_readlane((int)nt, (int)cur);
                 const u32 nx = (u32)__builtin_amdgcn_readlane((int)nxt, (int)cur);
-                if (lane == 0) { L.u.st.ch_lane[ncm] = (u16)cur; L.u.st.ch_s[ncm] = (u16)sidx; L.u.st.ch_e[ncm] = (u16)e; }
+                if (lane == ncm) { chL = cur; chS = sidx; chE = e; }
                 ncm++;
                 if (nx < 64) {
                     sidx = (u32)__builtin_amdgcn_readlane((int)give, (int)cur);
@@ -629,7 +768,6 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
             const u32 endq = (u32)__builtin_amdgcn_readlane((int)q, (int)cur);  // after the last member's list
             if ((u32)__builtin_amdgcn_readlane((int)nxt, (int)cur) == S_CAP && seg > IW_SEGMIN)
                 seg = (seg / 2 + 31) & ~31u;  // lists overflowed: shorter segments next round
-            if (lane == 0) { L.u.st.ch_lane[ncm] = 0; L.u.st.ch_s[ncm] = 0; L.u.st.ch_e[ncm] = 0; }
             IW_ADD(IWD_CHAIN, ncm);
             // token lists of other lanes are read below: their stores must be done
             __syncthreads();
@@ -640,16 +778,73 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
             // block at absolute B0 + 32 l, B0 = S & ~31 (64 blocks = the ring).
             u32 cm = 0, cj = 0;  // cursor: chain member, token index in its list
             // lane's token at the cursor + lane (a member's list may end inside a group)
+            auto mL = [&](u32 m) -> u32 { return (u32)__builtin_amdgcn_readlane((int)chL, (int)m); };
+            auto mE = [&](u32 m) -> u32 { return (u32)__builtin_amdgcn_readlane((int)chE, (int)m); };
+            auto mS1 = [&](u32 m) -> u32 { return m + 1 < ncm ? (u32)__builtin_amdgcn_readlane((int)chS, (int)(m + 1)) : 0u; };
             auto fetch = [&](u32 cm0, u32 cj0) -> u32 {
-                u32 m = cm0, jj = cj0 + lane;
-                while (m < ncm && jj >= L.u.st.ch_e[m]) { jj = jj - L.u.st.ch_e[m] + L.u.st.ch_s[m + 1]; m++; }
-                return m < ncm ? (u32)gl[(u64)L.u.st.ch_lane[m] * IW_TSTR + jj] : (W_MARK | M_END);
+                u32 jj = cj0 + lane, tl = 0xFFFFFFFFu, tj = 0;
+                for (u32 m = cm0; m < ncm; m++) {  // wave-uniform walk over the members a group spans
+                    const u32 e = mE(m), ln = mL(m);
+                    if (tl == 0xFFFFFFFFu && jj < e) { tl = ln; tj = jj; }
+                    if (__ballot(tl == 0xFFFFFFFFu) == 0) break;
+                    if (tl == 0xFFFFFFFFu) jj = jj - e + mS1(m);
+                }
+                return tl != 0xFFFFFFFFu ? (u32)gl[(u64)tl * IW_TSTR + tj] : (W_MARK | M_END);
             };
             auto advance = [&](u32& cm0, u32& cj0, u32 k) {
                 cj0 += k;
-                while (cm0 < ncm && cj0 >= L.u.st.ch_e[cm0]) { cj0 = cj0 - L.u.st.ch_e[cm0] + L.u.st.ch_s[cm0 + 1]; cm0++; }
+                while (cm0 < ncm) {
+                    const u32 e = mE(cm0);
+                    if (cj0 < e) break;
+                    cj0 = cj0 - e + mS1(cm0);
+                    cm0++;
+                }
             };
-            u32 tk_next = fetch(cm, cj);
+            // The token words of the next IW_GK groups are in flight while a
+            // group is placed (the lists sit in MALL/HBM: ~2 K cycles away).
+            // Each group slot is a named register that is loaded IW_GK groups
+            // before its use, so no in-flight value is copied at the loop's
+            // back edge (a copy would wait for it).  Within a stage every
+            // group but the last is taken whole, so the prefetch positions
+            // are exact; a new stage refetches from its cursor.
+#if ZIW_G2
+            // two chain tokens per lane per group (tokens 2l, 2l + 1): the
+            // group's fixed costs (scan, ballots, cursor walk) are paid once
+            // per 128 tokens
+            auto fetch2 = [&](u32 cm0, u32 cj0, u32& ta, u32& tb) {
+                u32 ja = cj0 + 2 * lane, jb = ja + 1, la = 0xFFFFFFFFu, lb = 0xFFFFFFFFu, pa = 0, pb = 0;
+                for (u32 m = cm0; m < ncm; m++) {
+                    const u32 e = mE(m), ln = mL(m), s1 = mS1(m);
+                    if (la == 0xFFFFFFFFu && ja < e) { la = ln; pa = ja; }
+                    if (lb == 0xFFFFFFFFu && jb < e) { lb = ln; pb = jb; }
+                    if (__ballot(la == 0xFFFFFFFFu || lb == 0xFFFFFFFFu) == 0) break;
+                    if (la == 0xFFFFFFFFu) ja = ja - e + s1;
+                    if (lb == 0xFFFFFFFFu) jb = jb - e + s1;
+                }
+                ta = la != 0xFFFFFFFFu ? (u32)gl[(u64)la * IW_TSTR + pa] : (W_MARK | M_END);
+                tb = lb != 0xFFFFFFFFu ? (u32)gl[(u64)lb * IW_TSTR + pb] : (W_MARK | M_END);
+            };
+            u32 tq0a, tq0b, tq1a, tq1b, tq2a, tq2b;
+            auto refetch = [&]() {
+                u32 cm1 = cm, cj1 = cj;
+                fetch2(cm1, cj1, tq0a, tq0b);
+                advance(cm1, cj1, 128);
+                fetch2(cm1, cj1, tq1a, tq1b);
+                advance(cm1, cj1, 128);
+                fetch2(cm1, cj1, tq2a, tq2b);
+            };
+#else
+            u32 tq0, tq1, tq2;
+            auto refetch = [&]() {
+                u32 cm1 = cm, cj1 = cj;
+                tq0 = fetch(cm1, cj1);
+                advance(cm1, cj1, 64);
+                tq1 = fetch(cm1, cj1);
+                advance(cm1, cj1, 64);
+                tq2 = fetch(cm1, cj1);
+            };
+#endif
+            refetch();
             bool round_done = false;
             while (!round_done && r == R_OK) {
                 const u64 S = P;
@@ -664,13 +859,14 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
                 bool far = false;
                 u32 why = 0;  // 1 final cut, 2 marker / round end, 3 capacity
                 u32 mcode = 0;
-                for (;;) {
+                // place one group of 64 tokens; true when the stage ends
+                auto group = [&](u32& tq) -> bool {
                     IW_ADD(IWD_GROUPS, 1);
-                    const u32 tk = tk_next;
-                    {  // prefetch the next group (right whenever this one is taken whole)
+                    const u32 tk = tq;
+                    {  // this slot's next group: IW_GK groups on
                         u32 cm1 = cm, cj1 = cj;
-                        advance(cm1, cj1, 64);
-                        tk_next = fetch(cm1, cj1);
+                        advance(cm1, cj1, 64 * IW_GK);
+                        tq = fetch(cm1, cj1);
                     }
                     const bool ismk = w_marker(tk);
                     const u64 mm = __ballot(ismk);
@@ -696,7 +892,7 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
                     }
                     if (ntk) emitted += (u32)__builtin_amdgcn_readlane((int)incl, (int)(ntk - 1));
                     advance(cm, cj, ntk);
-                    if (fin && emitted >= cap) { why = 1; break; }
+                    if (fin && emitted >= cap) { why = 1; return true; }
                     if (ntk < 64) {
                         if (ntk == fm) {
                             why = 2;
@@ -704,10 +900,76 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
                         } else {
                             why = 3;
                         }
-                        break;
+                        return true;
                     }
+                    return false;
+                };
+#if ZIW_G2
+                auto place = [&](u32 tk, u32 o) {
+                    u16 v;
+                    if (tk & W_MATCH) {
+                        const u32 d = (tk & 0x7FFF) + 1;
+                        if ((u64)d > S + o) far = true;  // before the stream start
+                        v = (u16)(d - 1);
+                    } else {
+                        v = (u16)(IE_VAL | (tk & 0xFF));
+                    }
+                    const u32 ri = (u32)((S + o) & (IW_S - 1));
+                    L.u.st.ptr[ri] = v;
+                    atomicOr(&L.u.st.head[ri >> 5], 1u << (ri & 31));
+                };
+                auto group2 = [&](u32& tqa, u32& tqb) -> bool {
+                    IW_ADD(IWD_GROUPS, 1);
+                    const u32 ta = tqa, tb = tqb;
+                    {
+                        u32 cm1 = cm, cj1 = cj;
+                        advance(cm1, cj1, 128 * IW_GK);
+                        fetch2(cm1, cj1, tqa, tqb);
+                    }
+                    const u64 ma = __ballot(w_marker(ta)), mb = __ballot(w_marker(tb));
+                    const u32 fa = ma ? 2 * (u32)__builtin_ctzll(ma) : 128u, fb = mb ? 2 * (u32)__builtin_ctzll(mb) + 1 : 128u;
+                    const u32 fm = fa < fb ? fa : fb;  // first marker, in token order
+                    const u32 ia = 2 * lane, ib = ia + 1;
+                    const u32 la = ia < fm ? w_len(ta) : 0u, lb = ib < fm ? w_len(tb) : 0u;
+                    const u32 ps = la + lb;
+                    const u32 incl = iw_incl_scan(ps);
+                    const u32 oa = emitted + incl - ps, ob = oa + la;
+                    const bool ka = ia < fm && (fin ? oa < cap : oa + la <= cap);
+                    const bool kb = ib < fm && (fin ? ob < cap : ob + lb <= cap);
+                    const u32 ntk = (u32)__popcll(__ballot(ka)) + (u32)__popcll(__ballot(kb));
+                    if (ka) place(ta, oa);
+                    if (kb) place(tb, ob);
+                    if (ntk) {
+                        const u32 t = ntk - 1;  // the last taken token: lane t / 2, slot t % 2
+                        const u32 ea = incl - ps + la;
+                        emitted += (u32)__builtin_amdgcn_readlane((int)((t & 1) ? incl : ea), (int)(t >> 1));
+                    }
+                    advance(cm, cj, ntk);
+                    if (fin && emitted >= cap) { why = 1; return true; }
+                    if (ntk < 128) {
+                        if (ntk == fm) {
+                            why = 2;
+                            mcode = (u32)__builtin_amdgcn_readlane((int)((fm & 1) ? tb : ta), (int)(fm >> 1)) & 3u;
+                        } else {
+                            why = 3;
+                        }
+                        return true;
+                    }
+                    return false;
+                };
+                for (;;) {
+                    if (group2(tq0a, tq0b)) break;
+                    if (group2(tq1a, tq1b)) break;
+                    if (group2(tq2a, tq2b)) break;
                 }
-                if (why != 0) tk_next = fetch(cm, cj);  // the next stage starts at the cursor
+#else
+                for (;;) {
+                    if (group(tq0)) break;
+                    if (group(tq1)) break;
+                    if (group(tq2)) break;
+                }
+#endif
+                refetch();  // the next stage starts at the cursor
                 IW_ADD(IWD_STAGES, 1);
                 if (__ballot(far) != 0) { r = R_INVALID; break; }
                 const u32 emit = emitted < cap ? emitted : cap;  // a token may cross N: clip
@@ -760,58 +1022,88 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
                     if (__ballot(nfar != 0)) {
                         const gu8* gd = (const gu8*)dst;
                         const u32 S32 = (u32)S;
+                        // The loads are scattered over 64 lanes' sources, so the
+                        // vector L1's address path (one line per lane request), not
+                        // latency, bounds this phase: four far entries of one match
+                        // (consecutive sources) come as one unaligned dword, the rest
+                        // byte by byte.  16 entries per round.
+                        typedef __attribute__((address_space(1))) u32 gu32_ua __attribute__((aligned(1)));
 #pragma unroll
-                        for (u32 qt = 0; qt < 4; qt++) {
-                            u32 bv[8];
+                        for (u32 qt = 0; qt < 2; qt++) {
+                            u32 qw[4], bv[16], pv[16];
+                            bool run[4];
 #pragma unroll
-                            for (u32 u = 0; u < 8; u++) {
-                                const u32 v = e16(ev, qt * 8 + u);
-                                const int xr = xr0 + (int)(qt * 8 + u);
-                                bv[u] = 0;
-                                if (xr >= 0 && xr < (int)emit && v >= IE_FAR && v < IE_VAL)
-                                    bv[u] = gd[swap_pos32(S32 - (v - IE_FAR + 1), tw)];
+                            for (u32 qd = 0; qd < 4; qd++) {
+                                bool all = !tw.swap;
+#pragma unroll
+                                for (u32 j = 0; j < 4; j++) {
+                                    const u32 k = qt * 16 + qd * 4 + j;
+                                    const u32 v = e16(ev, k);
+                                    const int xr = xr0 + (int)k;
+                                    const bool f = xr >= 0 && xr < (int)emit && v >= IE_FAR && v < IE_VAL;
+                                    pv[qd * 4 + j] = f ? S32 - (v - IE_FAR + 1) : 0xFFFFFFFFu;
+                                    all = all && f && (j == 0 || pv[qd * 4 + j] == pv[qd * 4] + j);
+                                }
+                                run[qd] = all;
+                                qw[qd] = all ? *(const gu32_ua*)(gd + pv[qd * 4]) : 0u;
+#pragma unroll
+                                for (u32 j = 0; j < 4; j++) {
+                                    const u32 pj = pv[qd * 4 + j];
+                                    bv[qd * 4 + j] = (!all && pj != 0xFFFFFFFFu) ? (u32)gd[swap_pos32(pj, tw)] : 0u;
+                                }
                             }
 #pragma unroll
-                            for (u32 u = 0; u < 8; u++) {
-                                const u32 v = e16(ev, qt * 8 + u);
-                                const int xr = xr0 + (int)(qt * 8 + u);
-                                if (xr >= 0 && xr < (int)emit && v >= IE_FAR && v < IE_VAL)
-                                    e16_set(ev, qt * 8 + u, IE_VAL | bv[u]);
-                            }
+                            for (u32 qd = 0; qd < 4; qd++)
+#pragma unroll
+                                for (u32 j = 0; j < 4; j++) {
+                                    const u32 k = qt * 16 + qd * 4 + j;
+                                    const u32 byte = run[qd] ? (qw[qd] >> (8 * j)) & 0xFF : bv[qd * 4 + j];
+                                    if (pv[qd * 4 + j] != 0xFFFFFFFFu) e16_set(ev, k, IE_VAL | byte);
+                                }
                         }
                     }
                     blk_store(L.u.st.ptr + rb, ev);
                     wsync();
                     IW_T(IWT_GATHER);
                     // pointer jumping: every pointer points strictly backwards, so
-                    // log2(IW_S) passes resolve any stage (the cap guards the invariant)
+                    // log2(IW_S) passes resolve any stage (the cap guards the invariant).
+                    // pm = my entries that are still pointers; a pass touches only
+                    // the entry positions some lane still needs (wave OR of pm,
+                    // scalar branches), so later passes cost what is left.
+                    u32 pm = 0;
+#pragma unroll
+                    for (u32 k = 0; k < 32; k++) {
+                        const int xr = xr0 + (int)k;
+                        if (xr >= 0 && xr < (int)emit && e16(ev, k) < IW_S) pm |= 1u << k;
+                    }
                     for (u32 pass = 0;; pass++) {
-                        bool pending = false;
+                        const u32 wm = iw_wave_or(pm);
+                        if (wm == 0) break;
+                        if (pass >= 13) { r = R_INVALID; break; }
 #pragma unroll
                         for (u32 half = 0; half < 2; half++) {
+                            if (((wm >> (16 * half)) & 0xFFFFu) == 0) continue;
                             u32 nw[16];
 #pragma unroll
                             for (u32 u = 0; u < 16; u++) {
                                 const u32 k = half * 16 + u;
-                                const u32 v = e16(ev, k);
-                                const int xr = xr0 + (int)k;
-                                nw[u] = (xr >= 0 && xr < (int)emit && v < IW_S) ? (u32)L.u.st.ptr[v] : v;
+                                nw[u] = 0;
+                                if ((wm >> k) & 1u)
+                                    if ((pm >> k) & 1u) nw[u] = (u32)L.u.st.ptr[e16(ev, k)];
                             }
 #pragma unroll
                             for (u32 u = 0; u < 16; u++) {
                                 const u32 k = half * 16 + u;
-                                const int xr = xr0 + (int)k;
-                                if (xr >= 0 && xr < (int)emit && e16(ev, k) < IW_S) {
-                                    e16_set(ev, k, nw[u]);
-                                    pending |= nw[u] < IW_S;
-                                }
+                                if ((wm >> k) & 1u)
+                                    if ((pm >> k) & 1u) {
+                                        e16_set(ev, k, nw[u]);
+                                        if (nw[u] >= IW_S) pm &= ~(1u << k);
+                                    }
                             }
                         }
                         blk_store(L.u.st.ptr + rb, ev);
                         IW_ADD(IWD_MRR, 1);
                         wsync();
-                        if (__ballot(pending) == 0) break;
-                        if (pass >= 12) { r = R_INVALID; break; }
                     }
                     IW_T(IWT_JUMP);
                     if (r != R_OK) break;
@@ -826,7 +1118,7 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
                     round_done = true;
                     if (boundary) {
                         u32 qn = endq;
-                        if (cm < ncm) qn = iw_pos(gl, L.u.st.ch_lane[cm], cj, R0 + L.u.st.ch_lane[cm] * seg);
+                        if (cm < ncm) qn = iw_pos(gl, mL(cm), cj, R0 + mL(cm) * seg);
                         b.cbase = ~0ull;
                         bi_seek(b, qn);
                     }
@@ -841,7 +1133,7 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
                         u32 sg = (rem / 64 + 31) & ~31u;
                         seg = sg < IW_SEGMIN ? IW_SEGMIN : sg > IW_SEGMAX ? IW_SEGMAX : sg;
                     } else if (mcode == M_EOB) {
-                        const u32 lm = L.u.st.ch_lane[cm];
+                        const u32 lm = mL(cm);
                         const u32 qe = iw_pos(gl, lm, cj + 1, R0 + lm * seg);  // after the EOB code
                         block_end = true;
                         b.cbase = ~0ull;
