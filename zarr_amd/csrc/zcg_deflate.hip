@@ -57,17 +57,18 @@ __constant__ u8 d_dist_extra[30] = {0, 0, 0, 0, 1, 1, 2, 2,  3,  3,  4,  4,  5, 
                                     6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
 __constant__ u8 d_clen_order[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
 
-__device__ __forceinline__ u32 len_code(u32 len) {  // 3..258 -> 0..28
-    u32 c = 0;
-#pragma unroll
-    for (u32 i = 1; i < 29; i++) c += (len >= d_len_base[i]) ? 1u : 0u;
-    return c;
+__device__ __forceinline__ u32 len_code(u32 len) {  // 3..258 -> 0..28 (d_len_base)
+    if (len == 258) return 28;
+    const u32 x = len - 3;
+    if (x < 8) return x;
+    const u32 k = 31 - __builtin_clz(x);  // 3..7
+    return 4 * (k - 1) + ((x >> (k - 2)) & 3);
 }
-__device__ __forceinline__ u32 dist_code(u32 d) {  // 1..32768 -> 0..29
-    u32 c = 0;
-#pragma unroll
-    for (u32 i = 1; i < 30; i++) c += (d >= d_dist_base[i]) ? 1u : 0u;
-    return c;
+__device__ __forceinline__ u32 dist_code(u32 d) {  // 1..32768 -> 0..29 (d_dist_base)
+    const u32 x = d - 1;
+    if (x < 4) return x;
+    const u32 k = 31 - __builtin_clz(x);  // 2..14
+    return 2 * k + ((x >> (k - 1)) & 1);
 }
 __device__ __forceinline__ u32 rev_bits(u32 v, u32 n) { return n ? __builtin_bitreverse32(v) >> (32 - n) : 0u; }
 
@@ -227,28 +228,6 @@ __device__ void parse_pass(DefLds& L, u32 h0, u32 wend, ParseCfg cfg, u32* bp, u
                            const u32* __restrict__ mt, const u8* __restrict__ src, u64 w0, DType t) {
     const u32 lane = lane_id();
     u32 ip = h0;
-    // literal emission for positions [a, b) (b - a <= 64)
-    auto literals = [&](u32 a, u32 b) {
-        const u32 p = a + lane;
-        const bool on = p < b;
-        const u32 byte = on ? (u32)norm_byte(src[swap_pos(w0 + p, t)], t) : 0u;  // serialised byte
-        if (!EMIT) {
-            if (on) atomicAdd(&L.lfreq[byte], 1u);
-            return;
-        }
-        const u32 cw = on ? L.lcode[byte] : 0u;
-        const u32 nb = cw >> 16;
-        if (on && nb == 0) L.ctl[CTL_ERR] = 1;
-        u32 x = nb;  // wave exclusive scan of code lengths
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const u32 y = __shfl_up(x, d, 64);
-            if ((int)lane >= d) x += y;
-        }
-        const u32 tot = __shfl(x, 63, 64);
-        if (on) ring_put(L, *bp + x - nb, cw & 0xFFFF, nb);
-        *bp += tot;
-    };
     while (ip < wend) {
         // keep the ring from wrapping: a group adds < 2 Kbit
         if (EMIT && (*bp >> 5) >= *fw + DF_FLUSH) ring_flush(L, out, fw, *bp >> 5);
@@ -261,38 +240,77 @@ __device__ void parse_pass(DefLds& L, u32 h0, u32 wend, ParseCfg cfg, u32* bp, u
         if (bl > wend - p) bl = wend - p;
         if (bl < 3 || (bl == 3 && p - br > 4096)) bl = 0;  // zlib TOO_FAR
         const unsigned long long mask = __ballot(bl >= 3);
-        // walk the group: successive greedy (lazy) matches from the lane lengths
-        u32 pos = 0;
-        while (pos < gend) {
-            const unsigned long long mm = mask & (~0ull << pos);
-            if (!mm) { literals(ip + pos, ip + gend); pos = gend; break; }
-            u32 f = (u32)__builtin_ctzll(mm);
-            u32 mlen = (u32)__shfl((int)bl, (int)f, 64), mref = (u32)__shfl((int)br, (int)f, 64);
-            if (cfg.lazy && mlen < 32 && f + 1 < gend && ((mask >> (f + 1)) & 1ull)) {
-                const u32 l2 = (u32)__shfl((int)bl, (int)(f + 1), 64);
-                if (l2 > mlen) { f = f + 1; mlen = l2; mref = (u32)__shfl((int)br, (int)f, 64); }
+        // The greedy (lazy) parse of the group as a chain over its positions:
+        // position p steps to p + 1 (literal), p + len (match) or, when the
+        // next position holds a longer match (lazy evaluation), emits a
+        // literal and that match and steps to p + 1 + len'.  The chain from 0
+        // is found by pointer doubling (lane k gets its k-th member in six
+        // ds_bpermute rounds), and the members emit in parallel at bit
+        // offsets from a wave prefix sum: the same parse, decisions and bits
+        // as a serial walk (zlib deflate_slow's order).
+        (void)mask;
+        const u32 bl1 = (u32)__shfl((int)bl, (int)((lane + 1) & 63), 64);
+        const u32 br1 = (u32)__shfl((int)br, (int)((lane + 1) & 63), 64);
+        const bool ism = bl >= 3;
+        const bool lz = cfg.lazy && ism && bl < 32 && lane + 1 < gend && bl1 > bl;
+        const u32 nx = !ism ? lane + 1 : lz ? lane + 1 + bl1 : lane + bl;
+        u32 J[6];
+        J[0] = nx;
+#pragma unroll
+        for (u32 k = 1; k < 6; k++) {
+            const u32 t = (u32)__shfl((int)J[k - 1], (int)(J[k - 1] & 63), 64);
+            J[k] = J[k - 1] < 64 ? t : J[k - 1];
+        }
+        u32 cur = 0;  // position of member #lane
+#pragma unroll
+        for (u32 k = 0; k < 6; k++) {
+            const u32 t = (u32)__shfl((int)J[k], (int)(cur & 63), 64);
+            if ((lane >> k) & 1u) cur = cur < 64 ? t : cur;
+        }
+        const bool mem = cur < gend;
+        const u32 nm = (u32)__popcll(__ballot(mem));  // >= 1: position 0 is a member
+        const u32 lastp = (u32)__builtin_amdgcn_readlane((int)cur, (int)(nm - 1));
+        const u32 pos = (u32)__builtin_amdgcn_readlane((int)nx, (int)lastp);  // first position after the group's chain
+        // my member's unit: literal, match, or literal + match (lazy)
+        const u32 q = cur & 63;
+        const u32 qism = (u32)__shfl((int)(ism ? 1u : 0u), (int)q, 64);
+        const u32 qlz = (u32)__shfl((int)(lz ? 1u : 0u), (int)q, 64);
+        const u32 qbl = (u32)__shfl((int)bl, (int)q, 64), qbr = (u32)__shfl((int)br, (int)q, 64);
+        const u32 qbl1 = (u32)__shfl((int)bl1, (int)q, 64), qbr1 = (u32)__shfl((int)br1, (int)q, 64);
+        const bool hlit = mem && (!qism || qlz);  // a literal at q
+        const bool hmat = mem && qism;            // a match at q (or q + 1 when lazy)
+        const u32 mpos = ip + q + (qlz ? 1u : 0u);
+        const u32 mlen = qlz ? qbl1 : qbl;
+        const u32 d = mpos - (qlz ? qbr1 : qbr);
+        const u32 byte = hlit ? (u32)norm_byte(src[swap_pos(w0 + ip + q, t)], t) : 0u;
+        const u32 lc = hmat ? len_code(mlen) : 0u, dc = hmat ? dist_code(d) : 0u;
+        if (!EMIT) {
+            if (hlit) atomicAdd(&L.lfreq[byte], 1u);
+            if (hmat) { atomicAdd(&L.lfreq[257 + lc], 1u); atomicAdd(&L.dfreq[dc], 1u); }
+        } else {
+            const u32 cw = hlit ? L.lcode[byte] : 0u;
+            const u32 nb = cw >> 16;
+            const u32 lcw = hmat ? L.lcode[257 + lc] : 0u, dcw = hmat ? L.dcode[dc] : 0u;
+            const u32 nl = lcw >> 16, nd = dcw >> 16;
+            const u32 el = hmat ? (u32)d_len_extra[lc] : 0u, ed = hmat ? (u32)d_dist_extra[dc] : 0u;
+            if ((hlit && nb == 0) || (hmat && (nl == 0 || nd == 0))) L.ctl[CTL_ERR] = 1;
+            const u32 nbits = nb + nl + el + nd + ed;
+            u32 x = nbits;  // wave inclusive scan of the units' bit counts
+#pragma unroll
+            for (int dd = 1; dd < 64; dd <<= 1) {
+                const u32 y = (u32)__shfl_up((int)x, dd, 64);
+                if ((int)lane >= dd) x += y;
             }
-            const u32 mpos = ip + f;
-            if (f > pos) literals(ip + pos, ip + f);
-            const u32 d = mpos - mref;
-            const u32 lc = len_code(mlen), dc = dist_code(d);
-            if (!EMIT) {
-                if (lane == 0) { atomicAdd(&L.lfreq[257 + lc], 1u); atomicAdd(&L.dfreq[dc], 1u); }
-            } else {
-                const u32 lcw = L.lcode[257 + lc], dcw = L.dcode[dc];  // uniform reads
-                const u32 nl = lcw >> 16, nd = dcw >> 16;
-                const u32 el = d_len_extra[lc], ed = d_dist_extra[dc];
-                if (lane == 0) {
-                    if (nl == 0 || nd == 0) L.ctl[CTL_ERR] = 1;
-                    u32 b = *bp;
-                    ring_put(L, b, lcw & 0xFFFF, nl); b += nl;
-                    ring_put(L, b, mlen - d_len_base[lc], el); b += el;
-                    ring_put(L, b, dcw & 0xFFFF, nd); b += nd;
-                    ring_put(L, b, d - d_dist_base[dc], ed);
-                }
-                *bp += nl + el + nd + ed;
+            const u32 tot = (u32)__shfl((int)x, 63, 64);
+            u32 b = *bp + x - nbits;
+            if (hlit) { ring_put(L, b, cw & 0xFFFF, nb); b += nb; }
+            if (hmat) {
+                ring_put(L, b, lcw & 0xFFFF, nl); b += nl;
+                ring_put(L, b, mlen - d_len_base[lc], el); b += el;
+                ring_put(L, b, dcw & 0xFFFF, nd); b += nd;
+                ring_put(L, b, d - d_dist_base[dc], ed);
             }
-            pos = f + mlen;
+            *bp += tot;
         }
         ip += pos;
     }
@@ -661,10 +679,11 @@ DfLayout df_layout(u64 D, u32 n) {
 }
 
 __device__ __forceinline__ u32 df_ser1(const u8* src, u64 x, const DType& t) {
-    return norm_byte(src[swap_pos(x, t)], t);
+    return norm_byte(((const gu8*)src)[swap_pos(x, t)], t);
 }
+typedef __attribute__((address_space(1))) u32 df_gu32_ua __attribute__((aligned(1)));
 __device__ __forceinline__ u32 df_ser4(const u8* src, u64 x, const DType& t) {  // bytes x..x+3, LE
-    if (!t.swap && !t.isbool) return ld32(src + x);
+    if (!t.swap && !t.isbool) return *(const df_gu32_ua*)((const gu8*)src + x);  // (global, not flat)
     return df_ser1(src, x, t) | (df_ser1(src, x + 1, t) << 8) | (df_ser1(src, x + 2, t) << 16) |
            (df_ser1(src, x + 3, t) << 24);
 }
@@ -745,7 +764,10 @@ hipError_t launch_deflate(const zcg_array* a, const zcg_chunk* d_chunks, uint32_
     const DfLayout y = df_layout(D, n);
     if (nseg && (ws_bytes < y.total || y.tot >= (1ull << 31))) return hipErrorInvalidValue;
     // zlib's configuration_table: max_chain (capped for the GPU) and nice_length
-    static const u32 chain[10] = {0, 4, 8, 32, 16, 32, 64, 64, 64, 64};
+#ifndef ZCG_DF_CHAIN6
+#define ZCG_DF_CHAIN6 32
+#endif
+    static const u32 chain[10] = {0, 4, 8, 32, 16, 32, ZCG_DF_CHAIN6, 64, 64, 64};
     static const u32 nice[10] = {0, 8, 16, 32, 16, 32, 128, 128, 258, 258};
     u8* w = (u8*)ws;
     if (nseg) {

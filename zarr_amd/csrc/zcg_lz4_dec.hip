@@ -772,16 +772,24 @@ constexpr u32 LZ_LRM = LZ_LRB - 1;
 constexpr u32 LZ_LWG = ZCG_LZ4_LWG;  // lanes (blocks) per workgroup
 
 // ZCG_LZ4_ULDS: the ring is written and read with byte-unaligned
-// ds_write_b128 / ds_read_b128 (gfx950 LDS in the unaligned alignment mode
-// the ROCm driver sets; tools/probe/lds_unaligned checks it).  The lane's
-// LDS block is [16-byte front pad | LZ_LRB ring | 16-byte mirror]: a vector
-// that crosses the ring end is written a second time LZ_LRB bytes lower, and
-// one that touches the ring's first 16 bytes a second time LZ_LRB higher, so
-// any 16 ring bytes are contiguous in the block.
+// ds_write_b128 / ds_read_b128 (gfx950 LDS runs in the unaligned alignment
+// mode; tools/probe/lds_unaligned checks it).  A lane's LDS block is
+// [16-byte pad | LZ_LRB ring | 16-byte mirror] (the mirror repeats the ring's
+// first 16 bytes), so any 16 ring bytes are contiguous.  An append at ring
+// offset w writes its vector at w (past the ring end it lands in the
+// mirror, which is right), then a second time: LZ_LRB lower when it crossed
+// the ring end (the wrapped part lands on the ring start, the rest in the
+// pad), LZ_LRB higher when it touched the ring's first 16 bytes (the
+// mirror; up to 15 bytes spill into the next lane's pad, and past the last
+// lane into 16 spare bytes).
 #ifndef ZCG_LZ4_ULDS
 #define ZCG_LZ4_ULDS 0
 #endif
 constexpr u32 LZ_LSTRIDE = ZCG_LZ4_ULDS ? ZCG_LZ4_LRB + 32 : ZCG_LZ4_LRB;  // LDS bytes per lane
+// a ring source is intact while it is nearer than this: an append writes 16
+// bytes (ULDS) or whole dwords past its k valid ones, which clobbers the ring
+// slots of the bytes 16 (4) bytes short of a full ring back
+constexpr u32 LZ_NEAR = ZCG_LZ4_ULDS ? ZCG_LZ4_LRB - 16 : ZCG_LZ4_LRB - 4;
 typedef __attribute__((ext_vector_type(4))) u32 lz_v4;
 __device__ __forceinline__ void lds_st16_ua(lu8* p, const u32x4& v) {
     const u32 a = (u32)(uintptr_t)p;
@@ -897,7 +905,7 @@ __device__ __forceinline__ u32x4 lz_src16(const LaneRing& O, u32 op, u32 off) {
 #ifdef ZCG_LZ4_DIAG_NOFAR  // timing diagnostic only (wrong bytes): every source from the ring
     if (true) {
 #else
-    if (off < LZ_LRB - 4) {
+    if (off < LZ_NEAR) {
 #endif
         const u32x4 v = O.rd16(p);
         return off < 16 ? lz_pattern(v, off) : v;
@@ -1184,7 +1192,7 @@ __device__ __forceinline__ bool lzq_parse(LzIn2& in, u32& ip, u32& opp, u32 iend
     if (opp < off) return false;
     if ((u64)opp + ml + 5 > cap) return false;
     // the source is in HBM already: prefetch its first vector
-    const bool pre = off >= LZ_LRB - 4 && opp - off + 16 <= O.fl && opp - off + 16 <= O.lim;
+    const bool pre = off >= LZ_NEAR && opp - off + 16 <= O.fl && opp - off + 16 <= O.lim;
     if (pre) fa = opp - off;
     q.ofs = Q_VALID | off | (pre ? Q_PRE : 0u);
     q.ml = ml;
@@ -1270,7 +1278,7 @@ __global__ __launch_bounds__(LZ_LWG, ZCG_LZ4_WPE) void lz4_lanes_kernel(const zc
                                                            u32 S, u32 vflags,
                                                            const Lz4ChunkInfo* __restrict__ info,
                                                            Lz4Slot* __restrict__ slots) {
-    __shared__ __attribute__((aligned(16))) u8 rings[LZ_LWG * LZ_LSTRIDE + ZCG_LZ4_LDS_PAD];
+    __shared__ __attribute__((aligned(16))) u8 rings[LZ_LWG * LZ_LSTRIDE + (ZCG_LZ4_ULDS ? 16 : 0) + ZCG_LZ4_LDS_PAD];
     const u64 g = (u64)blockIdx.x * LZ_LWG + threadIdx.x;
     const u32 c = (u32)(g / S);
     const u32 k = (u32)(g - (u64)c * S);
