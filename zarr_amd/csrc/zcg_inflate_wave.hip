@@ -789,7 +789,8 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
                     if (__ballot(tl == 0xFFFFFFFFu) == 0) break;
                     if (tl == 0xFFFFFFFFu) jj = jj - e + mS1(m);
                 }
-                return tl != 0xFFFFFFFFu ? (u32)gl[(u64)tl * IW_TSTR + tj] : (W_MARK | M_END);
+                const u32 v = gl[tl != 0xFFFFFFFFu ? (u64)tl * IW_TSTR + tj : 0ull];  // (unconditional load)
+                return tl != 0xFFFFFFFFu ? v : (W_MARK | M_END);
             };
             auto advance = [&](u32& cm0, u32& cj0, u32 k) {
                 cj0 += k;
@@ -811,7 +812,12 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
             // two chain tokens per lane per group (tokens 2l, 2l + 1): the
             // group's fixed costs (scan, ballots, cursor walk) are paid once
             // per 128 tokens
-            auto fetch2 = [&](u32 cm0, u32 cj0, u32& ta, u32& tb) {
+            // A slot holds the two raw loaded words and a validity mask (bit 0:
+            // token 2l, bit 1: token 2l + 1; a token past the chain is M_END).
+            // The words are loaded unconditionally (a dummy word otherwise) and
+            // not touched until the slot is consumed: any use of a loaded
+            // register, even a select, waits for it.
+            auto fetch2 = [&](u32 cm0, u32 cj0, u32& ta, u32& tb, u32& ok) {
                 u32 ja = cj0 + 2 * lane, jb = ja + 1, la = 0xFFFFFFFFu, lb = 0xFFFFFFFFu, pa = 0, pb = 0;
                 for (u32 m = cm0; m < ncm; m++) {
                     const u32 e = mE(m), ln = mL(m), s1 = mS1(m);
@@ -821,17 +827,18 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
                     if (la == 0xFFFFFFFFu) ja = ja - e + s1;
                     if (lb == 0xFFFFFFFFu) jb = jb - e + s1;
                 }
-                ta = la != 0xFFFFFFFFu ? (u32)gl[(u64)la * IW_TSTR + pa] : (W_MARK | M_END);
-                tb = lb != 0xFFFFFFFFu ? (u32)gl[(u64)lb * IW_TSTR + pb] : (W_MARK | M_END);
+                ok = (la != 0xFFFFFFFFu ? 1u : 0u) | (lb != 0xFFFFFFFFu ? 2u : 0u);
+                ta = gl[la != 0xFFFFFFFFu ? (u64)la * IW_TSTR + pa : 0ull];
+                tb = gl[lb != 0xFFFFFFFFu ? (u64)lb * IW_TSTR + pb : 0ull];
             };
-            u32 tq0a, tq0b, tq1a, tq1b, tq2a, tq2b;
+            u32 tq0a, tq0b, tq1a, tq1b, tq2a, tq2b, ok0, ok1, ok2;
             auto refetch = [&]() {
                 u32 cm1 = cm, cj1 = cj;
-                fetch2(cm1, cj1, tq0a, tq0b);
+                fetch2(cm1, cj1, tq0a, tq0b, ok0);
                 advance(cm1, cj1, 128);
-                fetch2(cm1, cj1, tq1a, tq1b);
+                fetch2(cm1, cj1, tq1a, tq1b, ok1);
                 advance(cm1, cj1, 128);
-                fetch2(cm1, cj1, tq2a, tq2b);
+                fetch2(cm1, cj1, tq2a, tq2b, ok2);
             };
 #else
             u32 tq0, tq1, tq2;
@@ -918,13 +925,13 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
                     L.u.st.ptr[ri] = v;
                     atomicOr(&L.u.st.head[ri >> 5], 1u << (ri & 31));
                 };
-                auto group2 = [&](u32& tqa, u32& tqb) -> bool {
+                auto group2 = [&](u32& tqa, u32& tqb, u32& okq) -> bool {
                     IW_ADD(IWD_GROUPS, 1);
-                    const u32 ta = tqa, tb = tqb;
+                    const u32 ta = (okq & 1u) ? tqa : (W_MARK | M_END), tb = (okq & 2u) ? tqb : (W_MARK | M_END);
                     {
                         u32 cm1 = cm, cj1 = cj;
                         advance(cm1, cj1, 128 * IW_GK);
-                        fetch2(cm1, cj1, tqa, tqb);
+                        fetch2(cm1, cj1, tqa, tqb, okq);
                     }
                     const u64 ma = __ballot(w_marker(ta)), mb = __ballot(w_marker(tb));
                     const u32 fa = ma ? 2 * (u32)__builtin_ctzll(ma) : 128u, fb = mb ? 2 * (u32)__builtin_ctzll(mb) + 1 : 128u;
@@ -958,9 +965,9 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
                     return false;
                 };
                 for (;;) {
-                    if (group2(tq0a, tq0b)) break;
-                    if (group2(tq1a, tq1b)) break;
-                    if (group2(tq2a, tq2b)) break;
+                    if (group2(tq0a, tq0b, ok0)) break;
+                    if (group2(tq1a, tq1b, ok1)) break;
+                    if (group2(tq2a, tq2b, ok2)) break;
                 }
 #else
                 for (;;) {
