@@ -752,7 +752,7 @@ __global__ __launch_bounds__(256) void lz4_blocks_kernel(const zcg_chunk* __rest
 #define ZCG_LZ4_BUF 1
 #endif
 #ifndef ZCG_LZ4_LANE_MIN_BLOCKS
-#define ZCG_LZ4_LANE_MIN_BLOCKS 196608  // ~12 288 chunks of 16 blocks (measured crossover 8-16 K chunks)
+#define ZCG_LZ4_LANE_MIN_BLOCKS 131072  // 8 192 chunks of 16 blocks (ULDS lane kernel 146 vs wave 140 GiB/s there; 77 vs 137 at 4 096)
 #endif
 #ifndef ZCG_LZ4_NT_FAR
 #define ZCG_LZ4_NT_FAR 0
@@ -774,22 +774,25 @@ constexpr u32 LZ_LWG = ZCG_LZ4_LWG;  // lanes (blocks) per workgroup
 // ZCG_LZ4_ULDS: the ring is written and read with byte-unaligned
 // ds_write_b128 / ds_read_b128 (gfx950 LDS runs in the unaligned alignment
 // mode; tools/probe/lds_unaligned checks it).  A lane's LDS block is
-// [16-byte pad | LZ_LRB ring | 16-byte mirror] (the mirror repeats the ring's
-// first 16 bytes), so any 16 ring bytes are contiguous.  An append at ring
-// offset w writes its vector at w (past the ring end it lands in the
-// mirror, which is right), then a second time: LZ_LRB lower when it crossed
-// the ring end (the wrapped part lands on the ring start, the rest in the
-// pad), LZ_LRB higher when it touched the ring's first 16 bytes (the
-// mirror; up to 15 bytes spill into the next lane's pad, and past the last
-// lane into 16 spare bytes).
+// [LZ_LRB ring | 32-byte mirror]; the mirror's first 16 bytes repeat the
+// ring's first 16, so any 16 ring bytes are contiguous.  An append at ring
+// offset w writes its vector at w (past the ring end it lands in the mirror,
+// which is right), then a second time: at w + LZ_LRB when it touched the
+// ring's first 16 bytes (the mirror), or, when it crossed the ring end, the
+// wrapped part shifted down to the ring start as one aligned vector.  That
+// vector's zero tail clobbers ring slots of bytes >= 98 back, so the ring
+// serves sources nearer than LZ_NEAR = 96 (older ones come from HBM, where
+// everything 64 bytes back is already flushed); the block stays 160 bytes,
+// 64 lanes = 10 KiB, 16 workgroups per CU.
 #ifndef ZCG_LZ4_ULDS
-#define ZCG_LZ4_ULDS 0
+#define ZCG_LZ4_ULDS 1
 #endif
 constexpr u32 LZ_LSTRIDE = ZCG_LZ4_ULDS ? ZCG_LZ4_LRB + 32 : ZCG_LZ4_LRB;  // LDS bytes per lane
-// a ring source is intact while it is nearer than this: an append writes 16
-// bytes (ULDS) or whole dwords past its k valid ones, which clobbers the ring
-// slots of the bytes 16 (4) bytes short of a full ring back
-constexpr u32 LZ_NEAR = ZCG_LZ4_ULDS ? ZCG_LZ4_LRB - 16 : ZCG_LZ4_LRB - 4;
+// a ring source is intact while it is nearer than this: an append writes
+// whole dwords past its k valid bytes (clobbering the slots of bytes a full
+// ring minus 4 back), or with ULDS 16 bytes plus the wrapped vector's zero
+// tail (bytes >= 98 back)
+constexpr u32 LZ_NEAR = ZCG_LZ4_ULDS ? 96u : ZCG_LZ4_LRB - 4;
 typedef __attribute__((ext_vector_type(4))) u32 lz_v4;
 __device__ __forceinline__ void lds_st16_ua(lu8* p, const u32x4& v) {
     const u32 a = (u32)(uintptr_t)p;
@@ -846,7 +849,7 @@ struct LaneRing {
     __device__ __forceinline__ void append16(u32& op, const u32x4& v, u32 k) {
         const u32 w = op & LZ_LRM;
         lds_st16_ua(R + w, v);
-        if (w > LZ_LRB - 16) lds_st16_ua(R + w - LZ_LRB, v);
+        if (w > LZ_LRB - 16) *(__attribute__((address_space(3))) u32x4*)R = win_shift(v, LZ_LRB - w);
         else if (w < 16) lds_st16_ua(R + w + LZ_LRB, v);
         op += k;
     }
@@ -1278,7 +1281,7 @@ __global__ __launch_bounds__(LZ_LWG, ZCG_LZ4_WPE) void lz4_lanes_kernel(const zc
                                                            u32 S, u32 vflags,
                                                            const Lz4ChunkInfo* __restrict__ info,
                                                            Lz4Slot* __restrict__ slots) {
-    __shared__ __attribute__((aligned(16))) u8 rings[LZ_LWG * LZ_LSTRIDE + (ZCG_LZ4_ULDS ? 16 : 0) + ZCG_LZ4_LDS_PAD];
+    __shared__ __attribute__((aligned(16))) u8 rings[LZ_LWG * LZ_LSTRIDE + ZCG_LZ4_LDS_PAD];
     const u64 g = (u64)blockIdx.x * LZ_LWG + threadIdx.x;
     const u32 c = (u32)(g / S);
     const u32 k = (u32)(g - (u64)c * S);
@@ -1306,7 +1309,7 @@ __global__ __launch_bounds__(LZ_LWG, ZCG_LZ4_WPE) void lz4_lanes_kernel(const zc
             for (; i < m; i++) dst[i] = s[i];
             got = cs;
         } else {
-            LaneRing O{(lu8*)(rings + threadIdx.x * LZ_LSTRIDE + (ZCG_LZ4_ULDS ? 16 : 0)), dst, lb, 0, 0};
+            LaneRing O{(lu8*)(rings + threadIdx.x * LZ_LSTRIDE), dst, lb, 0, 0};
             const u64 avail = ch.src_len - so;
             if (ZCG_LZ4_Q && avail >= 64)
                 st = lz4_lane_block_q(s, cs, avail < 0xFFFFFFF0ull ? (u32)avail : 0xFFFFFFF0u, O, ci.bmax, &got);
