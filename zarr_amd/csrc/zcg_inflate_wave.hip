@@ -1020,22 +1020,26 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
                     }
                     u32 nfar = 0;
 #pragma unroll
+                    // branch-free per entry (the lanes' token layouts differ, so
+                    // branches would only juggle exec masks): a token start sets
+                    // the match state (a literal clears it), a continuation steps
+                    // mj; entries outside [0, emit) keep their value (before the
+                    // stage no head bit is set, so the state stays clear there)
                     for (u32 k = 0; k < 32; k++) {
                         const int xr = xr0 + (int)k;
-                        if (xr < 0 || xr >= (int)emit) continue;
-                        u32 v = e16(ev, k);
-                        if ((hw >> k) & 1u) {
-                            if (v >= IE_VAL) { in_match = false; continue; }  // literal: final
-                            mo = xr; md = v + 1; mj = 0; in_match = true;
-                        } else if (!in_match) {
-                            continue;  // (unreachable for a well-formed stage)
-                        } else {
-                            mj = (mj + 1 == md) ? 0 : mj + 1;
-                        }
+                        const bool valid = xr >= 0 && xr < (int)emit;
+                        const u32 v = e16(ev, k);
+                        const bool head = (hw >> k) & 1u;
+                        const bool start = head && v < IE_VAL;
+                        in_match = start || (!head && in_match);
+                        mo = start ? xr : mo;
+                        md = start ? v + 1 : md;
+                        mj = start ? 0u : ((mj + 1 == md) ? 0u : mj + 1);
+                        const bool act = valid && in_match;
                         const int sp = mo - (int)md + (int)mj;
-                        if (sp < 0) { v = IE_FAR - 1 + (u32)(-sp); nfar++; }
-                        else v = (u32)((S + (u32)sp) & (IW_S - 1));
-                        e16_set(ev, k, v);
+                        const u32 nv = sp < 0 ? IE_FAR - 1 + (u32)(-sp) : (u32)((S + (u32)sp) & (IW_S - 1));
+                        e16_set(ev, k, act ? nv : v);
+                        nfar += (act && sp < 0) ? 1u : 0u;
                     }
                     IW_T(IWT_EXPAND);
                     // far codes: bytes before the stage, from the committed output
@@ -1103,22 +1107,25 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
 #pragma unroll
                         for (u32 half = 0; half < 2; half++) {
                             if (((wm >> (16 * half)) & 0xFFFFu) == 0) continue;
+                            // per position: a wave-uniform skip, then branch-free
+                            // lanes (every lane reads; the index is masked into the
+                            // ring, and lanes whose entry is final keep it)
                             u32 nw[16];
 #pragma unroll
                             for (u32 u = 0; u < 16; u++) {
                                 const u32 k = half * 16 + u;
                                 nw[u] = 0;
-                                if ((wm >> k) & 1u)
-                                    if ((pm >> k) & 1u) nw[u] = (u32)L.u.st.ptr[e16(ev, k)];
+                                if ((wm >> k) & 1u) nw[u] = (u32)L.u.st.ptr[e16(ev, k) & (IW_S - 1)];
                             }
 #pragma unroll
                             for (u32 u = 0; u < 16; u++) {
                                 const u32 k = half * 16 + u;
-                                if ((wm >> k) & 1u)
-                                    if ((pm >> k) & 1u) {
-                                        e16_set(ev, k, nw[u]);
-                                        if (nw[u] >= IW_S) pm &= ~(1u << k);
-                                    }
+                                if ((wm >> k) & 1u) {
+                                    const bool pk = (pm >> k) & 1u;
+                                    const u32 v = pk ? nw[u] : e16(ev, k);
+                                    e16_set(ev, k, v);
+                                    pm &= (pk && v >= IW_S) ? ~(1u << k) : ~0u;
+                                }
                             }
                         }
                         blk_store(L.u.st.ptr + rb, ev);
