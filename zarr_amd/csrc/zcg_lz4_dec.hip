@@ -787,6 +787,9 @@ constexpr u32 LZ_LWG = ZCG_LZ4_LWG;  // lanes (blocks) per workgroup
 #ifndef ZCG_LZ4_ULDS
 #define ZCG_LZ4_ULDS 1
 #endif
+#ifndef ZCG_LZ4_PERM
+#define ZCG_LZ4_PERM 1
+#endif
 constexpr u32 LZ_LSTRIDE = ZCG_LZ4_ULDS ? ZCG_LZ4_LRB + 32 : ZCG_LZ4_LRB;  // LDS bytes per lane
 // a ring source is intact while it is nearer than this: an append writes
 // whole dwords past its k valid bytes (clobbering the slots of bytes a full
@@ -900,10 +903,46 @@ __device__ __forceinline__ u32x4 lz_pattern(u32x4 v, u32 off) {
     return u32x4{(u32)lo, (u32)(lo >> 32), (u32)hi, (u32)(hi >> 32)};
 }
 
+// v_perm_b32 selectors of the period-`off` pattern (off < 16): output dword d
+// = perm(v.y, v.x, lo[d]) | perm(v.w, v.z, hi[d]); byte j takes source byte
+// j mod off (0x0C selects a zero byte).  One table row per offset replaces
+// the doubling loop of lz_pattern (up to four 128-bit shift rounds).
+__constant__ __attribute__((aligned(16))) u32 c_lz_pat[16][8] = {
+    {0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x0C0C0C0Cu, 0x0C0C0C0Cu, 0x0C0C0C0Cu, 0x0C0C0C0Cu},
+    {0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x0C0C0C0Cu, 0x0C0C0C0Cu, 0x0C0C0C0Cu, 0x0C0C0C0Cu},
+    {0x01000100u, 0x01000100u, 0x01000100u, 0x01000100u, 0x0C0C0C0Cu, 0x0C0C0C0Cu, 0x0C0C0C0Cu, 0x0C0C0C0Cu},
+    {0x00020100u, 0x01000201u, 0x02010002u, 0x00020100u, 0x0C0C0C0Cu, 0x0C0C0C0Cu, 0x0C0C0C0Cu, 0x0C0C0C0Cu},
+    {0x03020100u, 0x03020100u, 0x03020100u, 0x03020100u, 0x0C0C0C0Cu, 0x0C0C0C0Cu, 0x0C0C0C0Cu, 0x0C0C0C0Cu},
+    {0x03020100u, 0x02010004u, 0x01000403u, 0x00040302u, 0x0C0C0C0Cu, 0x0C0C0C0Cu, 0x0C0C0C0Cu, 0x0C0C0C0Cu},
+    {0x03020100u, 0x01000504u, 0x05040302u, 0x03020100u, 0x0C0C0C0Cu, 0x0C0C0C0Cu, 0x0C0C0C0Cu, 0x0C0C0C0Cu},
+    {0x03020100u, 0x00060504u, 0x04030201u, 0x01000605u, 0x0C0C0C0Cu, 0x0C0C0C0Cu, 0x0C0C0C0Cu, 0x0C0C0C0Cu},
+    {0x03020100u, 0x07060504u, 0x03020100u, 0x07060504u, 0x0C0C0C0Cu, 0x0C0C0C0Cu, 0x0C0C0C0Cu, 0x0C0C0C0Cu},
+    {0x03020100u, 0x07060504u, 0x0201000Cu, 0x06050403u, 0x0C0C0C0Cu, 0x0C0C0C0Cu, 0x0C0C0C00u, 0x0C0C0C0Cu},
+    {0x03020100u, 0x07060504u, 0x01000C0Cu, 0x05040302u, 0x0C0C0C0Cu, 0x0C0C0C0Cu, 0x0C0C0100u, 0x0C0C0C0Cu},
+    {0x03020100u, 0x07060504u, 0x000C0C0Cu, 0x04030201u, 0x0C0C0C0Cu, 0x0C0C0C0Cu, 0x0C020100u, 0x0C0C0C0Cu},
+    {0x03020100u, 0x07060504u, 0x0C0C0C0Cu, 0x03020100u, 0x0C0C0C0Cu, 0x0C0C0C0Cu, 0x03020100u, 0x0C0C0C0Cu},
+    {0x03020100u, 0x07060504u, 0x0C0C0C0Cu, 0x0201000Cu, 0x0C0C0C0Cu, 0x0C0C0C0Cu, 0x03020100u, 0x0C0C0C04u},
+    {0x03020100u, 0x07060504u, 0x0C0C0C0Cu, 0x01000C0Cu, 0x0C0C0C0Cu, 0x0C0C0C0Cu, 0x03020100u, 0x0C0C0504u},
+    {0x03020100u, 0x07060504u, 0x0C0C0C0Cu, 0x000C0C0Cu, 0x0C0C0C0Cu, 0x0C0C0C0Cu, 0x03020100u, 0x0C060504u}};
+struct LzPat {
+    u32x4 lo, hi;
+};
+__device__ __forceinline__ LzPat lz_pat_sel(u32 off) {  // any off: rows past 15 read row 0
+    const u32 r = off < 16 ? off : 0u;
+    const __attribute__((address_space(1))) u32x4* t = (const __attribute__((address_space(1))) u32x4*)&c_lz_pat[r][0];
+    return LzPat{t[0], t[1]};
+}
+__device__ __forceinline__ u32x4 lz_pattern_perm(const u32x4& v, const LzPat& s) {
+    return u32x4{__builtin_amdgcn_perm(v.y, v.x, s.lo.x) | __builtin_amdgcn_perm(v.w, v.z, s.hi.x),
+                 __builtin_amdgcn_perm(v.y, v.x, s.lo.y) | __builtin_amdgcn_perm(v.w, v.z, s.hi.y),
+                 __builtin_amdgcn_perm(v.y, v.x, s.lo.z) | __builtin_amdgcn_perm(v.w, v.z, s.hi.z),
+                 __builtin_amdgcn_perm(v.y, v.x, s.lo.w) | __builtin_amdgcn_perm(v.w, v.z, s.hi.w)};
+}
+
 // the 16 output bytes at op - off (off >= 1; periodic when off < 16): from the
 // ring when the source is near (its slots are not yet reused: off < LZ_LRB - 4,
 // the 4 covering the stale tail of the last written dword), else from HBM
-__device__ __forceinline__ u32x4 lz_src16(const LaneRing& O, u32 op, u32 off) {
+__device__ __forceinline__ u32x4 lz_src16(const LaneRing& O, u32 op, u32 off, const LzPat* ps = nullptr) {
     const u32 p = op - off;
 #ifdef ZCG_LZ4_DIAG_NOFAR  // timing diagnostic only (wrong bytes): every source from the ring
     if (true) {
@@ -911,6 +950,7 @@ __device__ __forceinline__ u32x4 lz_src16(const LaneRing& O, u32 op, u32 off) {
     if (off < LZ_NEAR) {
 #endif
         const u32x4 v = O.rd16(p);
+        if (ps) return off < 16 ? lz_pattern_perm(v, *ps) : v;
         return off < 16 ? lz_pattern(v, off) : v;
     }
     if (p + 16 <= O.lim) {
@@ -1037,10 +1077,16 @@ __device__ __forceinline__ int lz4_lane_block(const u8* __restrict__ src, u32 ie
         if (op < off) return ZCG_ERR_INVALID_DATA;
         if ((u64)op + ml + 5 > cap) return ZCG_ERR_INVALID_DATA;
         if (ip - in.wb > 8) in.at(ip);  // the next sequence's window, in flight during the copy
+#if ZCG_LZ4_PERM
+        const LzPat ps = lz_pat_sel(off);  // (loaded for every sequence: counted by the waits)
+        const LzPat* psp = &ps;
+#else
+        const LzPat* psp = nullptr;
+#endif
         for (u32 r = ml; r > 0;) {
             const u32 k = r < 16 ? r : 16;
             // lz4 1.9.3 decodes offset 0 to zeros
-            const u32x4 v = off ? lz_src16(O, op, off) : u32x4{0u, 0u, 0u, 0u};
+            const u32x4 v = off ? lz_src16(O, op, off, psp) : u32x4{0u, 0u, 0u, 0u};
             O.append16(op, v, k);
             O.flush(op);
             r -= k;
