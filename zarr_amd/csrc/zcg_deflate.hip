@@ -721,13 +721,22 @@ __global__ void df_best(const zcg_chunk* __restrict__ chunks, u32 c0, u64 D, u64
         const u8* src = (const u8*)chunks[c0 + cl].src;
         const u64 cbase = (u64)cl * D;
         const u32 mx = (D - p) < 258 ? (u32)(D - p) : 258u;
+        // bytes p+3..p+6 are compared with every candidate: load them once;
+        // the next chain link is loaded before this candidate's compare
+        const u32 pw = mx >= 7 ? df_ser4(src, p + 3, t) : 0u;
         u32 q = prev[g];
         for (u32 dep = 0; dep < depth && q != 0xFFFFFFFFu; dep++) {
             const u64 qp = q - cbase;
             if (p - qp > DF_HIST) break;
+            const u32 qn = prev[q];
             u32 k = 3;  // the 3 key bytes are equal
             bool diff = false;
-            while (k + 4 <= mx) {
+            if (mx >= 7) {
+                const u32 x = pw ^ df_ser4(src, qp + 3, t);
+                if (x) { k += (u32)__builtin_ctz(x) >> 3; diff = true; }
+                else k = 7;
+            }
+            while (!diff && k + 4 <= mx) {
                 const u32 x = df_ser4(src, p + k, t) ^ df_ser4(src, qp + k, t);
                 if (x) { k += (u32)__builtin_ctz(x) >> 3; diff = true; break; }
                 k += 4;
@@ -736,7 +745,7 @@ __global__ void df_best(const zcg_chunk* __restrict__ chunks, u32 c0, u64 D, u64
                 while (k < mx && df_ser1(src, p + k, t) == df_ser1(src, qp + k, t)) k++;
             if (k > best && !(k == 3 && p - qp > 4096)) { best = k; bd = (u32)(p - qp); }
             if (best >= nice) break;
-            q = prev[q];
+            q = qn;
         }
     }
     match[g] = best ? (best | ((bd - 1) << 16)) : 0u;
