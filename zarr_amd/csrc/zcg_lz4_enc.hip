@@ -318,8 +318,9 @@ LzLayout lz_layout(u64 D, u32 nbpc, u32 n) {
     return y;
 }
 
+typedef __attribute__((address_space(1))) u32 le_gu32_ua __attribute__((aligned(1)));
 __device__ __forceinline__ u32 lz_ser4(const u8* src, u64 x, const DType& t) {  // bytes x..x+3, LE
-    if (!t.swap && !t.isbool) return ld32(src + x);
+    if (!t.swap && !t.isbool) return *(const le_gu32_ua*)((const __attribute__((address_space(1))) u8*)src + x);  // (global, not flat)
     return (u32)src_byte(src, x, t) | ((u32)src_byte(src, x + 1, t) << 8) | ((u32)src_byte(src, x + 2, t) << 16) |
            ((u32)src_byte(src, x + 3, t) << 24);
 }
@@ -366,6 +367,7 @@ __global__ void lz_best(const zcg_chunk* __restrict__ chunks, u32 c0, u64 D, u32
         for (u32 dep = 0; dep < LZ_DEPTH && q != 0xFFFFFFFFu; dep++) {
             const u64 qp = q - cbase;
             if (p - qp > 65535) break;
+            const u32 qn = prev[q];  // the next link, in flight during this candidate's compare
             if (lz_ser4(src, qp, t) == v0) {
                 u32 k = 4;
                 bool diff = false;
@@ -379,7 +381,7 @@ __global__ void lz_best(const zcg_chunk* __restrict__ chunks, u32 c0, u64 D, u32
                 if (k > mx) k = mx;
                 if (k > best) { best = k; bd = (u32)(p - qp); }
             }
-            q = prev[q];
+            q = qn;
         }
     }
     match[g] = best >= 4 ? (best | (bd << 16)) : 0u;

@@ -518,8 +518,9 @@ XeLayout xe_layout(u64 D, u32 n) {
 }
 
 // serialised bytes x..x+3 of a chunk (little-endian in the result)
+typedef __attribute__((address_space(1))) u32 xe_gu32_ua __attribute__((aligned(1)));
 __device__ __forceinline__ u32 xe_ser4(const u8* src, u64 x, const DType& t) {
-    if (!t.swap && !t.isbool) return ld32(src + x);
+    if (!t.swap && !t.isbool) return *(const xe_gu32_ua*)((const __attribute__((address_space(1))) u8*)src + x);  // (global, not flat)
     return (u32)norm_byte(src[swap_pos(x, t)], t) | ((u32)norm_byte(src[swap_pos(x + 1, t)], t) << 8) |
            ((u32)norm_byte(src[swap_pos(x + 2, t)], t) << 16) | ((u32)norm_byte(src[swap_pos(x + 3, t)], t) << 24);
 }
@@ -563,6 +564,7 @@ __global__ void xe_best(const zcg_chunk* __restrict__ chunks, u32 c0, u64 D, u64
         for (u32 dep = 0; dep < XE_DEPTH && q != 0xFFFFFFFFu; dep++) {
             const u64 qp = q - cbase;
             if (p - qp >= dsize) break;  // beyond the preset's dictionary
+            const u32 qn = prev[q];  // the next link, in flight during this candidate's compare
             if (xe_ser4(src, qp, t) == v0) {
                 u32 k = 4;
                 bool diff = false;
@@ -576,7 +578,7 @@ __global__ void xe_best(const zcg_chunk* __restrict__ chunks, u32 c0, u64 D, u64
                 if (k > best) { best = k; bd = (u32)(p - qp); }
                 if (best >= XE_NICE) break;
             }
-            q = prev[q];
+            q = qn;
         }
     }
     blen[g] = (u16)best;
