@@ -64,14 +64,17 @@ enum zcg_status {
     ZCG_ERR_OUTPUT_TOO_SMALL = 5, /* encode: dst capacity below the stream size */
     ZCG_ABSENT = 6,             /* store: no chunk file (get() -> Ok(None), read_chunk -> None) */
     ZCG_ERR_IO = 7,             /* store: a filesystem error (open/lock/read/write)  */
+    ZCG_ERR_NOT_FOUND = 8,      /* store: key outside the hierarchy (io::ErrorKind::NotFound,
+                                   filesystem.rs:180-186)                        */
     ZCG_ERR_RUNTIME = 100       /* HIP runtime failure (see zcg_last_error)     */
 };
 
-/* Decode verification flags (zcg_compression.flags).  The reference's
- * read_exact never reaches the gzip trailer / LZ4 content checksum on a
- * full-length read, so these default OFF. */
-#define ZCG_FLAG_VERIFY_GZIP_CRC 0x1u
-#define ZCG_FLAG_VERIFY_LZ4_CONTENT_CHECKSUM 0x2u
+/* Decode flags (zcg_compression.flags).  The reference's read_exact never
+ * reaches the gzip CRC32/ISIZE trailer or the LZ4 content checksum on a
+ * full-length read, so neither is verified.  LZ4
+ * block checksums are verified as LZ4F does, unless this flag skips them
+ * (the decoded bytes are the same; only a corrupt checksum word changes the
+ * status).  Bits 0x1 and 0x2 are reserved. */
 #define ZCG_FLAG_SKIP_LZ4_BLOCK_CHECKSUM 0x4u
 /* Use the wave-serial inflate kernel instead of the parallel one (the two are
  * bit-identical; the serial one is kept as a differential reference). */
@@ -132,6 +135,10 @@ typedef struct zcg_ctx zcg_ctx;
 
 /* ---- context -------------------------------------------------------- */
 int zcg_abi_version(void);
+/* The kernels' tuning constants this library was built with, as
+ * "kernel:K=V,...;kernel:K=V,..." (A/B builds under tools/ change them; the
+ * product build uses the defaults, which tests/test_abi.py checks). */
+const char* zcg_build_config(void);
 zcg_ctx* zcg_create(int device);
 void zcg_destroy(zcg_ctx* ctx);
 const char* zcg_last_error(const zcg_ctx* ctx);
@@ -324,6 +331,18 @@ int zcg_array_meta_from_json(const char* json, uint64_t len, zcg_array_meta* out
  * (filesystem.rs:142-190). */
 uint64_t zcg_chunk_key(const char* path, const char* separator, const uint64_t* grid_position, uint32_t ndim,
                        char* out, uint64_t cap);
+
+/* FilesystemHierarchy::get_path (src/store/filesystem.rs:151-190): the file a
+ * key names under the store root `root`.  The key's leading '/'s are dropped
+ * (it is taken relative to the root), empty and "." components vanish, ".."
+ * stays in the path, and the key is refused with ZCG_ERR_NOT_FOUND when its
+ * NET nesting (+1 per normal component, -1 per "..") is negative — the
+ * reference's rule, so "a/../b" and even "../x" (net 0) are accepted, "../../x"
+ * is not.  The path is
+ * root + '/' + the normalised key.  *path_len (optional) receives its length;
+ * `out` (cap bytes, NUL-terminated) may be NULL to query the length, and a cap
+ * below path_len + 1 gives ZCG_ERR_OUTPUT_TOO_SMALL.  Returns ZCG_OK. */
+int zcg_store_path(const char* root, const char* key, char* out, uint64_t cap, uint64_t* path_len);
 
 #ifdef __cplusplus
 }

@@ -68,9 +68,11 @@ int main(int argc, char** argv) {
         const uint64_t klen = zcg_chunk_key(array_path, m.separator, pos, 3, NULL, 0);
         char* key = (char*)malloc(klen + 1);
         zcg_chunk_key(array_path, m.separator, pos, 3, key, klen + 1);
-        paths[i] = (char*)malloc(strlen(root) + klen + 1);
-        strcpy(paths[i], root);
-        strcat(paths[i], key);  /* the key is rooted: "/data/root/seq/i2/c<i>/<j>/<k>" */
+        /* the store's get_path (filesystem.rs:151-190): root joined with the key */
+        uint64_t plen = 0;
+        if (zcg_store_path(root, key, NULL, 0, &plen) != ZCG_OK) { fprintf(stderr, "zcg_store_path(%s)\n", key); return 1; }
+        paths[i] = (char*)malloc(plen + 1);
+        if (zcg_store_path(root, key, paths[i], plen + 1, NULL) != ZCG_OK) return 1;
         free(key);
         dsts[i] = malloc(N * 2);
     }

@@ -43,6 +43,27 @@ def test_abi_version_and_pure_helpers():
     assert L.zcg_codec_on_gpu(0, 0) == 1
 
 
+# The product build's tuning constants (A/B builds under tools/ pass -D
+# overrides; the shipped library must not be one of them).
+DEFAULT_BUILD_CONFIG = ("inflate_wave:S=2048,TCAP=768,WPE=4,EST_PCT=108,MARKW=32;"
+                        "inflate_par:PF=16,FU=16,WPE=3;deflate:CHAIN6=32;raw:VPT=1;region:U=4")
+
+
+def test_library_built_with_default_knobs():
+    L = _native.load_library()
+    assert L.zcg_build_config().decode() == DEFAULT_BUILD_CONFIG
+
+
+def test_product_sources_hold_no_diagnostic_modes():
+    """Timing-diagnostic modes that produce wrong output live in tools/, not in
+    the product kernels."""
+    srcs = glob.glob(os.path.join(ROOT, "zarr_amd", "csrc", "*.hip")) + \
+        glob.glob(os.path.join(ROOT, "zarr_amd", "csrc", "*.h"))
+    for p in srcs:
+        txt = open(p).read()
+        assert "DIAG" not in txt, p
+
+
 def test_struct_layout_matches_header():
     """sizeof checks mirrored from include/zchunk_gpu.h (compiled with gcc)."""
     import subprocess

@@ -268,6 +268,42 @@ def test_lz4_large(data, variant):
     check("lz4", s, "<i2", len(payload) // 2)
 
 
+def test_lz4_skip_block_checksum_flag():
+    """ZCG_FLAG_SKIP_LZ4_BLOCK_CHECKSUM: a frame with block checksums whose
+    checksum words are corrupt is InvalidData by default (LZ4F verifies them,
+    as the oracle does) and decodes to the intact payload with the flag, on
+    both block decoders."""
+    import torch
+    from zarr_amd._native import FLAG_SKIP_LZ4_BLOCK_CHECKSUM
+    from zarr_amd.batch import BatchCodec, PackedStreams
+    payload = rw(300000).tobytes()
+    s = zref.lz4_frame_custom(payload, block_checksum=True)
+    # walk the blocks (7-byte header: magic, FLG, BD, HC) and corrupt every checksum word
+    bad = bytearray(s)
+    pos, nblk = 7, 0
+    while True:
+        bs = struct.unpack_from("<I", bad, pos)[0]
+        if bs == 0:
+            break
+        n = bs & 0x7FFFFFFF
+        bad[pos + 4 + n] ^= 0x5A
+        pos += 4 + n + 4
+        nblk += 1
+    assert nblk >= 4
+    st_ref, _ = zref.decode_batch(zref.LZ4, [np.frombuffer(bytes(bad), np.uint8)], len(payload))
+    assert st_ref[0] == zref.INVALID_DATA
+    for lz4_sel in (0, 0x800, 0x1000):
+        for flags, want in ((0, zref.INVALID_DATA), (FLAG_SKIP_LZ4_BLOCK_CHECKSUM, zref.OK)):
+            packed = PackedStreams([bytes(bad)] * 3, len(payload), "cuda:0")
+            BatchCodec(0).decode(meta_for("lz4", "u1", len(payload)), packed, flags=flags | lz4_sel)
+            torch.cuda.synchronize()
+            st = packed.status.cpu().numpy()
+            assert (st == want).all(), (lz4_sel, flags, st)
+            if want == zref.OK:
+                out = packed.dst.cpu().numpy().reshape(3, len(payload))
+                assert all(out[i].tobytes() == payload for i in range(3))
+
+
 def test_lz4_errors():
     payload = rw(300000).tobytes()
     st, s = zref.encode(zref.LZ4, 65536, np.frombuffer(payload, np.uint8))
@@ -384,9 +420,11 @@ def test_lz4_next_header_after_n_bytes():
 
 @pytest.mark.parametrize("data", list(DATASETS))
 def test_inflate_parallel_vs_serial_kernel(data):
-    """The speculative parallel inflate kernel and the wave-serial one must
-    agree bit for bit (and with the oracle) on every deflate structure."""
-    from zarr_amd._native import FLAG_SERIAL_INFLATE
+    """The speculative inflate kernels (one wave per chunk, the default; the
+    256-lane round kernel, FLAG_INFLATE_BLOCK_PAR) and the wave-serial one
+    must agree bit for bit (and with the oracle) on every deflate structure;
+    the debug-counter flag must not change the output."""
+    from zarr_amd._native import FLAG_DEBUG_COUNTERS, FLAG_INFLATE_BLOCK_PAR, FLAG_SERIAL_INFLATE
     payload = DATASETS[data]()
     streams = [gzip_wrap(deflate(payload, lvl, strat), payload)
                for lvl, strat in ((1, 0), (6, 0), (9, 0), (6, zlib.Z_HUFFMAN_ONLY), (6, zlib.Z_RLE))]
@@ -395,8 +433,13 @@ def test_inflate_parallel_vs_serial_kernel(data):
             meta = meta_for("gzip", "u1", D)
             a = DefaultChunk.read_chunk(s, meta, [0], np.uint8).get_data()
             b = DefaultChunk.read_chunk(s, meta, [0], np.uint8, flags=FLAG_SERIAL_INFLATE).get_data()
-            assert np.array_equal(a, b)
+            c = DefaultChunk.read_chunk(s, meta, [0], np.uint8, flags=FLAG_INFLATE_BLOCK_PAR).get_data()
+            assert np.array_equal(a, b) and np.array_equal(a, c)
             assert a.tobytes() == payload[:D]
+    s = streams[1]
+    meta = meta_for("gzip", "u1", len(payload))
+    for f in (FLAG_DEBUG_COUNTERS, FLAG_DEBUG_COUNTERS | FLAG_INFLATE_BLOCK_PAR):
+        assert DefaultChunk.read_chunk(s, meta, [0], np.uint8, flags=f).get_data().tobytes() == payload
 
 
 @pytest.mark.parametrize("codec", ["gzip", "lz4", "raw", "xz", "bzip2"])
@@ -404,14 +447,14 @@ def test_decode_never_writes_past_n(codec):
     """read_exact stops at byte N even inside a long match: the bytes after
     N*elem_size in the caller's buffer stay untouched (chunk.rs:112-113)."""
     import torch
-    from zarr_amd._native import FLAG_SERIAL_INFLATE
+    from zarr_amd._native import FLAG_INFLATE_BLOCK_PAR, FLAG_SERIAL_INFLATE
     from zarr_amd.batch import BatchCodec, PackedStreams
     payloads = [bytes(300000), (b"abcdefgh" * 40000), rw(150000).tobytes()]
     streams = [zref.encode(CODEC_IDS[codec], DEFAULT_PARAM[codec], np.frombuffer(p, np.uint8))[1]
                for p in payloads]
     guard = 4096
     for D in (1, 777, 16385, 65537, 99999, 200003):
-        flag_sets = (0, FLAG_SERIAL_INFLATE) if codec == "gzip" else (0,)
+        flag_sets = (0, FLAG_SERIAL_INFLATE, FLAG_INFLATE_BLOCK_PAR) if codec == "gzip" else (0,)
         for flags in flag_sets:
             dst = torch.full((len(streams) * (D + guard),), 0xAB, dtype=torch.uint8, device="cuda:0")
             packed = PackedStreams(streams, D + guard, "cuda:0", dst=dst)
@@ -445,9 +488,10 @@ def check_many(codec, streams, dt, n, flags=0):
 
 def test_gzip_dynamic_header_corruption():
     """Every byte of three dynamic block headers (the first, and two after
-    full flushes) flipped several ways: the block-parallel header decoder must
-    classify and decode exactly like zlib."""
-    from zarr_amd._native import FLAG_SERIAL_INFLATE
+    full flushes) flipped several ways: the wave-parallel header decoder (and
+    the 256-lane kernel's block-parallel one) must classify and decode exactly
+    like zlib."""
+    from zarr_amd._native import FLAG_INFLATE_BLOCK_PAR, FLAG_SERIAL_INFLATE
     parts = [rw(20000, seed=s).tobytes() for s in range(3)]
     c = zlib.compressobj(6, zlib.DEFLATED, -15)
     raw, offs = b"", []
@@ -465,5 +509,5 @@ def test_gzip_dynamic_header_corruption():
                 bad = bytearray(s)
                 bad[hdr + off + k] ^= x
                 variants.append(bytes(bad))
-    for flags in (0, FLAG_SERIAL_INFLATE):
+    for flags in (0, FLAG_SERIAL_INFLATE, FLAG_INFLATE_BLOCK_PAR):
         check_many("gzip", variants, "u1", len(payload), flags)

@@ -2,6 +2,7 @@
 SURVEY §8(f) rank 4) against the host mirror (zarr_amd.metadata, itself
 pinned to the reference's serde rules: lib.rs:382-402, data_type.rs:125-251,
 compression/mod.rs:36-51).  Pure host code: runs without a GPU."""
+import ctypes
 import json
 import os
 import struct
@@ -206,3 +207,45 @@ def test_chunk_key_matches_get_chunk_key():
                 meta = ArrayMetadata.new([1] * max(len(grid), 1), [1] * max(len(grid), 1), "<i2", Raw())
                 meta.separator = sep
                 assert chunk_key_native(path, sep, grid) == get_chunk_key(path, meta, grid), (path, sep, grid)
+
+
+def test_store_path_net_nesting_rule(tmp_path):
+    """zcg_store_path is FilesystemHierarchy::get_path (filesystem.rs:151-190):
+    leading '/'s dropped, '.' and empty components dropped, '..' kept, and
+    NotFound only when the NET nesting is negative (not a prefix check)."""
+    root = str(tmp_path)
+    ok = {
+        "/data/root/c0/0": root + "/data/root/c0/0",
+        "a/../b": root + "/a/../b",          # net 1: accepted, '..' left to the OS
+        "/./c0/0": root + "/c0/0",
+        "//a//b/": root + "/a/b",
+        "../a/b": root + "/../a/b",          # net 1: the reference accepts it too
+        "a/../../b": root + "/a/../../b",    # net 0: accepted (prefix escape the rule allows)
+        "": root,
+        "/": root,
+        ".": root,
+    }
+    for key, want in ok.items():
+        st, p = _native.store_path(root, key)
+        assert st == _native.OK and p == want, (key, st, p)
+    # "../x" nets 0: the reference accepts it (its check is the net count only)
+    st, p = _native.store_path(root, "../x")
+    assert st == _native.OK and p == root + "/../x"
+    for key in ("..", "/../", "../../x", "a/../../x/..", "./../", "a/b/../../.."):
+        st, p = _native.store_path(root, key)
+        assert st == _native.NOT_FOUND, (key, st, p)
+    # the Python store goes through the same rule
+    from zarr_amd.storage import FilesystemHierarchy
+    from zarr_amd.chunk import ZarrIOError
+    h = FilesystemHierarchy.open_or_create(root)
+    assert h._path("a/../b") == root + "/a/../b"
+    with pytest.raises(ZarrIOError) as e:
+        h._path("/../../x")
+    assert e.value.kind == "NotFound"
+    # a too-small buffer reports the length
+    L = _native.load_library()
+    n = ctypes.c_uint64(0)
+    buf = ctypes.create_string_buffer(4)
+    assert L.zcg_store_path(root.encode(), b"abc", ctypes.addressof(buf), 4, ctypes.byref(n)) == \
+        _native.OUTPUT_TOO_SMALL
+    assert n.value == len(root) + 4

@@ -15,10 +15,9 @@ LIB_PATH = os.environ.get("ZCG_LIB") or os.path.join(_HERE, "libzchunk_gpu.so")
 
 OK, UNEXPECTED_EOF, INVALID_DATA, INVALID_INPUT, UNSUPPORTED, OUTPUT_TOO_SMALL = 0, 1, 2, 3, 4, 5
 ABSENT, IO = 6, 7  # store: no chunk file (read_chunk -> None); filesystem error
+NOT_FOUND = 8  # store: key outside the hierarchy (filesystem.rs:180-186)
 RUNTIME = 100
 
-FLAG_VERIFY_GZIP_CRC = 0x1
-FLAG_VERIFY_LZ4_CONTENT_CHECKSUM = 0x2
 FLAG_SKIP_LZ4_BLOCK_CHECKSUM = 0x4
 FLAG_SERIAL_INFLATE = 0x100
 FLAG_DEBUG_COUNTERS = 0x200
@@ -26,10 +25,11 @@ FLAG_INFLATE_BLOCK_PAR = 0x2000
 
 STATUS_NAMES = {OK: "Ok", UNEXPECTED_EOF: "UnexpectedEof", INVALID_DATA: "InvalidData",
                 INVALID_INPUT: "InvalidInput", UNSUPPORTED: "Unsupported",
-                OUTPUT_TOO_SMALL: "OutputTooSmall", ABSENT: "NotFound", IO: "Other", RUNTIME: "Runtime"}
+                OUTPUT_TOO_SMALL: "OutputTooSmall", ABSENT: "NotFound", IO: "Other", NOT_FOUND: "NotFound",
+                RUNTIME: "Runtime"}
 
 EXPORTED_SYMBOLS = (
-    "zcg_abi_version", "zcg_create", "zcg_destroy", "zcg_last_error",
+    "zcg_abi_version", "zcg_build_config", "zcg_create", "zcg_destroy", "zcg_last_error",
     "zcg_effective_gzip_level", "zcg_effective_lz4_block_size", "zcg_codec_on_gpu",
     "zcg_decode_batch", "zcg_encode_batch", "zcg_encode_bound", "zcg_workspace_bytes",
     "zcg_read_chunk", "zcg_write_chunk", "zcg_read_chunks_host",
@@ -37,7 +37,7 @@ EXPORTED_SYMBOLS = (
     "zcg_store_read_chunks", "zcg_store_write_chunks",
     "zcg_multi_create", "zcg_multi_destroy", "zcg_multi_last_error", "zcg_multi_device_count",
     "zcg_multi_read_chunks_host", "zcg_multi_store_read_chunks", "zcg_multi_store_write_chunks",
-    "zcg_array_meta_from_json", "zcg_chunk_key",
+    "zcg_array_meta_from_json", "zcg_chunk_key", "zcg_store_path",
     "zcg_store_read_chunks_device", "zcg_store_write_chunks_device",
 )
 
@@ -111,6 +111,7 @@ def load_library(path: str = LIB_PATH):
         L = ctypes.CDLL(path)
         vp, u32, u64, i32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int32
         L.zcg_abi_version.restype = ctypes.c_int
+        L.zcg_build_config.restype = ctypes.c_char_p
         L.zcg_create.argtypes = [ctypes.c_int]
         L.zcg_create.restype = vp
         L.zcg_destroy.argtypes = [vp]
@@ -166,6 +167,8 @@ def load_library(path: str = LIB_PATH):
         L.zcg_array_meta_from_json.restype = ctypes.c_int
         L.zcg_chunk_key.argtypes = [ctypes.c_char_p, ctypes.c_char_p, vp, u32, vp, u64]
         L.zcg_chunk_key.restype = u64
+        L.zcg_store_path.argtypes = [ctypes.c_char_p, ctypes.c_char_p, vp, u64, ctypes.POINTER(u64)]
+        L.zcg_store_path.restype = ctypes.c_int
         L.zcg_store_read_chunks_device.argtypes = [vp, ctypes.POINTER(Array), u32, vp, vp, vp, u32]
         L.zcg_store_read_chunks_device.restype = ctypes.c_int
         L.zcg_store_write_chunks_device.argtypes = [vp, ctypes.POINTER(Array), u32, vp, vp, vp, u32]
@@ -210,6 +213,18 @@ def context(device: int = 0) -> Context:
         with _lock:
             _contexts[device] = ctx
     return ctx
+
+
+def store_path(root: str, key: str) -> "tuple[int, str]":
+    """zcg_store_path (host code, no GPU): (status, path)."""
+    L = load_library()
+    n = ctypes.c_uint64(0)
+    st = L.zcg_store_path(root.encode(), key.encode(), None, 0, ctypes.byref(n))
+    if st != OK:
+        return st, ""
+    out = ctypes.create_string_buffer(n.value + 1)
+    st = L.zcg_store_path(root.encode(), key.encode(), ctypes.addressof(out), n.value + 1, ctypes.byref(n))
+    return st, out.value.decode()
 
 
 def array_meta_from_json(text) -> "tuple[int, ArrayMeta, str]":

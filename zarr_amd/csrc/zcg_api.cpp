@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -126,9 +127,50 @@ int stream_ws(zcg_ctx* ctx, void* stream, size_t need, zcg_ctx::Ws** out) {
 
 }  // namespace
 
+namespace zcg {
+namespace {
+std::mutex g_dev_mu;
+std::map<int, uint32_t> g_dev_cus;
+std::map<std::pair<const void*, int>, hipError_t> g_lds_attr;
+}  // namespace
+
+uint32_t device_cu_count() {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::lock_guard<std::mutex> lk(g_dev_mu);
+    auto it = g_dev_cus.find(dev);
+    if (it != g_dev_cus.end()) return it->second;
+    int v = 0;
+    const uint32_t cus =
+        (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0) ? (uint32_t)v
+                                                                                                      : 256u;
+    g_dev_cus[dev] = cus;
+    return cus;
+}
+
+hipError_t lds_attr_once(const void* kernel, int bytes) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::lock_guard<std::mutex> lk(g_dev_mu);
+    const auto key = std::make_pair(kernel, dev);
+    auto it = g_lds_attr.find(key);
+    if (it != g_lds_attr.end() && it->second == hipSuccess) return hipSuccess;
+    const hipError_t e = hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    g_lds_attr[key] = e;
+    return e;
+}
+}  // namespace zcg
+
 extern "C" {
 
 int zcg_abi_version(void) { return ZCG_ABI_VERSION; }
+
+
+const char* zcg_build_config(void) {
+    static const std::string cfg = std::string(zcg::cfg_inflate_wave()) + ";" + zcg::cfg_inflate_par() + ";" +
+                                   zcg::cfg_deflate() + ";" + zcg::cfg_raw() + ";" + zcg::cfg_region();
+    return cfg.c_str();
+}
 
 zcg_ctx* zcg_create(int device) {
     int cnt = 0;

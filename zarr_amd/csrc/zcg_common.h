@@ -238,6 +238,21 @@ struct RegionArgs {
 // Internal launchers (zcg_*.hip) used by zcg_api.cpp.
 namespace zcg {
 struct Workspace;  // defined in zcg_api.cpp
+// Tuning constants of a kernel source, as "name:K=V,K=V" (stringified macros):
+// zcg_build_config() reports them, and tests/test_abi.py checks that the
+// shipped library was built with the defaults.
+#define ZCG_STR2(x) #x
+#define ZCG_STR(x) ZCG_STR2(x)
+const char* cfg_inflate_wave();
+const char* cfg_inflate_par();
+const char* cfg_deflate();
+const char* cfg_raw();
+const char* cfg_region();
+// Per-device facts and settings, made once per device under a lock (the
+// zcg_multi_* calls launch from one host thread per device): the current
+// device's CU count, and a kernel's dynamic-LDS limit raised to `bytes`.
+uint32_t device_cu_count();
+hipError_t lds_attr_once(const void* kernel, int bytes);
 hipError_t launch_raw(const zcg_array* a, const zcg_chunk* d_chunks, uint32_t n, int32_t* d_status,
                       uint64_t* d_out_len, int encode, hipStream_t s);
 hipError_t launch_lz4_decode(const zcg_array* a, const zcg_chunk* d_chunks, uint32_t n,

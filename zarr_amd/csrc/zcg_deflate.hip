@@ -760,6 +760,11 @@ uint64_t deflate_ws_bytes(const zcg_array* a, uint32_t n) {
     return df_layout(D, n).total;
 }
 
+#ifndef ZCG_DF_CHAIN6
+#define ZCG_DF_CHAIN6 32
+#endif
+const char* cfg_deflate() { return "deflate:CHAIN6=" ZCG_STR(ZCG_DF_CHAIN6); }
+
 hipError_t launch_deflate(const zcg_array* a, const zcg_chunk* d_chunks, uint32_t n,
                           uint64_t* d_out_len, int32_t* d_status, void* ws, uint64_t ws_bytes,
                           hipStream_t s) {
@@ -773,21 +778,12 @@ hipError_t launch_deflate(const zcg_array* a, const zcg_chunk* d_chunks, uint32_
     const DfLayout y = df_layout(D, n);
     if (nseg && (ws_bytes < y.total || y.tot >= (1ull << 31))) return hipErrorInvalidValue;
     // zlib's configuration_table: max_chain (capped for the GPU) and nice_length
-#ifndef ZCG_DF_CHAIN6
-#define ZCG_DF_CHAIN6 32
-#endif
     static const u32 chain[10] = {0, 4, 8, 32, 16, 32, ZCG_DF_CHAIN6, 64, 64, 64};
     static const u32 nice[10] = {0, 8, 16, 32, 16, 32, 128, 128, 258, 258};
     u8* w = (u8*)ws;
     if (nseg) {
-        static bool attr = false;
-        if (!attr) {
-            hipError_t e = hipFuncSetAttribute((const void*)deflate_segment,
-                                               hipFuncAttributeMaxDynamicSharedMemorySize,
-                                               (int)sizeof(DefLds));
-            if (e != hipSuccess) return e;
-            attr = true;
-        }
+        if (hipError_t e = lds_attr_once((const void*)deflate_segment, (int)sizeof(DefLds)); e != hipSuccess)
+            return e;
         for (u32 s0 = 0; s0 < n; s0 += y.sm) {
             const u32 scnt = (n - s0) < y.sm ? (n - s0) : y.sm;
             if (level > 0) {

@@ -1075,20 +1075,18 @@ uint64_t inflate_par_ws_bytes(const zcg_array* a, uint32_t n) {
     return PI_OWNER_BYTES + (u64)PI_NSLOT * PI_SLOT_WORDS * 4;
 }
 
+const char* cfg_inflate_par() {
+    return "inflate_par:PF=" ZCG_STR(ZCG_INF_PF) ",FU=" ZCG_STR(ZCG_INF_FU) ",WPE=" ZCG_STR(ZCG_INF_WPE);
+}
+
 hipError_t launch_inflate_par(const zcg_array* a, const zcg_chunk* d_chunks, uint32_t n,
                               int32_t* d_status, void* ws, uint64_t ws_bytes, hipStream_t s) {
     if (n == 0) return hipSuccess;
     if (!ws || ws_bytes < inflate_par_ws_bytes(a, n)) return hipErrorInvalidValue;
     const DType t = make_dtype(a->dtype);
     const u64 D = a->chunk_num_elements * (u64)t.es;
-    static bool attr_set = false;
     const size_t lds = sizeof(ParLds);
-    if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void*)inflate_par_kernel,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        if (e != hipSuccess) return e;
-        attr_set = true;
-    }
+    if (hipError_t e = lds_attr_once((const void*)inflate_par_kernel, (int)lds); e != hipSuccess) return e;
     u32* owner = (u32*)ws;  // the workspace is shared by the stream's codecs: clear the owners
     hipError_t e = hipMemsetAsync(owner, 0, PI_OWNER_BYTES, s);
     if (e != hipSuccess) return e;

@@ -59,9 +59,6 @@ namespace zcg {
 constexpr u32 IW_S = ZIW_S;            // stage ring entries: 64 lane blocks of IW_BLK
 constexpr u32 IW_BLK = IW_S / 64;
 constexpr u32 IW_TCAP = ZIW_TCAP;
-#ifndef ZIW_G2
-#define ZIW_G2 1
-#endif
 constexpr u32 IW_GK = 3;       // token groups in flight in the L phase (named slots)  // far-byte loads in flight per lane (gather)
 constexpr u32 IW_SEGMIN = 128;   // bits per lane segment
 constexpr u32 IW_SEGMAX = 4096;
@@ -408,9 +405,6 @@ __device__ __forceinline__ void blk_store(u16* p, const u32* w) {
 // bits, repeat count), and the true chain is walked through the window with
 // v_readlane on wave-uniform positions, so a symbol costs a few scalar
 // instructions instead of two dependent LDS round trips.
-#ifndef ZIW_PHDR
-#define ZIW_PHDR 1
-#endif
 template <int LB, u32 LCAP, int DB, u32 DCAP>
 __device__ __attribute__((always_inline)) int read_dynamic_wave(BitIn& b, u8* lens, HuffLds* lh, u32* ltab,
                                                                 HuffLds* dh, u32* dtab) {
@@ -586,13 +580,8 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
         u32 type = 0, slen = 0;
         b.cbase = ~0ull;  // the reader's LDS cache shares storage with the stage
         wsync();
-#if ZIW_PHDR
         r = read_block_header_wave<W_LB, W_LCAP, W_DB, W_DCAP>(b, &last, &type, &slen, L.u.h.lens, &L.u.h.lh, L.ltab,
                                                                &L.u.h.dh, L.dtab);
-#else
-        r = read_block_header<W_LB, W_LCAP, W_DB, W_DCAP>(b, &last, &type, &slen, L.u.h.lens, &L.u.h.lh, L.ltab,
-                                                          &L.u.h.dh, L.dtab);
-#endif
         const u32 hdr_end = (u32)b.consumed;
         IW_T(IWT_HDR);
         if (r != R_OK) break;
@@ -794,17 +783,6 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
             auto mL = [&](u32 m) -> u32 { return (u32)__builtin_amdgcn_readlane((int)chL, (int)m); };
             auto mE = [&](u32 m) -> u32 { return (u32)__builtin_amdgcn_readlane((int)chE, (int)m); };
             auto mS1 = [&](u32 m) -> u32 { return m + 1 < ncm ? (u32)__builtin_amdgcn_readlane((int)chS, (int)(m + 1)) : 0u; };
-            auto fetch = [&](u32 cm0, u32 cj0) -> u32 {
-                u32 jj = cj0 + lane, tl = 0xFFFFFFFFu, tj = 0;
-                for (u32 m = cm0; m < ncm; m++) {  // wave-uniform walk over the members a group spans
-                    const u32 e = mE(m), ln = mL(m);
-                    if (tl == 0xFFFFFFFFu && jj < e) { tl = ln; tj = jj; }
-                    if (__ballot(tl == 0xFFFFFFFFu) == 0) break;
-                    if (tl == 0xFFFFFFFFu) jj = jj - e + mS1(m);
-                }
-                const u32 v = gl[tl != 0xFFFFFFFFu ? (u64)tl * IW_TSTR + tj : 0ull];  // (unconditional load)
-                return tl != 0xFFFFFFFFu ? v : (W_MARK | M_END);
-            };
             auto advance = [&](u32& cm0, u32& cj0, u32 k) {
                 cj0 += k;
                 while (cm0 < ncm) {
@@ -821,7 +799,6 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
             // back edge (a copy would wait for it).  Within a stage every
             // group but the last is taken whole, so the prefetch positions
             // are exact; a new stage refetches from its cursor.
-#if ZIW_G2
             // two chain tokens per lane per group (tokens 2l, 2l + 1): the
             // group's fixed costs (scan, ballots, cursor walk) are paid once
             // per 128 tokens
@@ -853,17 +830,6 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
                 advance(cm1, cj1, 128);
                 fetch2(cm1, cj1, tq2a, tq2b, ok2);
             };
-#else
-            u32 tq0, tq1, tq2;
-            auto refetch = [&]() {
-                u32 cm1 = cm, cj1 = cj;
-                tq0 = fetch(cm1, cj1);
-                advance(cm1, cj1, 64);
-                tq1 = fetch(cm1, cj1);
-                advance(cm1, cj1, 64);
-                tq2 = fetch(cm1, cj1);
-            };
-#endif
             refetch();
             bool round_done = false;
             while (!round_done && r == R_OK) {
@@ -879,52 +845,6 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
                 bool far = false;
                 u32 why = 0;  // 1 final cut, 2 marker / round end, 3 capacity
                 u32 mcode = 0;
-                // place one group of 64 tokens; true when the stage ends
-                auto group = [&](u32& tq) -> bool {
-                    IW_ADD(IWD_GROUPS, 1);
-                    const u32 tk = tq;
-                    {  // this slot's next group: IW_GK groups on
-                        u32 cm1 = cm, cj1 = cj;
-                        advance(cm1, cj1, 64 * IW_GK);
-                        tq = fetch(cm1, cj1);
-                    }
-                    const bool ismk = w_marker(tk);
-                    const u64 mm = __ballot(ismk);
-                    const u32 fm = mm ? (u32)__builtin_ctzll(mm) : 64u;
-                    const u32 len = lane < fm ? w_len(tk) : 0u;
-                    const u32 incl = iw_incl_scan(len);
-                    const u32 o = emitted + incl - len;
-                    const bool take = lane < fm && (fin ? o < cap : o + len <= cap);
-                    const u64 tm = __ballot(take);
-                    const u32 ntk = (u32)__popcll(tm);
-                    if (take) {
-                        u16 v;
-                        if (tk & W_MATCH) {
-                            const u32 d = (tk & 0x7FFF) + 1;
-                            if ((u64)d > S + o) far = true;  // before the stream start
-                            v = (u16)(d - 1);
-                        } else {
-                            v = (u16)(IE_VAL | (tk & 0xFF));
-                        }
-                        const u32 ri = (u32)((S + o) & (IW_S - 1));
-                        L.u.st.ptr[ri] = v;
-                        atomicOr(&L.u.st.head[ri >> 5], 1u << (ri & 31));
-                    }
-                    if (ntk) emitted += (u32)__builtin_amdgcn_readlane((int)incl, (int)(ntk - 1));
-                    advance(cm, cj, ntk);
-                    if (fin && emitted >= cap) { why = 1; return true; }
-                    if (ntk < 64) {
-                        if (ntk == fm) {
-                            why = 2;
-                            mcode = (u32)__builtin_amdgcn_readlane((int)tk, (int)fm) & 3u;
-                        } else {
-                            why = 3;
-                        }
-                        return true;
-                    }
-                    return false;
-                };
-#if ZIW_G2
                 auto place = [&](u32 tk, u32 o) {
                     u16 v;
                     if (tk & W_MATCH) {
@@ -982,13 +902,6 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
                     if (group2(tq1a, tq1b, ok1)) break;
                     if (group2(tq2a, tq2b, ok2)) break;
                 }
-#else
-                for (;;) {
-                    if (group(tq0)) break;
-                    if (group(tq1)) break;
-                    if (group(tq2)) break;
-                }
-#endif
                 refetch();  // the next stage starts at the cursor
                 IW_ADD(IWD_STAGES, 1);
                 if (__ballot(far) != 0) { r = R_INVALID; break; }
@@ -1217,19 +1130,18 @@ extern "C" int zcg__debug_inflate_wave_counters(unsigned long long* out, int res
 // Slots: one per resident wave (the LDS footprint bounds residency), never
 // more than the batch.
 static u32 iw_nslot(uint32_t n) {
-    static u32 cus = 0;
-    if (!cus) {
-        int dev = 0, v = 0;
-        (void)hipGetDevice(&dev);
-        cus = (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
-                  ? (u32)v : 256u;
-    }
+    const u32 cus = device_cu_count();
     u32 per_cu = (u32)(160 * 1024 / sizeof(IwLds));
     if (per_cu < 1) per_cu = 1;
     u64 ns = (u64)cus * per_cu;
     if (ns > n) ns = n;
     if (ns > IW_NSLOT_MAX) ns = IW_NSLOT_MAX;
     return (u32)ns;
+}
+
+const char* cfg_inflate_wave() {
+    return "inflate_wave:S=" ZCG_STR(ZIW_S) ",TCAP=" ZCG_STR(ZIW_TCAP) ",WPE=" ZCG_STR(ZIW_WPE)
+           ",EST_PCT=" ZCG_STR(ZIW_EST_PCT) ",MARKW=" ZCG_STR(ZIW_MARKW);
 }
 
 uint64_t inflate_wave_ws_bytes(const zcg_array* a, uint32_t n) {
@@ -1244,14 +1156,8 @@ hipError_t launch_inflate_wave(const zcg_array* a, const zcg_chunk* d_chunks, ui
     if (!ws || ws_bytes < inflate_wave_ws_bytes(a, n)) return hipErrorInvalidValue;
     const DType t = make_dtype(a->dtype);
     const u64 D = a->chunk_num_elements * (u64)t.es;
-    static bool attr_set = false;
     const size_t lds = sizeof(IwLds);
-    if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void*)inflate_wave_kernel,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        if (e != hipSuccess) return e;
-        attr_set = true;
-    }
+    if (hipError_t e = lds_attr_once((const void*)inflate_wave_kernel, (int)lds); e != hipSuccess) return e;
     const u32 nslot = iw_nslot(n);
     u32* owner = (u32*)ws;
     hipError_t e = hipMemsetAsync(owner, 0, (size_t)nslot * 4, s);

@@ -744,36 +744,19 @@ __global__ __launch_bounds__(256) void lz4_blocks_kernel(const zcg_chunk* __rest
 // the 64 lanes of a wave write 64 different blocks.  Match sources nearer
 // than the ring come from LDS; older ones from the block's own HBM output,
 // which this lane stored earlier (same-thread order).  Input comes through a
-// 16-byte register window (LzWin).
-#ifndef ZCG_LZ4_LRB
-#define ZCG_LZ4_LRB 128
-#endif
-#ifndef ZCG_LZ4_BUF
-#define ZCG_LZ4_BUF 1
-#endif
-#ifndef ZCG_LZ4_LANE_MIN_BLOCKS
-#define ZCG_LZ4_LANE_MIN_BLOCKS 131072  // 8 192 chunks of 16 blocks (ULDS lane kernel 146 vs wave 140 GiB/s there; 77 vs 137 at 4 096)
-#endif
-#ifndef ZCG_LZ4_NT_FAR
-#define ZCG_LZ4_NT_FAR 0
-#endif
-#ifndef ZCG_LZ4_NT_ST
-#define ZCG_LZ4_NT_ST 0
-#endif
-#ifndef ZCG_LZ4_LDS_PAD
-#define ZCG_LZ4_LDS_PAD 0
-#endif
-constexpr u32 LZ_LRB = ZCG_LZ4_LRB;  // ring bytes per lane (>= 2 * LZ_LPC)
+// 64-byte register buffer (LzBuf).
+// Measured choices (A/B on one box): a 128-byte ring per lane,
+// 64 lanes per workgroup, and the lane kernel from 131 072 blocks (8 192
+// chunks of 16 blocks: lane 146 vs wave 140 GiB/s there, 77 vs 137 at 4 096).
+constexpr u32 LZ_LRB = 128;         // ring bytes per lane (>= 2 * LZ_LPC)
 constexpr u32 LZ_LPC = LZ_LRB / 2;  // flush granularity = longest piece written between flushes
 constexpr u32 LZ_LRM = LZ_LRB - 1;
-#ifndef ZCG_LZ4_LWG
-#define ZCG_LZ4_LWG 64
-#endif
-constexpr u32 LZ_LWG = ZCG_LZ4_LWG;  // lanes (blocks) per workgroup
+constexpr u32 LZ_LWG = 64;          // lanes (blocks) per workgroup
+constexpr u64 LZ_LANE_MIN_BLOCKS = 131072;
 
-// ZCG_LZ4_ULDS: the ring is written and read with byte-unaligned
-// ds_write_b128 / ds_read_b128 (gfx950 LDS runs in the unaligned alignment
-// mode; tools/probe/lds_unaligned checks it).  A lane's LDS block is
+// The ring is written and read with byte-unaligned ds_write_b128 /
+// ds_read_b128 (gfx950 LDS runs in the unaligned alignment mode;
+// tools/probe/lds_unaligned checks it).  A lane's LDS block is
 // [LZ_LRB ring | 32-byte mirror]; the mirror's first 16 bytes repeat the
 // ring's first 16, so any 16 ring bytes are contiguous.  An append at ring
 // offset w writes its vector at w (past the ring end it lands in the mirror,
@@ -784,18 +767,8 @@ constexpr u32 LZ_LWG = ZCG_LZ4_LWG;  // lanes (blocks) per workgroup
 // serves sources nearer than LZ_NEAR = 96 (older ones come from HBM, where
 // everything 64 bytes back is already flushed); the block stays 160 bytes,
 // 64 lanes = 10 KiB, 16 workgroups per CU.
-#ifndef ZCG_LZ4_ULDS
-#define ZCG_LZ4_ULDS 1
-#endif
-#ifndef ZCG_LZ4_PERM
-#define ZCG_LZ4_PERM 1
-#endif
-constexpr u32 LZ_LSTRIDE = ZCG_LZ4_ULDS ? ZCG_LZ4_LRB + 32 : ZCG_LZ4_LRB;  // LDS bytes per lane
-// a ring source is intact while it is nearer than this: an append writes
-// whole dwords past its k valid bytes (clobbering the slots of bytes a full
-// ring minus 4 back), or with ULDS 16 bytes plus the wrapped vector's zero
-// tail (bytes >= 98 back)
-constexpr u32 LZ_NEAR = ZCG_LZ4_ULDS ? 96u : ZCG_LZ4_LRB - 4;
+constexpr u32 LZ_LSTRIDE = LZ_LRB + 32;  // LDS bytes per lane
+constexpr u32 LZ_NEAR = 96u;
 typedef __attribute__((ext_vector_type(4))) u32 lz_v4;
 __device__ __forceinline__ void lds_st16_ua(lu8* p, const u32x4& v) {
     const u32 a = (u32)(uintptr_t)p;
@@ -814,24 +787,14 @@ struct LaneRing {
     gu8* dst;    // the block's output
     u32 lim;     // bytes of the block below N*size (never store at >= lim)
     u32 fl;      // output below fl is in HBM (a multiple of LZ_LPC)
-    u32 tw;      // the ring dword holding output byte op (its bytes below op & 3 are valid)
-    __device__ __forceinline__ void wr32(u32 a, u32 v) { *(lu32*)(R + (a & LZ_LRM)) = v; }
-    __device__ __forceinline__ u32 rd32(u32 a) const { return *(const lu32*)(R + (a & LZ_LRM)); }
     __device__ __forceinline__ void store_piece(u32 a) {
-#ifdef ZCG_LZ4_DIAG_NOSTORE  // timing diagnostic only: no output stores
-        if (a < 0x7FFFFFFFu) return;
-#endif
         if (a >= lim) return;
         const lu8* p = R + (a & LZ_LRM);
         if (a + LZ_LPC <= lim) {
 #pragma unroll
             for (u32 i = 0; i < LZ_LPC / 16; i++) {
                 const u32x4 v = *(const __attribute__((address_space(3))) u32x4*)(p + 16 * i);
-#if ZCG_LZ4_NT_ST
-                __builtin_nontemporal_store(v, (u32x4 __attribute__((address_space(1)))*)(dst + a + 16 * i));
-#else
                 *(gu32x4_ua*)(dst + a + 16 * i) = v;
-#endif
             }
         } else {
             for (u32 i = 0; a + i < lim; i++) dst[a + i] = p[i];
@@ -845,7 +808,6 @@ struct LaneRing {
         flush(op);
         for (u32 i = fl; i < op && i < lim; i++) dst[i] = R[i & LZ_LRM];
     }
-#if ZCG_LZ4_ULDS
     // append the first k (1..16) bytes of v at op: one unaligned 16-byte
     // write (bytes past op + k are stale and overwritten later), a second
     // one when it crosses the ring end or covers its first 16 bytes
@@ -857,56 +819,12 @@ struct LaneRing {
         op += k;
     }
     __device__ __forceinline__ u32x4 rd16(u32 p) const { return lds_ld16_ua(R + (p & LZ_LRM)); }
-#else
-    // append the first k (1..16) bytes of v at op: up to five dword writes
-    // (v_alignbyte merges), the dword holding the new op is kept in tw
-    __device__ __forceinline__ void append16(u32& op, const u32x4& v, u32 k) {
-        const u32 sh = op & 3, a = op & ~3u, t = 4 - sh;
-        const u32 m = sh ? (0xFFFFFFFFu >> (8 * t)) : 0u;
-        u32 d[5];
-        d[0] = (tw & m) | (v.x << (8 * sh));
-        d[1] = sh ? __builtin_amdgcn_alignbyte(v.y, v.x, t) : v.y;
-        d[2] = sh ? __builtin_amdgcn_alignbyte(v.z, v.y, t) : v.z;
-        d[3] = sh ? __builtin_amdgcn_alignbyte(v.w, v.z, t) : v.w;
-        d[4] = sh ? (v.w >> (8 * t)) : 0u;
-        const u32 e = sh + k;
-#pragma unroll
-        for (u32 j = 0; j < 5; j++)
-            if (4 * j < e) wr32(a + 4 * j, d[j]);
-        const u32 q = e >> 2;
-        tw = q == 0 ? d[0] : q == 1 ? d[1] : q == 2 ? d[2] : q == 3 ? d[3] : d[4];
-        op += k;
-    }
-    // the 16 ring bytes at p (p < op; bytes at >= op are stale)
-    __device__ __forceinline__ u32x4 rd16(u32 p) const {
-        const u32 b = p & ~3u, sh = p & 3;
-        const u32 w0 = rd32(b), w1 = rd32(b + 4), w2 = rd32(b + 8), w3 = rd32(b + 12), w4 = rd32(b + 16);
-        if (!sh) return u32x4{w0, w1, w2, w3};
-        return u32x4{__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
-                     __builtin_amdgcn_alignbyte(w3, w2, sh), __builtin_amdgcn_alignbyte(w4, w3, sh)};
-    }
-#endif
 };
-
-// v with its first `off` (1..15) bytes repeated: byte j = byte (j mod off)
-__device__ __forceinline__ u32x4 lz_pattern(u32x4 v, u32 off) {
-    u64 lo = ((u64)v.y << 32) | v.x, hi = ((u64)v.w << 32) | v.z;
-    if (off < 8) { lo &= (1ull << (8 * off)) - 1; hi = 0; }
-    else hi &= (1ull << (8 * (off - 8))) - 1;  // off = 8: keeps nothing of hi
-    for (u32 L = off; L < 16; L *= 2) {  // double the valid prefix
-        u64 slo, shi;
-        if (L >= 8) { shi = lo << (8 * (L - 8)); slo = 0; }
-        else { shi = (hi << (8 * L)) | (lo >> (64 - 8 * L)); slo = lo << (8 * L); }
-        lo |= slo;
-        hi |= shi;
-    }
-    return u32x4{(u32)lo, (u32)(lo >> 32), (u32)hi, (u32)(hi >> 32)};
-}
 
 // v_perm_b32 selectors of the period-`off` pattern (off < 16): output dword d
 // = perm(v.y, v.x, lo[d]) | perm(v.w, v.z, hi[d]); byte j takes source byte
 // j mod off (0x0C selects a zero byte).  One table row per offset replaces
-// the doubling loop of lz_pattern (up to four 128-bit shift rounds).
+// a doubling loop (up to four 128-bit shift rounds).
 __constant__ __attribute__((aligned(16))) u32 c_lz_pat[16][8] = {
     {0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x0C0C0C0Cu, 0x0C0C0C0Cu, 0x0C0C0C0Cu, 0x0C0C0C0Cu},
     {0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x0C0C0C0Cu, 0x0C0C0C0Cu, 0x0C0C0C0Cu, 0x0C0C0C0Cu},
@@ -942,26 +860,13 @@ __device__ __forceinline__ u32x4 lz_pattern_perm(const u32x4& v, const LzPat& s)
 // the 16 output bytes at op - off (off >= 1; periodic when off < 16): from the
 // ring when the source is near (its slots are not yet reused: off < LZ_LRB - 4,
 // the 4 covering the stale tail of the last written dword), else from HBM
-__device__ __forceinline__ u32x4 lz_src16(const LaneRing& O, u32 op, u32 off, const LzPat* ps = nullptr) {
+__device__ __forceinline__ u32x4 lz_src16(const LaneRing& O, u32 op, u32 off, const LzPat& ps) {
     const u32 p = op - off;
-#ifdef ZCG_LZ4_DIAG_NOFAR  // timing diagnostic only (wrong bytes): every source from the ring
-    if (true) {
-#else
     if (off < LZ_NEAR) {
-#endif
         const u32x4 v = O.rd16(p);
-        if (ps) return off < 16 ? lz_pattern_perm(v, *ps) : v;
-        return off < 16 ? lz_pattern(v, off) : v;
+        return off < 16 ? lz_pattern_perm(v, ps) : v;
     }
-    if (p + 16 <= O.lim) {
-#if ZCG_LZ4_NT_FAR
-        const gu32* q = (const gu32*)(O.dst + p);  // (dword loads: p is any byte offset)
-        return u32x4{__builtin_nontemporal_load(q), __builtin_nontemporal_load(q + 1),
-                     __builtin_nontemporal_load(q + 2), __builtin_nontemporal_load(q + 3)};
-#else
-        return *(const gu32x4_ua*)(O.dst + p);
-#endif
-    }
+    if (p + 16 <= O.lim) return *(const gu32x4_ua*)(O.dst + p);
     u64 lo = 0, hi = 0;  // the block's last bytes: nothing at >= lim is stored (or needed)
     for (u32 k = 0; k < 16; k++) {
         const u64 b = p + k < O.lim ? (u64)O.dst[p + k] : 0ull;
@@ -1028,15 +933,10 @@ struct LzBuf {
 __device__ __forceinline__ int lz4_lane_block(const u8* __restrict__ src, u32 iend, u64 avail, LaneRing& O, u32 cap,
                               u32* out_n) {
     u32 ip = 0, op = 0;
-#if ZCG_LZ4_BUF
     LzBuf in;
     in.src = src; in.avail = avail;
     in.load_buf(0);
     in.at(0);
-#else
-    LzWin in{src, avail, u32x4{0, 0, 0, 0}, 0};
-    in.at(0);
-#endif
     for (;;) {
         if (ip >= iend) return ZCG_ERR_INVALID_DATA;
         const u32 token = in.byte(ip++);
@@ -1077,16 +977,11 @@ __device__ __forceinline__ int lz4_lane_block(const u8* __restrict__ src, u32 ie
         if (op < off) return ZCG_ERR_INVALID_DATA;
         if ((u64)op + ml + 5 > cap) return ZCG_ERR_INVALID_DATA;
         if (ip - in.wb > 8) in.at(ip);  // the next sequence's window, in flight during the copy
-#if ZCG_LZ4_PERM
         const LzPat ps = lz_pat_sel(off);  // (loaded for every sequence: counted by the waits)
-        const LzPat* psp = &ps;
-#else
-        const LzPat* psp = nullptr;
-#endif
         for (u32 r = ml; r > 0;) {
             const u32 k = r < 16 ? r : 16;
             // lz4 1.9.3 decodes offset 0 to zeros
-            const u32x4 v = off ? lz_src16(O, op, off, psp) : u32x4{0u, 0u, 0u, 0u};
+            const u32x4 v = off ? lz_src16(O, op, off, ps) : u32x4{0u, 0u, 0u, 0u};
             O.append16(op, v, k);
             O.flush(op);
             r -= k;
@@ -1096,238 +991,11 @@ __device__ __forceinline__ int lz4_lane_block(const u8* __restrict__ src, u32 ie
     return ZCG_OK;
 }
 
-// ---- the same decode with the sequence parse running QK sequences ahead ------
-// A lane's decode is a chain of dependent steps, and at 2-4 waves per SIMD
-// the exposed latency of each step's memory reads (the match source from HBM
-// for 70 % of C4 sequences, a new input line every ~14) is what bounds it.
-// The parse of a sequence (token, lengths, offset, and every check of
-// LZ4_decompress_safe: they need only ip, op and the lengths) does not depend
-// on the output, so it runs QK sequences ahead of the execution:
-//  * parsing sequence s+QK issues the loads that sequence will need — its
-//    first 16 literal bytes, and, when its match source is already in HBM
-//    (offset past the ring and the source below the flushed mark), the first
-//    16 source bytes — into the queue slot that sequence s just left;
-//  * the loads are issued on every step whatever the sequence needs (a dummy
-//    address otherwise), so the compiler can count the vector-memory
-//    operations between a slot's loads and their use and wait for those
-//    alone (vmcnt counts loads and stores together, in issue order);
-//  * the input is two 64-byte register buffers, the next one loaded as soon
-//    as the parse enters the current one.
-// The queue is QK named slots in a QK-times unrolled loop, so a slot's loads
-// stay in flight in place across the loop's back edge (no register copies).
-#ifndef ZCG_LZ4_Q
-#define ZCG_LZ4_Q 0
-#endif
-#ifndef ZCG_LZ4_QK
-#define ZCG_LZ4_QK 4
-#endif
-
-// win_load for a global pointer (global_load, not flat: a flat load makes
-// every later wait a full vmcnt(0) + lgkmcnt(0))
-__device__ __forceinline__ u32x4 gwin_load(const gu8* __restrict__ src, u32 q, u32 avail) {
-    if (q + 16 <= avail) return *(const gu32x4_ua*)(src + q);
-    u64 lo = 0, hi = 0;
-    for (u32 k = 0; k < 16; k++) {
-        const u64 b = (q + k < avail) ? (u64)src[q + k] : 0ull;
-        if (k < 8) lo |= b << (8 * k);
-        else hi |= b << (8 * (k - 8));
-    }
-    return u32x4{(u32)lo, (u32)(lo >> 32), (u32)hi, (u32)(hi >> 32)};
-}
-
-struct LzIn2 {
-    const gu8* src;
-    u32 avail;            // readable bytes from src (>= 64 on this path)
-    u32x4 b0, b1, b2, b3;  // [bb, bb + 64)
-    u32x4 n0, n1, n2, n3;  // [bb + 64, bb + 128), in flight until first used
-    u32 bb;
-    u32x4 w;  // [wb, wb + 16)
-    u32 wb;
-    // 16 bytes at q; near the stream end the last 16 readable bytes are
-    // loaded and shifted into place (zero fill past avail)
-    __device__ __forceinline__ u32x4 vec(u32 q) const {
-        const u32 a = q + 16 <= avail ? q : avail - 16;
-        const u32x4 v = *(const gu32x4_ua*)(src + a);
-        return a == q ? v : (q - a >= 16 ? u32x4{0u, 0u, 0u, 0u} : win_shift(v, q - a));
-    }
-    __device__ __forceinline__ void load_at(u32 q) {
-        bb = q & ~15u;
-        b0 = vec(bb); b1 = vec(bb + 16); b2 = vec(bb + 32); b3 = vec(bb + 48);
-        n0 = vec(bb + 64); n1 = vec(bb + 80); n2 = vec(bb + 96); n3 = vec(bb + 112);
-    }
-    __device__ __forceinline__ void at(u32 q) {
-        u32 d = q - bb;
-        if (d >= 64) {
-            if (d < 128) {
-                b0 = n0; b1 = n1; b2 = n2; b3 = n3;
-                bb += 64;
-                n0 = vec(bb + 64); n1 = vec(bb + 80); n2 = vec(bb + 96); n3 = vec(bb + 112);
-            } else {
-                load_at(q);
-            }
-            d = q - bb;
-        }
-        const u32 qd = d >> 4;
-        u32x4 c0 = b0, c1 = b1, c2 = b2, c3 = b3, c4 = n0;
-        asm volatile("" : "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3), "+v"(c4));
-        const u32x4 lo = qd == 0 ? c0 : qd == 1 ? c1 : qd == 2 ? c2 : c3;
-        const u32x4 hi = qd == 0 ? c1 : qd == 1 ? c2 : qd == 2 ? c3 : c4;
-        const u32 s4 = (d >> 2) & 3, sb = d & 3;
-        const u32 y0 = sel4(s4, lo.x, lo.y, lo.z, lo.w), y1 = sel4(s4, lo.y, lo.z, lo.w, hi.x);
-        const u32 y2 = sel4(s4, lo.z, lo.w, hi.x, hi.y), y3 = sel4(s4, lo.w, hi.x, hi.y, hi.z);
-        const u32 y4 = sel4(s4, hi.x, hi.y, hi.z, hi.w);
-        w = sb ? u32x4{__builtin_amdgcn_alignbyte(y1, y0, sb), __builtin_amdgcn_alignbyte(y2, y1, sb),
-                       __builtin_amdgcn_alignbyte(y3, y2, sb), __builtin_amdgcn_alignbyte(y4, y3, sb)}
-               : u32x4{y0, y1, y2, y3};
-        wb = q;
-    }
-    __device__ __forceinline__ u32 byte(u32 q) {
-        u32 d = q - wb;
-        if (d >= 16) { at(q); d = 0; }
-        return win_byte(w, d);
-    }
-};
-
-struct LzQSeq {
-    u32 lit, lip;  // literal count and their input position
-    u32 ofs;       // offset | Q_PRE (first source vector prefetched) | Q_LAST | Q_VALID
-    u32 ml;        // match length (incl. the 4)
-    u32x4 lv, fv;  // first 16 literal bytes, first 16 match-source bytes
-};
-constexpr u32 Q_PRE = 1u << 16, Q_LAST = 1u << 17, Q_VALID = 1u << 18;
-
-// parse the sequence at ip (output position opp) into q; returns false on
-// corrupt input (LZ4_decompress_safe's checks, in lz4_lane_block's order)
-__device__ __forceinline__ bool lzq_parse(LzIn2& in, u32& ip, u32& opp, u32 iend, u32 cap, const LaneRing& O,
-                                          LzQSeq& q, bool& pdone, u32& la, u32& fa) {
-    if (ip >= iend) return false;
-    if (ip - in.wb > 8) in.at(ip);
-    const u32 token = in.byte(ip++);
-    u32 lit = token >> 4;
-    if (lit == 15) {
-        if ((i64)ip >= (i64)iend - 15) return false;
-        u32 s;
-        do {
-            s = in.byte(ip++);
-            lit += s;
-        } while (s == 255 && (i64)ip < (i64)iend - 15);
-    }
-    const u64 cpy = (u64)opp + lit;
-    const bool last = cpy + 12 > cap || (i64)ip + lit > (i64)iend - 8;
-    if (last && ((u64)ip + lit != iend || cpy > cap)) return false;
-    q.lit = lit;
-    q.lip = ip;
-    la = ip;
-    ip += lit;
-    opp += lit;
-    if (last) {
-        q.ofs = Q_VALID | Q_LAST;
-        q.ml = 0;
-        pdone = true;
-        return true;
-    }
-    const u32 off = in.byte(ip) | (in.byte(ip + 1) << 8);
-    ip += 2;
-    u32 ml = token & 15;
-    if (ml == 15) {
-        u32 s;
-        do {
-            s = in.byte(ip++);
-            ml += s;
-            if ((i64)ip >= (i64)iend - 4) return false;
-        } while (s == 255);
-    }
-    ml += 4;
-    if (opp < off) return false;
-    if ((u64)opp + ml + 5 > cap) return false;
-    // the source is in HBM already: prefetch its first vector
-    const bool pre = off >= LZ_NEAR && opp - off + 16 <= O.fl && opp - off + 16 <= O.lim;
-    if (pre) fa = opp - off;
-    q.ofs = Q_VALID | off | (pre ? Q_PRE : 0u);
-    q.ml = ml;
-    opp += ml;
-    return true;
-}
-
-__device__ __forceinline__ void lzq_exec(const gu8* src, u32 avail, LaneRing& O, u32& op, const LzQSeq& q) {
-    const u32 lit = q.lit;
-    if (lit) {
-        const u32x4 v = q.lip + 16 <= avail ? q.lv : gwin_load(src, q.lip, avail);
-        const u32 k = lit < 16 ? lit : 16;
-        O.append16(op, v, k);
-        O.flush(op);
-        for (u32 j0 = 16; j0 < lit; j0 += 16) {
-            const u32 k2 = lit - j0 < 16 ? lit - j0 : 16;
-            O.append16(op, gwin_load(src, q.lip + j0, avail), k2);
-            O.flush(op);
-        }
-    }
-    if (q.ofs & Q_LAST) return;
-    const u32 off = q.ofs & 0xFFFFu;
-    u32 r = q.ml;
-    {
-        const u32 k = r < 16 ? r : 16;
-        const u32x4 v = (q.ofs & Q_PRE) ? q.fv : (off ? lz_src16(O, op, off) : u32x4{0u, 0u, 0u, 0u});
-        O.append16(op, v, k);
-        O.flush(op);
-        r -= k;
-    }
-    while (r > 0) {
-        const u32 k = r < 16 ? r : 16;
-        const u32x4 v = off ? lz_src16(O, op, off) : u32x4{0u, 0u, 0u, 0u};
-        O.append16(op, v, k);
-        O.flush(op);
-        r -= k;
-    }
-}
-
-__device__ __forceinline__ int lz4_lane_block_q(const u8* __restrict__ src8, u32 iend, u32 avail, LaneRing& O,
-                                                u32 cap, u32* out_n) {
-    const gu8* src = (const gu8*)src8;
-    LzIn2 in;
-    in.src = src;
-    in.avail = avail;
-    in.load_at(0);
-    in.wb = 0x80000000u;  // no window yet
-    u32 ip = 0, opp = 0, op = 0;
-    bool pdone = false;
-    LzQSeq q0, q1, q2, q3;
-    q0.ofs = q1.ofs = q2.ofs = q3.ofs = 0;
-    // one queue step on slot q: run the sequence it holds, refill it
-#define LZQ_STEP(q)                                                                              \
-    {                                                                                            \
-        if (q.ofs & Q_VALID) {                                                                   \
-            lzq_exec(src, avail, O, op, q);                                                      \
-            if (q.ofs & Q_LAST) { *out_n = op; return ZCG_OK; }                                  \
-        }                                                                                        \
-        u32 la = ip, fa = 0;                                                                     \
-        q.ofs = 0;                                                                               \
-        if (!pdone && !lzq_parse(in, ip, opp, iend, cap, O, q, pdone, la, fa))                   \
-            return ZCG_ERR_INVALID_DATA;                                                         \
-        const u32 la2 = la + 16 <= avail ? la : avail - 16;                                      \
-        q.lv = *(const gu32x4_ua*)(src + la2);                                                   \
-        q.fv = *(const gu32x4_ua*)((q.ofs & Q_PRE) ? (const gu8*)O.dst + fa : src + la2);        \
-    }
-    static_assert(ZCG_LZ4_QK == 3 || ZCG_LZ4_QK == 4, "three or four named queue slots");
-    for (;;) {
-        LZQ_STEP(q0);
-        LZQ_STEP(q1);
-        LZQ_STEP(q2);
-#if ZCG_LZ4_QK == 4
-        LZQ_STEP(q3);
-#endif
-    }
-#undef LZQ_STEP
-}
-
-#ifndef ZCG_LZ4_WPE
-#define ZCG_LZ4_WPE 1
-#endif
-__global__ __launch_bounds__(LZ_LWG, ZCG_LZ4_WPE) void lz4_lanes_kernel(const zcg_chunk* __restrict__ chunks, u32 n, u64 D,
+__global__ __launch_bounds__(LZ_LWG, 1) void lz4_lanes_kernel(const zcg_chunk* __restrict__ chunks, u32 n, u64 D,
                                                            u32 S, u32 vflags,
                                                            const Lz4ChunkInfo* __restrict__ info,
                                                            Lz4Slot* __restrict__ slots) {
-    __shared__ __attribute__((aligned(16))) u8 rings[LZ_LWG * LZ_LSTRIDE + ZCG_LZ4_LDS_PAD];
+    __shared__ __attribute__((aligned(16))) u8 rings[LZ_LWG * LZ_LSTRIDE];
     const u64 g = (u64)blockIdx.x * LZ_LWG + threadIdx.x;
     const u32 c = (u32)(g / S);
     const u32 k = (u32)(g - (u64)c * S);
@@ -1355,12 +1023,9 @@ __global__ __launch_bounds__(LZ_LWG, ZCG_LZ4_WPE) void lz4_lanes_kernel(const zc
             for (; i < m; i++) dst[i] = s[i];
             got = cs;
         } else {
-            LaneRing O{(lu8*)(rings + threadIdx.x * LZ_LSTRIDE), dst, lb, 0, 0};
+            LaneRing O{(lu8*)(rings + threadIdx.x * LZ_LSTRIDE), dst, lb, 0};
             const u64 avail = ch.src_len - so;
-            if (ZCG_LZ4_Q && avail >= 64)
-                st = lz4_lane_block_q(s, cs, avail < 0xFFFFFFF0ull ? (u32)avail : 0xFFFFFFF0u, O, ci.bmax, &got);
-            else
-                st = lz4_lane_block(s, cs, avail, O, ci.bmax, &got);
+            st = lz4_lane_block(s, cs, avail, O, ci.bmax, &got);
             if (st == ZCG_OK) O.finish(got);
         }
     }
@@ -1447,7 +1112,7 @@ hipError_t launch_lz4_decode(const zcg_array* a, const zcg_chunk* d_chunks, uint
         // latency; smaller batches run one wave per block
         const u32 fl = a->compression.flags;
         const bool wave = (fl & ZCG_FLAG_LZ4_WAVE_PER_BLOCK) ||
-                          (!(fl & ZCG_FLAG_LZ4_LANE_PER_BLOCK) && waves < ZCG_LZ4_LANE_MIN_BLOCKS);
+                          (!(fl & ZCG_FLAG_LZ4_LANE_PER_BLOCK) && waves < LZ_LANE_MIN_BLOCKS);
         if (wave)
             hipLaunchKernelGGL(lz4_blocks_kernel, dim3((u32)((waves + 3) / 4)), dim3(256), 0, s, d_chunks, n, D,
                                (u32)S, a->compression.flags, (const Lz4ChunkInfo*)info, slots);

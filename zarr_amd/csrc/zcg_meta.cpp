@@ -491,6 +491,49 @@ extern "C" int zcg_array_meta_from_json(const char* json, uint64_t len, zcg_arra
     return st;
 }
 
+// FilesystemHierarchy::get_path (filesystem.rs:151-190) on Unix paths.  The
+// key is split the way std::path::Path::components does: leading '/'s are the
+// root (dropped: the key is taken relative to the store), empty components
+// ("a//b", a trailing '/') and "." components vanish (a file the OS names
+// the same with or without them), ".." stays literal (the
+// OS resolves it against the joined path, as it does for the reference's
+// PathBuf).  Only the NET nesting is checked: +1 per normal component, -1 per
+// "..", NotFound when the total is negative (so "a/../b" and "../a/b" are
+// accepted, "a/../../b" too, and "../../x" is not).
+extern "C" int zcg_store_path(const char* root, const char* key, char* out, uint64_t cap, uint64_t* path_len) {
+    if (!root || !key) return ZCG_ERR_INVALID_INPUT;
+    std::string rel;
+    long nest = 0;
+    const char* p = key;
+    while (*p == '/') p++;
+    while (*p) {
+        const char* e = p;
+        while (*e && *e != '/') e++;
+        const size_t n = (size_t)(e - p);
+        const bool cur = n == 1 && p[0] == '.';
+        const bool par = n == 2 && p[0] == '.' && p[1] == '.';
+        if (n && !cur) {
+            nest += par ? -1 : 1;
+            if (!rel.empty()) rel += '/';
+            rel.append(p, n);
+        }
+        p = *e ? e + 1 : e;
+    }
+    if (nest < 0) return ZCG_ERR_NOT_FOUND;
+    std::string path = root;
+    if (!rel.empty()) {
+        if (path.empty() || path.back() != '/') path += '/';
+        path += rel;
+    }
+    if (path_len) *path_len = path.size();
+    if (!out || cap < path.size() + 1) {
+        if (out && cap) out[0] = 0;
+        return out ? ZCG_ERR_OUTPUT_TOO_SMALL : ZCG_OK;
+    }
+    memcpy(out, path.c_str(), path.size() + 1);
+    return ZCG_OK;
+}
+
 extern "C" uint64_t zcg_chunk_key(const char* path, const char* separator, const uint64_t* grid_position,
                                   uint32_t ndim, char* out, uint64_t cap) {
     std::string p = path ? path : "";

@@ -95,4 +95,6 @@ hipError_t launch_raw(const zcg_array* a, const zcg_chunk* d_chunks, uint32_t n,
     return hipGetLastError();
 }
 
+const char* cfg_raw() { return "raw:VPT=" ZCG_STR(ZCG_RAW_VPT); }
+
 }  // namespace zcg

@@ -258,4 +258,6 @@ hipError_t launch_region(const RegionArgs& a, const void* const* d_table, void* 
     return hipGetLastError();
 }
 
+const char* cfg_region() { return "region:U=" ZCG_STR(ZCG_RG_U); }
+
 }  // namespace zcg

@@ -71,10 +71,15 @@ class FilesystemHierarchy:
 
     # ---- keys -----------------------------------------------------------------
     def _path(self, key: str) -> str:
-        parts = [p for p in key.split("/") if p not in ("", ".")]
-        if ".." in parts:
-            raise ZarrIOError("NotFound", "key escapes the hierarchy root")
-        return os.path.join(self.base_path, *parts)
+        """FilesystemHierarchy::get_path (filesystem.rs:151-190) through the
+        C ABI (zcg_store_path): the key relative to the root, refused with
+        NotFound when its net nesting is negative."""
+        st, p = _native.store_path(self.base_path, key)
+        if st == _native.NOT_FOUND:
+            raise ZarrIOError("NotFound", "Path name is outside this Zarr filesystem")
+        if st != _native.OK:
+            raise ZarrIOError(_native.STATUS_NAMES.get(st, "Other"), f"zcg_store_path: status {st}")
+        return p
 
     def array_metadata_key(self, path_name: str) -> str:
         suffix = self.entry.get("metadata_key_suffix", ".json").lstrip(".")
