@@ -407,10 +407,14 @@ def encode_leg(codec, n, steps, warmup, pool, rank, world, dev, cpu_seconds=0.0,
     assert (status.cpu().numpy() == 0).all()
     ol = out_len.cpu().numpy()
     out_bytes = int(ol.sum())
-    # decodability: a sample of the streams through the reference's library
-    for i in sorted({0, 1, n // 2, n - 1}):
+    # decodability: a sample of the streams through the reference's library,
+    # and whether the bytes equal the reference library's own stream
+    same = 0
+    sample = sorted({0, 1, n // 2, n - 1})
+    for i in sample:
         s = dst[i * cap:i * cap + int(ol[i])].cpu().numpy().tobytes()
         assert host_decode_check(codec, s, D) == vals[ids[i] % pool].tobytes(), f"{codec} encode: chunk {i}"
+        same += int(s == host_encode(codec, [vals[ids[i] % pool]], 1)[0])
     _, t_max, dev_ms = timed_launches(lambda: bc.encode(meta, desc, n, out_len, status, stream=stream),
                                       steps, world, stream, dev)
     achieved = (n * D + out_bytes) / (dev_ms * 1e-3) / 1e9
@@ -421,6 +425,7 @@ def encode_leg(codec, n, steps, warmup, pool, rank, world, dev, cpu_seconds=0.0,
            "value": round(world * n * D * steps / t_max / GIB, 3), "unit": "GiB/s (input)",
            "ms_per_step": round(t_max / steps * 1e3, 3), "device_ms": round(dev_ms, 3),
            "batch_per_gpu": n, "ratio": round(n * D / out_bytes, 3), "decoded_sample_ok": True,
+           "bytes_equal_reference_sample": f"{same}/{len(sample)}",
            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                         "traffic": pmc_traffic(f"{codec}_encode", n),
@@ -570,6 +575,8 @@ def compact_leg(r):
         out["traffic_x"] = round(tr / ab, 2)
     if "ref_ratio" in r:
         out["ref_ratio"] = r["ref_ratio"]
+    if "bytes_equal_reference_sample" in r:
+        out["same_bytes"] = r["bytes_equal_reference_sample"]
     cb = r.get("cpu_baseline")
     if cb:
         out["cpu"] = [cb["value"], cb["value_t1"], cb["cores"]]

@@ -89,10 +89,13 @@ enum zcg_status {
  * size picks (lanes for large batches). */
 #define ZCG_FLAG_LZ4_WAVE_PER_BLOCK 0x800u
 #define ZCG_FLAG_LZ4_LANE_PER_BLOCK 0x1000u
-/* Gzip decode with the 256-lane round kernel (fine 256-bit segments, one
- * workgroup of 4 waves per chunk) instead of the default one-wave-per-chunk
- * kernel (coarse segments); bit-identical, kept as a differential reference. */
+/* Gzip decode kernel choice (all bit-identical).  By default a batch of at
+ * most 3 chunks per CU (one generation of the 256-lane kernel) runs the
+ * 256-lane round kernel (fine 256-bit segments, one workgroup of 4 waves per
+ * chunk: half the latency of a lone chunk), a larger one the one-wave-per-chunk
+ * kernel (coarse segments, 16 chunks per CU).  These flags force one. */
 #define ZCG_FLAG_INFLATE_BLOCK_PAR 0x2000u
+#define ZCG_FLAG_INFLATE_WAVE 0x4000u
 
 /* CompressionType + its configuration (camelCase JSON keys in the reference). */
 typedef struct zcg_compression {

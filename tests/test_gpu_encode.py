@@ -1,13 +1,16 @@
-"""GPU encoders (write_chunk, chunk.rs:306-323) — parity by round trip.
+"""GPU encoders (write_chunk, chunk.rs:306-323).
 
 The reference pins encoded bytes only for the doc-spec vectors
-(tests.rs:147-159); everything larger is "parity unpinned" (SURVEY §8c,
-zarrita_compat.rs:101-102).  So: byte-exact on the doc-spec vector, and for
-every other input the GPU stream must (a) decode with the oracle (the same
-liblz4 LZ4F the reference's lz4-rs wraps) to exactly the serialised input,
-(b) carry the lz4-rs frame conventions (lz.rs:81-92: FLG 0x64, BD from the
-effective block size, header checksum, independent blocks, content checksum
-= XXH32 of the content), and (c) decode with our own GPU decoder.
+(tests.rs:147-159); everything larger is "parity unpinned" in the reference's
+own tests (zarrita_compat.rs:101-102).  LZ4 frames are
+nevertheless compared byte for byte with the oracle's liblz4 LZ4F frames
+(the library lz4-rs wraps, fed as lz4-rs feeds it): the GPU block compressor
+restates liblz4's, so write_chunk's bytes are the reference's.  For every
+codec the GPU stream must also (a) decode with the oracle to exactly the
+serialised input, (b) carry the crate's container conventions (lz4: lz.rs:81-92
+FLG 0x64, BD from the effective block size, header checksum, independent
+blocks, content checksum = XXH32 of the content), and (c) decode with our own
+GPU decoder.
 """
 import os
 import struct
@@ -61,6 +64,12 @@ def encode_batch(meta, arrays, cap_extra=0):
 
 
 def check_lz4_frame(stream: bytes, content: bytes, block_size: int):
+    # byte-identical to lz4-rs's frame (liblz4 LZ4F, level 0, independent blocks)
+    st, ref = zref.encode(zref.LZ4, block_size, np.frombuffer(content, np.uint8))
+    assert st == zref.OK
+    if stream != ref:
+        k = next((i for i in range(min(len(stream), len(ref))) if stream[i] != ref[i]), min(len(stream), len(ref)))
+        raise AssertionError(f"lz4 frame differs from liblz4's at byte {k} (len {len(stream)} vs {len(ref)})")
     assert stream[:4] == b"\x04\x22\x4d\x18"
     flg, bd = stream[4], stream[5]
     assert flg == 0x64  # version 01 | independent blocks | content checksum

@@ -32,15 +32,20 @@ def meta_for(codec, dt, n, param=None):
     return ArrayMetadata.new([n], [n], dt, COMP[codec](p))
 
 
-def gpu_decode(codec, stream, dt, n, param=None):
+def gpu_decode(codec, stream, dt, n, param=None, flags=0):
     """read_chunk on the GPU; returns (kind or 'Ok', host-native bytes)."""
     es, be, isb, npdt = dtype_info(dt)
     meta = meta_for(codec, dt, n, param)
     try:
-        ch = DefaultChunk.read_chunk(stream, meta, [0], npdt)
+        ch = DefaultChunk.read_chunk(stream, meta, [0], npdt, flags=flags)
     except ZarrIOError as e:
         return e.kind, b""
     return "Ok", ch.get_data().tobytes()
+
+
+# a one-chunk gzip read runs the 256-lane kernel by default (small batch);
+# every gzip check also forces the one-wave-per-chunk kernel (the C2 kernel)
+FLAG_INFLATE_WAVE = 0x4000
 
 
 KIND = {zref.OK: "Ok", zref.EOF: "UnexpectedEof", zref.INVALID_DATA: "InvalidData"}
@@ -49,10 +54,11 @@ KIND = {zref.OK: "Ok", zref.EOF: "UnexpectedEof", zref.INVALID_DATA: "InvalidDat
 def check(codec, stream, dt, n, param=None):
     es, be, isb, _ = dtype_info(dt)
     st, ref = zref.decode(CODEC_IDS[codec], stream, n * es, es, be, isb)
-    kind, out = gpu_decode(codec, stream, dt, n, param)
-    assert kind == KIND[st], (kind, st)
-    if st == zref.OK:
-        assert out == ref
+    for flags in ((0, FLAG_INFLATE_WAVE) if codec == "gzip" else (0,)):
+        kind, out = gpu_decode(codec, stream, dt, n, param, flags)
+        assert kind == KIND[st], (kind, st, flags)
+        if st == zref.OK:
+            assert out == ref, flags
 
 
 def test_native_library_is_loaded():
@@ -87,8 +93,9 @@ def test_zarrita_golden_replay():
     meta = ArrayMetadata.from_json(zarrita_meta_json())
     chunks = zarrita_chunks()
     for g, stream, expected in chunks:
-        ch = DefaultChunk.read_chunk(stream, meta, list(g), np.int16)
-        assert np.array_equal(ch.get_data(), expected), g
+        for flags in (0, FLAG_INFLATE_WAVE):
+            ch = DefaultChunk.read_chunk(stream, meta, list(g), np.int16, flags=flags)
+            assert np.array_equal(ch.get_data(), expected), (g, flags)
     status, outs = read_chunks_host(meta, [c[1] for c in chunks], np.int16)
     assert (status == 0).all()
     for (g, _, expected), o in zip(chunks, outs):
@@ -434,11 +441,12 @@ def test_inflate_parallel_vs_serial_kernel(data):
             a = DefaultChunk.read_chunk(s, meta, [0], np.uint8).get_data()
             b = DefaultChunk.read_chunk(s, meta, [0], np.uint8, flags=FLAG_SERIAL_INFLATE).get_data()
             c = DefaultChunk.read_chunk(s, meta, [0], np.uint8, flags=FLAG_INFLATE_BLOCK_PAR).get_data()
-            assert np.array_equal(a, b) and np.array_equal(a, c)
+            w = DefaultChunk.read_chunk(s, meta, [0], np.uint8, flags=FLAG_INFLATE_WAVE).get_data()
+            assert np.array_equal(a, b) and np.array_equal(a, c) and np.array_equal(a, w)
             assert a.tobytes() == payload[:D]
     s = streams[1]
     meta = meta_for("gzip", "u1", len(payload))
-    for f in (FLAG_DEBUG_COUNTERS, FLAG_DEBUG_COUNTERS | FLAG_INFLATE_BLOCK_PAR):
+    for f in (FLAG_DEBUG_COUNTERS | FLAG_INFLATE_WAVE, FLAG_DEBUG_COUNTERS | FLAG_INFLATE_BLOCK_PAR):
         assert DefaultChunk.read_chunk(s, meta, [0], np.uint8, flags=f).get_data().tobytes() == payload
 
 
@@ -454,7 +462,7 @@ def test_decode_never_writes_past_n(codec):
                for p in payloads]
     guard = 4096
     for D in (1, 777, 16385, 65537, 99999, 200003):
-        flag_sets = (0, FLAG_SERIAL_INFLATE, FLAG_INFLATE_BLOCK_PAR) if codec == "gzip" else (0,)
+        flag_sets = (0, FLAG_SERIAL_INFLATE, FLAG_INFLATE_BLOCK_PAR, FLAG_INFLATE_WAVE) if codec == "gzip" else (0,)
         for flags in flag_sets:
             dst = torch.full((len(streams) * (D + guard),), 0xAB, dtype=torch.uint8, device="cuda:0")
             packed = PackedStreams(streams, D + guard, "cuda:0", dst=dst)
@@ -509,5 +517,5 @@ def test_gzip_dynamic_header_corruption():
                 bad = bytearray(s)
                 bad[hdr + off + k] ^= x
                 variants.append(bytes(bad))
-    for flags in (0, FLAG_SERIAL_INFLATE, FLAG_INFLATE_BLOCK_PAR):
+    for flags in (0, FLAG_SERIAL_INFLATE, FLAG_INFLATE_BLOCK_PAR, FLAG_INFLATE_WAVE):
         check_many("gzip", variants, "u1", len(payload), flags)

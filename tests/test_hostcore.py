@@ -147,3 +147,71 @@ def test_bzip2_core_reference_vector():
     st, out = host_bz2(bytes.fromhex(d["chunks"]["bzip2"]["hex"]), 12)
     assert st == 0
     assert np.frombuffer(out, ">i2").tolist() == d["expected_values"]
+
+
+# ---- LZ4 block compressor: serial restatement vs liblz4 (byte-exact) -------
+_LZ4 = None
+
+
+def liblz4():
+    global _LZ4
+    if _LZ4 is None:
+        import ctypes.util
+        _LZ4 = ctypes.CDLL(ctypes.util.find_library("lz4") or "liblz4.so.1")
+        _LZ4.LZ4_compress_fast.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                           ctypes.c_int]
+        _LZ4.LZ4_compress_fast.restype = ctypes.c_int
+    return _LZ4
+
+
+def lz4_pair(block: bytes):
+    """(liblz4, restatement) of one block at LZ4F's capacity srcSize - 1."""
+    n = len(block)
+    a = np.frombuffer(block, np.uint8) if n else np.zeros(1, np.uint8)
+    cap = max(n - 1, 0)
+    o1 = np.zeros(n + 64, np.uint8)
+    o2 = np.zeros(n + 64, np.uint8)
+    r1 = liblz4().LZ4_compress_fast(a.ctypes.data, o1.ctypes.data, n, cap, 1)
+    h = host()
+    h.zref_lz4_fast_block.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
+    r2 = h.zref_lz4_fast_block(a.ctypes.data, n, o2.ctypes.data, cap)
+    return (r1, o1[:max(r1, 0)].tobytes()), (r2, o2[:max(r2, 0)].tobytes())
+
+
+def lz4_blocks_corpus(seed):
+    rng = np.random.default_rng(seed)
+    out = []
+    for k in range(4):
+        for n in (0, 1, 12, 13, 14, 100, 4095, 4096, 65535, 65536):
+            out.append(_data(rng, k, n))
+    # C4-shaped blocks (random walk i16), the C2 "quant" f32 field, sparse
+    # repeats, near-incompressible blocks around the stored/compressed boundary
+    for _ in range(12):
+        out.append(np.cumsum(rng.integers(-3, 4, 32768)).astype("<i2").tobytes())
+    i = np.arange(16384)
+    out.append((np.round(64 * (100 * np.sin(0.05 * (i + seed)) + i % 7)) / 64).astype("<f4").tobytes())
+    for frac in (0.0, 0.002, 0.01, 0.03):
+        b = rng.integers(0, 256, 65536, dtype=np.uint8)
+        m = rng.random(65536) < frac
+        b[m] = 0
+        out.append(b.tobytes())
+    b = bytearray(rng.integers(0, 256, 65536, dtype=np.uint8).tobytes())
+    for _ in range(40):  # copies of earlier pieces at random offsets
+        L = int(rng.integers(4, 300)); s = int(rng.integers(0, 65536 - L)); d = int(rng.integers(0, 65536 - L))
+        b[d:d + L] = b[s:s + L]
+    out.append(bytes(b))
+    # byU32 blocks (lz4 blockSize 256K / 1M): distances past 65 535 are skipped
+    for n in (65546, 65547, 70000, 262144):
+        out.append(np.cumsum(rng.integers(-3, 4, n // 2)).astype("<i2").tobytes())
+    b = rng.integers(0, 256, 200000, dtype=np.uint8)
+    b[100000:150000] = b[0:50000]  # repeats 100 000 back: out of range
+    b[150000:160000] = b[120000:130000]
+    out.append(b.tobytes())
+    return out
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_lz4_fast_block_restatement_matches_liblz4(seed):
+    for blk in lz4_blocks_corpus(seed):
+        (r1, o1), (r2, o2) = lz4_pair(blk)
+        assert r1 == r2 and o1 == o2, (len(blk), r1, r2)

@@ -49,7 +49,7 @@ def timed(flags, reps=5):
     return round(min(ts), 3), round(float(np.median(ts)), 3)
 
 
-for tag, fl in (("wave", 0), ("blockpar", _native.FLAG_INFLATE_BLOCK_PAR)):
+for tag, fl in (("wave", _native.FLAG_INFLATE_WAVE), ("blockpar", _native.FLAG_INFLATE_BLOCK_PAR)):
     packed.dst.zero_()
     mn, med = timed(fl)
     check(tag)
@@ -61,7 +61,7 @@ fn = L.zcg__debug_inflate_wave_counters
 fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
 out = np.zeros(32, np.uint64)
 fn(out.ctypes.data, 1)
-codec.decode(meta, packed, flags=_native.FLAG_DEBUG_COUNTERS)
+codec.decode(meta, packed, flags=_native.FLAG_DEBUG_COUNTERS | _native.FLAG_INFLATE_WAVE)
 torch.cuda.synchronize()
 fn(out.ctypes.data, 1)
 names = {0: "rounds", 1: "blocks", 2: "stages", 3: "groups", 4: "p1_lane_it", 5: "p2_lane_it", 6: "chain",

@@ -22,6 +22,7 @@ FLAG_SKIP_LZ4_BLOCK_CHECKSUM = 0x4
 FLAG_SERIAL_INFLATE = 0x100
 FLAG_DEBUG_COUNTERS = 0x200
 FLAG_INFLATE_BLOCK_PAR = 0x2000
+FLAG_INFLATE_WAVE = 0x4000
 
 STATUS_NAMES = {OK: "Ok", UNEXPECTED_EOF: "UnexpectedEof", INVALID_DATA: "InvalidData",
                 INVALID_INPUT: "InvalidInput", UNSUPPORTED: "Unsupported",

@@ -235,6 +235,17 @@ uint64_t zcg_encode_bound(const zcg_compression* c, uint64_t n) {
     }
 }
 
+// Gzip decode: the 256-lane kernel for a batch that fits one generation of
+// it (3 workgroups per CU), the one-wave-per-chunk kernel above that
+// (measured, 4 096 C2 chunks vs fewer: 128-512 chunks 9.2-9.8 ms vs 17-18 ms,
+// 1 024 18.6 vs 18.2, 4 096 55.7 vs 31.5).
+static bool inflate_par_pick(const zcg_array* a, uint32_t n) {
+    const uint32_t f = a->compression.flags;
+    if (f & ZCG_FLAG_INFLATE_BLOCK_PAR) return true;
+    if (f & ZCG_FLAG_INFLATE_WAVE) return false;
+    return n <= 3 * zcg::device_cu_count();
+}
+
 uint64_t zcg_workspace_bytes(const zcg_array* a, uint32_t n, int encode) {
     if (!a) return 0;
     if (a->compression.codec == ZCG_CODEC_BZIP2)
@@ -243,7 +254,7 @@ uint64_t zcg_workspace_bytes(const zcg_array* a, uint32_t n, int encode) {
     if (a->compression.codec == ZCG_CODEC_GZIP)
         return encode ? deflate_ws_bytes(a, n)
                       : ((a->compression.flags & ZCG_FLAG_SERIAL_INFLATE) ? 0
-                         : (a->compression.flags & ZCG_FLAG_INFLATE_BLOCK_PAR) ? inflate_par_ws_bytes(a, n)
+                         : inflate_par_pick(a, n) ? inflate_par_ws_bytes(a, n)
                                                                                 : inflate_wave_ws_bytes(a, n));
     if (a->compression.codec == ZCG_CODEC_LZ4) return encode ? lz4_encode_ws_bytes(a, n) : lz4_decode_ws_bytes(a, n);
     return 0;
@@ -272,7 +283,7 @@ int zcg_decode_batch(zcg_ctx* ctx, const zcg_array* a, const zcg_chunk* d_chunks
             break;
         }
         zcg_ctx::Ws* w = nullptr;
-        if (a->compression.flags & ZCG_FLAG_INFLATE_BLOCK_PAR) {
+        if (inflate_par_pick(a, n)) {
             const int r = stream_ws(ctx, stream, inflate_par_ws_bytes(a, n), &w);
             if (r != ZCG_OK) return r;
             e = launch_inflate_par(a, d_chunks, n, d_status, w->p, w->bytes, s);

@@ -1,46 +1,54 @@
-// zcg_lz4_enc.hip — LZ4 frame encoder (write_chunk for CompressionType::Lz4).
+// zcg_lz4_enc.hip — LZ4 frame encoder (write_chunk for CompressionType::Lz4),
+// byte-identical to the reference's.
 //
 // Reference: lz.rs:81-92 builds lz4-rs's encoder with the effective block size
 // (lz.rs:55-65), BlockMode::Independent, level 0, content checksum on, no
-// content size, no block checksum; LZ4F then writes
+// content size, no block checksum; LZ4F (liblz4 1.9.3, lz4-sys) then writes
 //   magic 04 22 4D 18 | FLG 0x64 | BD (id << 4) | HC = XXH32(FLG,BD) >> 8
 //   blocks: u32 LE size (bit 31 = stored) + data; an end mark 0; XXH32(content).
-// A block is stored uncompressed when its compressed form is not smaller
-// (LZ4F_makeBlock).  The compressed bytes themselves are not pinned by the
-// reference; any valid LZ4 block that LZ4_decompress_safe accepts
-// is a correct encoding, checked by round trips through the oracle.
+// Each block is LZ4F_makeBlock -> LZ4F_compressBlock ->
+// LZ4_compress_fast_extState_fastReset(acceleration 1) on a cleared table with
+// dstCapacity = srcSize - 1, and is stored raw when that returns 0.  The
+// block compressor is a deterministic serial algorithm; tests/hostcore/
+// lz4_fast_ref.c restates it serially (pinned byte for byte to liblz4's
+// LZ4_compress_fast by tests/test_hostcore.py) and this file restates the
+// same steps with a wave-parallel search, so the GPU frames equal lz4-rs's
+// frames byte for byte (tests/test_gpu_encode.py compares them with the
+// oracle's liblz4 LZ4F frames).
 //
 // Kernels (stream-ordered):
-//   0. match finding, data-parallel over every position of a sub-batch
-//      (<= 128 MiB): keys (block, 20-bit hash of 4 serialised bytes) sorted
-//      with the positions as values (hipCUB radix sort, stable), lz_chain links
-//      each position to its predecessor with the same key, lz_best walks up to
-//      LZ_DEPTH candidates with offsets <= 65535 and keeps the longest match
-//      that ends before the block's last 5 literals (LZ4's end-of-block rules).
-//   1. lz4_block_compress: one wave per block, greedy like LZ4's fast
-//      encoder: the 64 lanes hold 64 consecutive positions' precomputed
-//      matches and the first one starts the next sequence; literals are read
-//      from HBM with the dtype transform (write_data's byte order,
-//      chunk.rs:118-140), so the kernel uses no LDS.
-//      Block k is written at its upper-bound slot 7 + k*(B+4) of dst.
+//   1. lz4_block_exact: one wave per block, the hash table (16 KiB) in LDS.
+//      The match search of LZ4_compress_generic visits positions with
+//      data-independent steps (1 for the first 65 attempts, then growing by
+//      the skip trigger) and, per attempt, reads the table at the position's
+//      hash, writes the position there and compares 4 bytes.  The wave runs 64
+//      attempts at once: lane j takes attempt k0 + j (its position from a
+//      prefix sum of the steps), reads its candidate from the table, and the
+//      first lane whose candidate matches ends the search.  A lane's candidate
+//      is the table's value only if no earlier lane of the batch writes the
+//      same hash; the lanes tag their table entries with their lane id and
+//      read them back, so the batch is cut at the first lane that shares a
+//      hash with an earlier lane (it starts the next batch).  The table is
+//      then left exactly as the serial attempts leave it.  Catch-up, match
+//      length (LZ4_count), the output-budget checks, the table fill at ip-2
+//      and the next-position test are the serial code's, run wave-uniform.
+//      Literals are read with the dtype transform (write_data's byte order,
+//      chunk.rs:118-140).  Block k is written at its upper-bound slot
+//      7 + k*(B+4) of dst.
 //   2. lz4_frame_finalize: one workgroup per chunk writes the frame header,
 //      compacts the blocks to their final offsets (tile copies, dst <= src),
 //      writes the end mark and the output length.
 //   3. lz4_content_xxh32: 4 lanes per chunk (one XXH32 accumulator each)
 //      hash the serialised content and write the content checksum.
-#include <hipcub/hipcub.hpp>
-
 #include "zcg_common.h"
 
 namespace zcg {
 
-constexpr u32 LE_WIN = 65536;       // LDS window (matches stay inside it)
-constexpr u32 LE_HBITS = 12;        // hash table entries = 4096
-constexpr u32 LE_MFLIMIT = 12;      // last match starts >= 12 bytes before block end
-constexpr u32 LE_LASTLIT = 5;       // last 5 bytes are literals
-constexpr u32 LE_MINLEN = 13;       // shorter blocks are literals only
+constexpr u32 LE_MFLIMIT = 12;      // MFLIMIT
+constexpr u32 LE_LASTLIT = 5;       // LASTLITERALS
+constexpr u32 LE_MINLEN = 13;       // LZ4_minLength: shorter blocks are literals only (-> stored)
 constexpr u32 LE_HDR = 7;           // frame header bytes
-constexpr u32 LE_MCAP = 32;         // match bytes measured by lz_best (longer ones are extended here)
+constexpr u32 LE_64KLIMIT = 65536 + LE_MFLIMIT - 1;  // LZ4_64Klimit: byU16 table below it
 
 // Logical (serialised) byte x of the chunk: the stream holds elements in the
 // array's byte order; bool as 0/1.
@@ -48,117 +56,243 @@ __device__ __forceinline__ u8 src_byte(const u8* src, u64 x, const DType& t) {
     return norm_byte(src[swap_pos(x, t)], t);
 }
 
-// Write `n` literal bytes of the chunk starting at logical position `x` to
-// out[o..).  Bytes inside the staged window come from LDS, others from src.
-__device__ void put_literals(u8* out, u64 o, const u8* src, u64 x, u32 n, const u8* win, u64 wbase,
-                             u32 wlen, const DType& t) {
-    const u32 lane = lane_id();
-    for (u32 k = lane; k < n; k += 64) {
-        const u64 p = x + k;
-        u8 v;
-        if (p >= wbase && p < wbase + wlen) v = win[p - wbase];
-        else v = src_byte(src, p, t);
-        out[o + k] = v;
+typedef __attribute__((address_space(1))) u32 le_gu32_ua __attribute__((aligned(1)));
+
+// The serialised chunk as the block compressor reads it (plain loads for
+// little-endian non-bool types, the transform byte by byte otherwise).
+struct LeSrc {
+    const u8* src;
+    DType t;
+    bool plain;
+    __device__ __forceinline__ u8 b1(u64 x) const {
+        return plain ? ((const gu8*)src)[x] : src_byte(src, x, t);
     }
+    __device__ __forceinline__ u32 b4(u64 x) const {
+        if (plain) return *(const le_gu32_ua*)((const gu8*)src + x);
+        return (u32)b1(x) | ((u32)b1(x + 1) << 8) | ((u32)b1(x + 2) << 16) | ((u32)b1(x + 3) << 24);
+    }
+};
+
+__device__ __forceinline__ void le_wsync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// Bytes of a length field (token nibble already counts 15).
-__device__ __forceinline__ u32 len_bytes(u32 v) { return v >= 15 ? (v - 15) / 255 + 1 : 0; }
-
-__device__ void put_len(u8* out, u64 o, u32 v) {  // v >= 15; writes len_bytes(v) bytes
-    const u32 lane = lane_id();
-    const u32 nb = len_bytes(v);
-    for (u32 k = lane; k + 1 < nb; k += 64) out[o + k] = 255;
-    if (lane == 0) out[o + nb - 1] = (u8)((v - 15) % 255);
+__device__ __forceinline__ u32 le_incl_scan(u32 v) {
+    const u32 lane = (u32)lane_id();
+#pragma unroll
+    for (u32 d = 1; d < 64; d <<= 1) {
+        const u32 x = (u32)__shfl_up((int)v, d, 64);
+        v += lane >= d ? x : 0u;
+    }
+    return v;
 }
 
-__global__ __launch_bounds__(64) void lz4_block_compress(const zcg_chunk* __restrict__ chunks, u32 c0, u32 n,
-                                                         u64 D, u32 B, u32 nbpc, u64 bound, DType t,
-                                                         const u32* __restrict__ match) {
+__device__ __forceinline__ u32 le_wave_min(u32 v) {
+#pragma unroll
+    for (u32 d = 1; d < 64; d <<= 1) {
+        const u32 x = (u32)__shfl_xor((int)v, d, 64);
+        v = x < v ? x : v;
+    }
+    return v;
+}
+
+// LZ4_hashPosition: byU16 (block < LZ4_64Klimit): hash4, 13 bits;
+// byU32: hash5 of the 5 bytes at p, 12 bits (LZ4_hash5 on a 64-bit LE host)
+template <bool U32>
+__device__ __forceinline__ u32 le_hash(const LeSrc& v, u64 p) {
+    if (!U32) return (v.b4(p) * 2654435761u) >> 19;
+    const u64 q = (u64)v.b4(p) | ((u64)v.b1(p + 4) << 32);
+    return (u32)(((q << 24) * 889523592379ull) >> 52);
+}
+
+// One block of S bytes starting at logical b0, compressed into out[0, cap)
+// as LZ4_compress_generic (limitedOutput, noDict, acceleration 1); returns the
+// compressed size, or 0 when it does not fit (the caller stores the block).
+// T: the wave's 16 KiB table (u16 entries for byU16, u32 for byU32).
+template <bool U32>
+__device__ u32 le_block(const LeSrc& v, u64 b0, u32 S, u8* out, u32 cap, lu32* T32) {
+    const u32 lane = (u32)lane_id();
+    __attribute__((address_space(3))) u16* T16 = (__attribute__((address_space(3))) u16*)T32;
+    auto tget = [&](u32 h) -> u32 { return U32 ? T32[h] : (u32)T16[h]; };
+    auto tput = [&](u32 h, u32 x) { if (U32) T32[h] = x; else T16[h] = (u16)x; };
+    auto hp = [&](u32 p) -> u32 { return le_hash<U32>(v, b0 + p); };
+    auto r4 = [&](u32 p) -> u32 { return v.b4(b0 + p); };
+    // write n literal bytes [a, a + n) at out[o..)
+    auto put_lits = [&](u32 o, u32 a, u32 n) {
+        for (u32 i = lane; i < n; i += 64) out[o + i] = v.b1(b0 + a + i);
+    };
+    // a length field's extra bytes (value >= 15): (x-15)/255 bytes of 255, then (x-15)%255
+    auto put_len = [&](u32 o, u32 x) -> u32 {
+        const u32 r = x - 15, nb = r / 255;
+        for (u32 i = lane; i < nb; i += 64) out[o + i] = 255;
+        if (lane == 0) out[o + nb] = (u8)(r % 255);
+        return nb + 1;
+    };
+    u32 op = 0, anchor = 0;
+    if (S >= LE_MINLEN) {
+        const u32 mfl1 = S - LE_MFLIMIT + 1;  // mflimitPlusOne
+        const u32 mlim = S - LE_LASTLIT;      // matchlimit
+        // the table is clear (index 0 everywhere): putPosition(0) changes nothing
+        u32 ip = 1;
+        for (;;) {
+            // ---- match search from ip: 64 attempts per step ------------------
+            u32 s0 = ip, k0 = 0, mpos = 0, mref = 0;
+            bool found = false;
+            for (;;) {
+                const u32 k = k0 + lane;
+                const u32 st = k == 0 ? 1u : (63u + k) >> 6;  // the step after attempt k
+                const u32 inc = le_incl_scan(st);
+                const u32 pos = s0 + inc - st, nxt = s0 + inc;
+                const bool valid = nxt <= mfl1;  // (a prefix of the lanes)
+                const u64 vm = __ballot(valid);
+                if (!vm) break;
+                const u32 V = (u32)__popcll(vm);
+                u32 h = 0, old = 0;
+                if (valid) { h = hp(pos); old = tget(h); }
+                le_wsync();
+                if (valid) tput(h, lane);  // tag: who writes this hash last in the batch
+                le_wsync();
+                const u32 rd = valid ? tget(h) : lane;
+                const bool dup = valid && rd != lane;
+                // smallest lane of any hash shared inside the batch
+                const u32 g = le_wave_min(dup ? (rd < lane ? rd : lane) : 64u);
+                const u32 P = g + 1 < V ? g + 1 : V;  // lanes [0, P) see the serial candidates
+                bool ok = false;
+                if (lane < P && (!U32 || old + 65535u >= pos)) ok = r4(old) == r4(pos);
+                const u64 om = __ballot(ok);
+                const u32 w = om ? (u32)__builtin_ctzll(om) : 64u;
+                const u32 m = w < 64 ? w : P - 1;  // last attempt taken
+                // leave the table as attempts 0..m leave it (lanes <= m hash apart)
+                le_wsync();
+                if (valid && lane > m) tput(h, old);
+                le_wsync();
+                if (valid && lane <= m) tput(h, pos);
+                le_wsync();
+                if (w < 64) {
+                    mpos = (u32)__builtin_amdgcn_readlane((int)pos, (int)w);
+                    mref = (u32)__builtin_amdgcn_readlane((int)old, (int)w);
+                    found = true;
+                    break;
+                }
+                if (P == V && V < 64) break;  // attempt V ends the search: last literals
+                s0 = (u32)__builtin_amdgcn_readlane((int)nxt, (int)(P - 1));
+                k0 += P;
+            }
+            if (!found) break;
+            // ---- catch up --------------------------------------------------------
+            u32 mip = mpos, mm = mref;
+            for (;;) {
+                const u32 lim = (mip - anchor) < mm ? (mip - anchor) : mm;
+                const bool eq = lane < lim && v.b1(b0 + mip - 1 - lane) == v.b1(b0 + mm - 1 - lane);
+                const u64 ne = __ballot(!eq);
+                const u32 c = ne ? (u32)__builtin_ctzll(ne) : 64u;
+                mip -= c;
+                mm -= c;
+                if (c < 64) break;
+            }
+            // ---- literals --------------------------------------------------------
+            const u32 lit = mip - anchor;
+            u32 tpos = op;
+            op++;
+            if ((u64)op + lit + (2 + 1 + LE_LASTLIT) + lit / 255 > cap) return 0;
+            if (lit >= 15) op += put_len(op, lit);
+            put_lits(op, anchor, lit);
+            op += lit;
+            u32 tok = (lit < 15 ? lit : 15u) << 4;
+            for (;;) {  // _next_match
+                const u32 off = mip - mm;
+                if (lane == 0) { out[op] = (u8)off; out[op + 1] = (u8)(off >> 8); }
+                op += 2;
+                // LZ4_count(ip + 4, match + 4, matchlimit), 256 bytes per step
+                u32 mc = 0;
+                for (;;) {
+                    const u32 a = mip + 4 + mc + 4 * lane, bq = mm + 4 + mc + 4 * lane;
+                    u32 x;
+                    if (a + 4 <= mlim) {
+                        x = r4(a) ^ r4(bq);
+                    } else {
+                        x = 0;
+                        for (u32 j = 0; j < 4; j++) {
+                            const bool d = a + j >= mlim || v.b1(b0 + a + j) != v.b1(b0 + bq + j);
+                            x |= d ? (0xFFu << (8 * j)) : 0u;
+                        }
+                    }
+                    const u64 dm = __ballot(x != 0);
+                    if (!dm) { mc += 256; continue; }
+                    const u32 f = (u32)__builtin_ctzll(dm);
+                    const u32 xf = (u32)__builtin_amdgcn_readlane((int)x, (int)f);
+                    mc += 4 * f + ((u32)__builtin_ctz(xf) >> 3);
+                    break;
+                }
+                mip += mc + 4;
+                if ((u64)op + (1 + LE_LASTLIT) + (mc + 240) / 255 > cap) return 0;
+                if (mc >= 15) {
+                    tok |= 15;
+                    op += put_len(op, mc);
+                } else {
+                    tok |= mc;
+                }
+                if (lane == 0) out[tpos] = (u8)tok;
+                anchor = mip;
+                if (mip >= mfl1) break;
+                // fill table at ip - 2, then test the next position
+                const u32 h2 = hp(mip - 2);
+                le_wsync();
+                tput(h2, mip - 2);
+                le_wsync();
+                const u32 h = hp(mip);
+                const u32 cand = tget(h);
+                le_wsync();
+                tput(h, mip);
+                le_wsync();
+                if ((!U32 || cand + 65535u >= mip) && r4(cand) == r4(mip)) {
+                    tpos = op;
+                    op++;
+                    tok = 0;
+                    mm = cand;
+                    continue;
+                }
+                break;
+            }
+            if (anchor >= mfl1) break;
+            ip = mip + 1;
+        }
+    }
+    // ---- last literals -----------------------------------------------------------
+    const u32 last = S - anchor;
+    if ((u64)op + last + 1 + (last + 240) / 255 > cap) return 0;
+    if (lane == 0) out[op] = (u8)((last < 15 ? last : 15u) << 4);
+    op++;
+    if (last >= 15) op += put_len(op, last);
+    put_lits(op, anchor, last);
+    return op + last;
+}
+
+__global__ __launch_bounds__(64) void lz4_block_exact(const zcg_chunk* __restrict__ chunks, u32 n, u64 D, u32 B,
+                                                      u32 nbpc, u64 bound, DType t) {
+    __shared__ __attribute__((aligned(16))) u32 T[4096];  // 16 KiB: 8192 u16 or 4096 u32 entries
     const u32 lane = threadIdx.x;
-    const u32 cl = blockIdx.x / nbpc, k = blockIdx.x % nbpc;
-    if (cl >= n) return;
-    const u32 c = c0 + cl;
+    const u32 c = blockIdx.x / nbpc, k = blockIdx.x % nbpc;
+    if (c >= n) return;
     const zcg_chunk ch = chunks[c];
     if (ch.dst_cap < bound || ch.src_len < D) return;  // finalize reports the status
-    const u8* src = (const u8*)ch.src;
-    u8* dst = (u8*)ch.dst;
-    const u64 b0 = (u64)k * B;                          // logical start of the block
-    const u32 S = (u32)((D - b0) < B ? (D - b0) : B);   // block bytes
-    const u32* mt = match + (u64)cl * D + b0;           // precomputed matches of the block
-    u8* hdr = dst + LE_HDR + (u64)k * (B + 4);
+    const u64 b0 = (u64)k * B;
+    const u32 S = (u32)((D - b0) < B ? (D - b0) : B);
+    u8* hdr = (u8*)ch.dst + LE_HDR + (u64)k * (B + 4);
     u8* out = hdr + 4;
-    u64 op = 0;          // output bytes of this block
-    bool stored = S < LE_MINLEN;
-    u64 anchor = 0;      // block-relative start of the pending literal run
-    if (!stored) {
-        // match starts < S - MFLIMIT, match ends <= S - LASTLIT (lz_best clips)
-        const u32 mflim = S - LE_MFLIMIT;
-        u32 ip = 0;
-        u32 wbase = 0xFFFFFFFFu, wm = 0;  // 64 positions' matches, one per lane
-        while (ip < mflim) {
-            if (ip < wbase || ip >= wbase + 64) {
-                wbase = ip;
-                const u32 p = ip + lane;
-                wm = p < mflim ? mt[p] : 0u;
-            }
-            const u32 sh = ip - wbase;
-            const unsigned long long m = __ballot((wm & 0xFFFF) >= 4) & (~0ull << sh);
-            if (!m) { ip = wbase + 64; continue; }
-            const u32 f = (u32)__builtin_ctzll(m);
-            const u32 mv = __shfl(wm, (int)f, 64);
-            const u32 mpos = wbase + f;
-            u32 mlen = mv & 0xFFFF;
-            const u32 d = mv >> 16;
-            if (mlen == LE_MCAP) {  // measured to the cap: extend 64 bytes per step
-                const u32 lim = S - LE_LASTLIT;  // block-relative match end limit
-                u32 e2 = mpos + mlen;
-                for (;;) {
-                    const u32 x = e2 + lane;
-                    const bool ok = x < lim && src_byte(src, b0 + x, t) == src_byte(src, b0 + x - d, t);
-                    const unsigned long long bm = __ballot(!ok);
-                    const u32 run = bm ? (u32)__builtin_ctzll(bm) : 64u;
-                    e2 += run;
-                    if (run < 64) break;
-                }
-                mlen = e2 - mpos;
-            }
-            // ---- emit the sequence: literals [anchor, mpos), match (d, mlen) ----
-            const u32 lit = (u32)(mpos - anchor);
-            const u64 sz = 1 + len_bytes(lit) + lit + 2 + len_bytes(mlen - 4);
-            if (op + sz + 1 + LE_LASTLIT >= S) { stored = true; break; }
-            if (lane == 0) out[op] = (u8)(((lit < 15 ? lit : 15) << 4) | ((mlen - 4) < 15 ? (mlen - 4) : 15));
-            u64 o = op + 1;
-            if (lit >= 15) { put_len(out, o, lit); o += len_bytes(lit); }
-            put_literals(out, o, src, b0 + anchor, lit, nullptr, 0, 0, t);
-            o += lit;
-            if (lane == 0) { out[o] = (u8)(d & 0xFF); out[o + 1] = (u8)(d >> 8); }
-            o += 2;
-            if (mlen - 4 >= 15) { put_len(out, o, mlen - 4); o += len_bytes(mlen - 4); }
-            op = o;
-            anchor = mpos + mlen;
-            ip = mpos + mlen;
-        }
-    }
-    if (!stored) {  // last literals
-        const u32 lit = (u32)(S - anchor);
-        const u64 sz = 1 + len_bytes(lit) + lit;
-        if (op + sz >= S) {
-            stored = true;
-        } else {
-            if (lane == 0) out[op] = (u8)((lit < 15 ? lit : 15) << 4);
-            u64 o = op + 1;
-            if (lit >= 15) { put_len(out, o, lit); o += len_bytes(lit); }
-            put_literals(out, o, src, b0 + anchor, lit, nullptr, 0, 0, t);
-            op = o + lit;
-        }
-    }
-    if (stored) {  // uncompressed block (LZ4F_makeBlock)
-        for (u32 q = lane; q < S; q += 64) out[q] = src_byte(src, b0 + q, t);
-        op = S;
-    }
+    const LeSrc v{(const u8*)ch.src, t, !t.swap && !t.isbool};
+    for (u32 i = lane; i < 1024; i += 64) ((__attribute__((address_space(3))) u32x4*)T)[i] = u32x4{0u, 0u, 0u, 0u};
+    le_wsync();
+    const u32 cap = S - 1;
+    const u32 cs = S >= LE_64KLIMIT ? le_block<true>(v, b0, S, out, cap, (lu32*)T)
+                                    : le_block<false>(v, b0, S, out, cap, (lu32*)T);
+    const bool stored = cs == 0;
+    if (stored)  // LZ4F_makeBlock: the block raw
+        for (u32 q = lane; q < S; q += 64) out[q] = v.b1(b0 + q);
     if (lane == 0) {
-        const u32 w = (u32)op | (stored ? 0x80000000u : 0u);
+        const u32 w = stored ? (S | 0x80000000u) : cs;
         hdr[0] = (u8)w; hdr[1] = (u8)(w >> 8); hdr[2] = (u8)(w >> 16); hdr[3] = (u8)(w >> 24);
     }
 }
@@ -274,133 +408,17 @@ __global__ __launch_bounds__(64) void lz4_content_xxh32(const zcg_chunk* __restr
     o[0] = (u8)h; o[1] = (u8)(h >> 8); o[2] = (u8)(h >> 16); o[3] = (u8)(h >> 24);
 }
 
-namespace {
-
-constexpr u32 LZ_DEPTH = 4;                 // chain candidates per position
-constexpr u32 LZ_CAP = LE_MCAP;             // bytes measured per candidate
-constexpr u32 LZ_KEYBITS = 20;
-constexpr u64 LZ_SUB_BYTES = 128ull << 20;  // input bytes per match-finder sub-batch
-constexpr u64 LZ_SUPER_BYTES = 1ull << 30;  // input bytes per block-compress launch
-
-struct LzLayout {
-    u32 m, sm;
-    u64 tot, cub_bytes;
-    u64 off_ka, off_kb, off_va, off_vb, off_prev, off_match, off_cub, total;
-};
-
-LzLayout lz_layout(u64 D, u32 nbpc, u32 n) {
-    LzLayout y{};
-    u64 m = D ? LZ_SUB_BYTES / D : n;
-    if (m < 1) m = 1;
-    if (m > n) m = n;
-    while (m > 1 && m * nbpc > 4096) m--;  // block id + 20 hash bits fit 32
-    y.m = (u32)m;
-    y.tot = m * D;
-    u64 sm = D ? LZ_SUPER_BYTES / D : n;
-    sm = sm / m * m;
-    if (sm < m) sm = m;
-    if (sm > n) sm = n;
-    y.sm = (u32)sm;
-    size_t cb = 0;
-    hipcub::DoubleBuffer<u32> kk(nullptr, nullptr), v(nullptr, nullptr);
-    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, cb, kk, v, (int)(y.tot ? y.tot : 1), 0, 32);
-    y.cub_bytes = (cb + 511) & ~255ull;
-    u64 p = 0;
-    auto take = [&](u64 bytes) { const u64 o = p; p = (p + bytes + 255) & ~255ull; return o; };
-    y.off_ka = take(4 * y.tot);
-    y.off_kb = take(4 * y.tot);
-    y.off_va = take(4 * y.tot);
-    y.off_vb = take(4 * y.tot);
-    y.off_prev = take(4 * y.tot);
-    y.off_match = take(4 * (u64)y.sm * D);
-    y.off_cub = take(y.cub_bytes);
-    y.total = p;
-    return y;
-}
-
-typedef __attribute__((address_space(1))) u32 le_gu32_ua __attribute__((aligned(1)));
-__device__ __forceinline__ u32 lz_ser4(const u8* src, u64 x, const DType& t) {  // bytes x..x+3, LE
-    if (!t.swap && !t.isbool) return *(const le_gu32_ua*)((const __attribute__((address_space(1))) u8*)src + x);  // (global, not flat)
-    return (u32)src_byte(src, x, t) | ((u32)src_byte(src, x + 1, t) << 8) | ((u32)src_byte(src, x + 2, t) << 16) |
-           ((u32)src_byte(src, x + 3, t) << 24);
-}
-
-__global__ void lz_keys(const zcg_chunk* __restrict__ chunks, u32 c0, u64 D, u32 B, u32 nbpc, u64 tot, DType t,
-                        u32* __restrict__ keys, u32* __restrict__ vals) {
-    const u64 g = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= tot) return;
-    const u32 cl = (u32)(g / D);
-    const u64 p = g - (u64)cl * D;
-    const u32 blk = (u32)(p / B);
-    const u64 bend = ((u64)blk + 1) * B < D ? ((u64)blk + 1) * B : D;
-    u32 h = 0;
-    if (p + 4 <= bend && chunks[c0 + cl].src_len >= D) h = (lz_ser4((const u8*)chunks[c0 + cl].src, p, t) * 2654435761u) >> (32 - LZ_KEYBITS);
-    keys[g] = ((cl * nbpc + blk) << LZ_KEYBITS) | h;
-    vals[g] = (u32)g;
-}
-
-__global__ void lz_chain(u64 tot, const u32* __restrict__ keys, const u32* __restrict__ vals,
-                         u32* __restrict__ prev) {
-    const u64 j = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= tot) return;
-    prev[vals[j]] = (j > 0 && keys[j] == keys[j - 1]) ? vals[j - 1] : 0xFFFFFFFFu;
-}
-
-// match[g] = len | offset << 16 (len 0: none); the match starts before the
-// block's MFLIMIT and ends at or before its last LASTLIT bytes
-__global__ void lz_best(const zcg_chunk* __restrict__ chunks, u32 c0, u64 D, u32 B, u64 tot, DType t,
-                        const u32* __restrict__ prev, u32* __restrict__ match) {
-    const u64 g = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= tot) return;
-    const u32 cl = (u32)(g / D);
-    const u64 p = g - (u64)cl * D;
-    const u64 bs = p / B * B;
-    const u64 bend = bs + B < D ? bs + B : D;
-    u32 best = 0, bd = 0;
-    if (p + LE_MFLIMIT < bend && chunks[c0 + cl].src_len >= D) {  // short src: INVALID_DATA in finalize
-        const u8* src = (const u8*)chunks[c0 + cl].src;
-        const u64 cbase = (u64)cl * D;
-        u32 mx = (u32)(bend - LE_LASTLIT - p);  // bytes the match may cover
-        if (mx > LZ_CAP) mx = LZ_CAP;           // longer matches are extended by lz4_block_compress
-        const u32 v0 = lz_ser4(src, p, t);
-        u32 q = prev[g];
-        for (u32 dep = 0; dep < LZ_DEPTH && q != 0xFFFFFFFFu; dep++) {
-            const u64 qp = q - cbase;
-            if (p - qp > 65535) break;
-            const u32 qn = prev[q];  // the next link, in flight during this candidate's compare
-            if (lz_ser4(src, qp, t) == v0) {
-                u32 k = 4;
-                bool diff = false;
-                while (k + 4 <= mx) {
-                    const u32 x = lz_ser4(src, p + k, t) ^ lz_ser4(src, qp + k, t);
-                    if (x) { k += (u32)__builtin_ctz(x) >> 3; diff = true; break; }
-                    k += 4;
-                }
-                if (!diff)
-                    while (k < mx && src_byte(src, p + k, t) == src_byte(src, qp + k, t)) k++;
-                if (k > mx) k = mx;
-                if (k > best) { best = k; bd = (u32)(p - qp); }
-            }
-            q = qn;
-        }
-    }
-    match[g] = best >= 4 ? (best | (bd << 16)) : 0u;
-}
-
-}  // namespace
-
 uint64_t lz4_encode_ws_bytes(const zcg_array* a, uint32_t n) {
-    const DType t = make_dtype(a->dtype);
-    const u64 D = a->chunk_num_elements * (u64)t.es;
-    const u32 B = (u32)zcg_effective_lz4_block_size(a->compression.lz4_block_size);
-    const u32 nbpc = (u32)((D + B - 1) / B);
-    if (n == 0 || nbpc == 0) return 0;
-    return lz_layout(D, nbpc, n).total;
+    (void)a;
+    (void)n;
+    return 0;  // the block compressor's table lives in LDS
 }
 
 hipError_t launch_lz4_encode(const zcg_array* a, const zcg_chunk* d_chunks, uint32_t n,
                              uint64_t* d_out_len, int32_t* d_status, void* ws, uint64_t ws_bytes,
                              hipStream_t s) {
+    (void)ws;
+    (void)ws_bytes;
     if (n == 0) return hipSuccess;
     const DType t = make_dtype(a->dtype);
     const u64 D = a->chunk_num_elements * (u64)t.es;
@@ -409,35 +427,9 @@ hipError_t launch_lz4_encode(const zcg_array* a, const zcg_chunk* d_chunks, uint
     const u64 bound = zcg_encode_bound(&a->compression, D);
     if (nbpc) {
         if (nbpc > 4096) return hipErrorInvalidValue;
-        const LzLayout y = lz_layout(D, nbpc, n);
-        if (ws_bytes < y.total || y.tot >= (1ull << 31)) return hipErrorInvalidValue;
-        u8* w = (u8*)ws;
-        for (u32 s0 = 0; s0 < n; s0 += y.sm) {
-            const u32 scnt = (n - s0) < y.sm ? (n - s0) : y.sm;
-            for (u32 c0 = s0; c0 < s0 + scnt; c0 += y.m) {
-                const u32 cnt = (s0 + scnt - c0) < y.m ? (s0 + scnt - c0) : y.m;
-                const u64 tot = (u64)cnt * D;
-                u32 *ka = (u32*)(w + y.off_ka), *kb = (u32*)(w + y.off_kb);
-                u32 *va = (u32*)(w + y.off_va), *vb = (u32*)(w + y.off_vb);
-                const u32 G = (u32)((tot + 255) / 256);
-                u32 bbits = 0;
-                while ((1u << bbits) < cnt * nbpc) bbits++;
-                hipLaunchKernelGGL(lz_keys, dim3(G), dim3(256), 0, s, d_chunks, c0, D, B, nbpc, tot, t, ka, va);
-                hipcub::DoubleBuffer<u32> dk(ka, kb), dv(va, vb);
-                size_t cb = y.cub_bytes;
-                hipError_t e = hipcub::DeviceRadixSort::SortPairs(w + y.off_cub, cb, dk, dv, (int)tot, 0,
-                                                                  (int)(LZ_KEYBITS + bbits), s);
-                if (e != hipSuccess) return e;
-                hipLaunchKernelGGL(lz_chain, dim3(G), dim3(256), 0, s, tot, dk.Current(), dv.Current(),
-                                   (u32*)(w + y.off_prev));
-                hipLaunchKernelGGL(lz_best, dim3(G), dim3(256), 0, s, d_chunks, c0, D, B, tot, t,
-                                   (const u32*)(w + y.off_prev), (u32*)(w + y.off_match) + (u64)(c0 - s0) * D);
-            }
-            const u64 nb = (u64)scnt * nbpc;
-            if (nb > 0x7FFFFFFFull) return hipErrorInvalidValue;
-            hipLaunchKernelGGL(lz4_block_compress, dim3((u32)nb), dim3(64), 0, s, d_chunks, s0, scnt, D, B, nbpc,
-                               bound, t, (const u32*)(w + y.off_match));
-        }
+        const u64 nb = (u64)n * nbpc;
+        if (nb > 0x7FFFFFFFull) return hipErrorInvalidValue;
+        hipLaunchKernelGGL(lz4_block_exact, dim3((u32)nb), dim3(64), 0, s, d_chunks, n, D, B, nbpc, bound, t);
     }
     hipLaunchKernelGGL(lz4_frame_finalize, dim3(n), dim3(256), 0, s, d_chunks, n, D, B, nbpc, bound,
                        (u64*)d_out_len, d_status);
