@@ -1,7 +1,8 @@
 """ZCG_FLAG_LZ4_{WAVE,LANE}_PER_BLOCK: the two LZ4 block decoders (one lane per
 block, picked for large batches; one wave per block, picked for small ones)
-must give the same bytes and statuses on valid, truncated and corrupted
-frames (lz.rs:81-83 -> LZ4F_decompress), and both must match the oracle."""
+and the default pick must give the same bytes and statuses on valid,
+truncated and corrupted frames (lz.rs:81-83 -> LZ4F_decompress), and all must
+match the oracle."""
 import os
 import sys
 
@@ -61,14 +62,15 @@ def test_lane_and_wave_decoders_agree():
     allst = streams + extra
     s0, o0 = _decode(allst, D, FLAG_LANE)
     s1, o1 = _decode(allst, D, FLAG_WAVE)
-    assert s0.tolist() == s1.tolist()
+    s2, o2 = _decode(allst, D, 0)
+    assert s0.tolist() == s1.tolist() == s2.tolist()
     for i, p in enumerate(pays):
-        assert s0[i] == 0 and bytes(o0[i]) == p and bytes(o1[i]) == p
+        assert s0[i] == 0 and bytes(o0[i]) == p and bytes(o1[i]) == p and bytes(o2[i]) == p
     for i, st in enumerate(allst):
         ost, ref = zref.decode(zref.LZ4, st, D, 1)
         assert ost == s0[i], i
         if ost == 0:
-            assert bytes(o0[i]) == ref and bytes(o1[i]) == ref
+            assert bytes(o0[i]) == ref and bytes(o1[i]) == ref and bytes(o2[i]) == ref
 
 
 FRAMES = {"reference": {}, "linked": dict(linked=True), "block_checksum": dict(block_checksum=True),
@@ -76,10 +78,11 @@ FRAMES = {"reference": {}, "linked": dict(linked=True), "block_checksum": dict(b
           "bd4m": dict(block_size_id=7), "small_blocks": dict(auto_flush=True, feed=10000)}
 
 
+@pytest.mark.parametrize("flags", [0, FLAG_LANE], ids=["default", "lane"])
 @pytest.mark.parametrize("frame", list(FRAMES))
-def test_lane_decoder_frame_variants(frame):
-    """Every frame layout the reference decoder accepts, through the lane
-    decoder, at full length and truncating read_exact lengths."""
+def test_decoder_frame_variants(frame, flags):
+    """Every frame layout the reference decoder accepts, through the default
+    and the lane decoder, at full length and truncating read_exact lengths."""
     pays = _payloads()
     streams = []
     for p in pays:
@@ -88,7 +91,7 @@ def test_lane_decoder_frame_variants(frame):
         else:
             streams.append(zref.lz4_frame_custom(p, **FRAMES[frame]))
     for D in (1 << 20, (1 << 20) - 1000, 65536 * 3, 65536 * 3 + 7):
-        st, out = _decode(streams, D, FLAG_LANE)
+        st, out = _decode(streams, D, flags)
         for i, s in enumerate(streams):
             ost, ref = zref.decode(zref.LZ4, s, D, 1)
             assert ost == st[i], (frame, D, i)

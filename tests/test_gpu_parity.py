@@ -327,7 +327,7 @@ def test_lz4_errors():
     check("lz4", bytes(bad), "u1", len(payload))
 
 
-@pytest.mark.parametrize("lz4_flags", [0, 0x1000], ids=["auto", "lane_per_block"])
+@pytest.mark.parametrize("lz4_flags", [0, 0x1000, 0x800], ids=["default", "lane_per_block", "wave_per_block"])
 def test_lz4_corruption_sweep(lz4_flags):
     """Byte corruptions and truncations of LZ4 frames everywhere (block
     headers, tokens, length bytes, offsets, literals, end mark, checksums),

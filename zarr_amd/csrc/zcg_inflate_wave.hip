@@ -56,12 +56,6 @@
 #ifndef ZIW_DBG
 #define ZIW_DBG 1  // 0: the debug-counter code is compiled out (the flag is ignored)
 #endif
-#ifndef ZIW_GATHER1
-#define ZIW_GATHER1 0  // 1: the far gather issues all 32 entries' loads before one wait
-#endif
-#ifndef ZIW_REFETCH_LATE
-#define ZIW_REFETCH_LATE 0  // 1: the next stage's token loads are issued after the far gather
-#endif
 
 namespace zcg {
 
@@ -911,9 +905,7 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
                     if (group2(tq1a, tq1b, ok1)) break;
                     if (group2(tq2a, tq2b, ok2)) break;
                 }
-#if !ZIW_REFETCH_LATE
                 refetch();  // the next stage starts at the cursor
-#endif
                 IW_ADD(IWD_STAGES, 1);
                 if (__ballot(far) != 0) { r = R_INVALID; break; }
                 const u32 emit = emitted < cap ? emitted : cap;  // a token may cross N: clip
@@ -976,47 +968,6 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
                         // (consecutive sources) come as one unaligned dword, the rest
                         // byte by byte.  16 entries per round.
                         typedef __attribute__((address_space(1))) u32 gu32_ua __attribute__((aligned(1)));
-#if ZIW_GATHER1
-                        // all 32 entries' loads in flight before one wait
-                        u32 qw[8], bv[32];
-#pragma unroll
-                        for (u32 qd = 0; qd < 8; qd++) {
-                            u32 pv[4];
-                            bool all = !tw.swap;
-#pragma unroll
-                            for (u32 j = 0; j < 4; j++) {
-                                const u32 k = qd * 4 + j;
-                                const u32 v = e16(ev, k);
-                                const int xr = xr0 + (int)k;
-                                const bool f = xr >= 0 && xr < (int)emit && v >= IE_FAR && v < IE_VAL;
-                                pv[j] = f ? S32 - (v - IE_FAR + 1) : 0xFFFFFFFFu;
-                                all = all && f && (j == 0 || pv[j] == pv[0] + j);
-                            }
-                            qw[qd] = all ? *(const gu32_ua*)(gd + pv[0]) : 0u;
-#pragma unroll
-                            for (u32 j = 0; j < 4; j++)
-                                bv[qd * 4 + j] = (!all && pv[j] != 0xFFFFFFFFu) ? (u32)gd[swap_pos32(pv[j], tw)] : 0u;
-                        }
-#pragma unroll
-                        for (u32 qd = 0; qd < 8; qd++) {
-                            u32 pv[4];
-                            bool all = !tw.swap;
-#pragma unroll
-                            for (u32 j = 0; j < 4; j++) {
-                                const u32 k = qd * 4 + j;
-                                const u32 v = e16(ev, k);
-                                const int xr = xr0 + (int)k;
-                                const bool f = xr >= 0 && xr < (int)emit && v >= IE_FAR && v < IE_VAL;
-                                pv[j] = f ? S32 - (v - IE_FAR + 1) : 0xFFFFFFFFu;
-                                all = all && f && (j == 0 || pv[j] == pv[0] + j);
-                            }
-#pragma unroll
-                            for (u32 j = 0; j < 4; j++) {
-                                const u32 byte = all ? (qw[qd] >> (8 * j)) & 0xFF : bv[qd * 4 + j];
-                                if (pv[j] != 0xFFFFFFFFu) e16_set(ev, qd * 4 + j, IE_VAL | byte);
-                            }
-                        }
-#else
 #pragma unroll
                         for (u32 qt = 0; qt < 2; qt++) {
                             u32 qw[4], bv[16], pv[16];
@@ -1050,14 +1001,10 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
                                     if (pv[qd * 4 + j] != 0xFFFFFFFFu) e16_set(ev, k, IE_VAL | byte);
                                 }
                         }
-#endif
                     }
                     blk_store(L.u.st.ptr + rb, ev);
                     wsync();
                     IW_T(IWT_GATHER);
-#if ZIW_REFETCH_LATE
-                    refetch();  // the next stage starts at the cursor (after the far loads: vmcnt is in order)
-#endif
                     // pointer jumping: every pointer points strictly backwards, so
                     // log2(IW_S) passes resolve any stage (the cap guards the invariant).
                     // pm = my entries that are still pointers; a pass touches only
@@ -1107,11 +1054,6 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
                     P = S + emit;
                     IW_T(IWT_COMMIT);
                 }
-#if ZIW_REFETCH_LATE
-                else {
-                    refetch();
-                }
-#endif
                 if (why == 1) {
                     // output full: zlib's look-ahead continues at the first untaken token
                     boundary = emitted == cap;
@@ -1202,8 +1144,7 @@ static u32 iw_nslot(uint32_t n) {
 
 const char* cfg_inflate_wave() {
     return "inflate_wave:S=" ZCG_STR(ZIW_S) ",TCAP=" ZCG_STR(ZIW_TCAP) ",WPE=" ZCG_STR(ZIW_WPE)
-           ",EST_PCT=" ZCG_STR(ZIW_EST_PCT) ",MARKW=" ZCG_STR(ZIW_MARKW) ",DBG=" ZCG_STR(ZIW_DBG)
-           ",REFETCH_LATE=" ZCG_STR(ZIW_REFETCH_LATE) ",GATHER1=" ZCG_STR(ZIW_GATHER1);
+           ",EST_PCT=" ZCG_STR(ZIW_EST_PCT) ",MARKW=" ZCG_STR(ZIW_MARKW) ",DBG=" ZCG_STR(ZIW_DBG);
 }
 
 uint64_t inflate_wave_ws_bytes(const zcg_array* a, uint32_t n) {
