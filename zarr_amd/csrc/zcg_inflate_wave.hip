@@ -69,12 +69,12 @@ constexpr u32 IW_K = 4;          // decode steps between staged-token / mark flu
 constexpr u32 IW_KH = 2;         // flush periods per outer step (reader loads at its top, absorbs at its bottom)
 constexpr u32 IW_TSTR = IW_TCAP + IW_K;          // token list stride (a flush writes IW_K words)
 constexpr u32 IW_MWIN = 8;                       // mark words a lane keeps in LDS between flushes
-constexpr u32 IW_MWORDS = IW_SEGMAX / 32 + 2 + IW_MWIN;  // mark words per segment (bitmap, u32)
 #ifndef ZIW_MARKW
 #define ZIW_MARKW 32
 #endif
 constexpr u32 IW_MARKW = ZIW_MARKW;  // bitmap words kept per segment (the rest is never read)
-static_assert(IW_MARKW + 16 <= IW_MWORDS, "dummy mark slot");
+constexpr u32 IW_MWORDS = IW_MARKW + IW_MWIN;  // mark words per segment (bitmap, u32; the last window may spill past IW_MARKW)
+static_assert(IW_MARKW + IW_MWIN <= IW_MWORDS, "mark window inside the bitmap");
 constexpr u32 IW_EST0 = 64 * 3072;  // first block's body estimate (zlib-6 blocks: ~195 Kbit)
 static_assert(IW_S == 2048 && IW_BLK == 32, "the L phase keeps one 32-entry block per lane in registers");
 
@@ -674,11 +674,13 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
                 for (u32 j = 0; j < IW_MWIN; j++) mv[j] = L.u.hr.mwin[j][lane];
                 // marks are kept for the first IW_MARKW words of the segment only
                 // (a misaligned decoder syncs within ~450 bits at p99); later
-                // flushes go to a dummy slot of the lane's bitmap, which stays
-                // in L2, so the stores stay unconditional (counted by the waits)
-                gu32* const mt = w0 < IW_MARKW ? mk + w0 : mk + IW_MARKW + 8;
-                *(gu32x4_a4*)(mt) = u32x4{mv[0], mv[1], mv[2], mv[3]};
-                *(gu32x4_a4*)(mt + 4) = u32x4{mv[4], mv[5], mv[6], mv[7]};
+                // flushes store nothing (stores to a dummy slot instead cost
+                // 14 GB of writes and 11 % of the time per C2 launch: the slot
+                // lines do not stay in L2 under 4 096 chunks' token lists)
+                if (w0 < IW_MARKW) {
+                    *(gu32x4_a4*)(mk + w0) = u32x4{mv[0], mv[1], mv[2], mv[3]};
+                    *(gu32x4_a4*)(mk + w0 + 4) = u32x4{mv[4], mv[5], mv[6], mv[7]};
+                }
                 // slide the window to the word of my next token start (< 8 words on)
                 const u32 w1 = (q - p) >> 5, dw = w1 - w0;
 #pragma unroll
