@@ -384,6 +384,56 @@ def test_xz_encode_incompressible_no_expansion():
     assert len(outs[0]) < D + D // 1000
 
 
+@pytest.mark.parametrize("preset", [4, 6, 9])
+@pytest.mark.parametrize("kind", ["text", "randwalk", "mixed", "zeros", "uniform", "quant"])
+def test_xz_opt_matches_restatement(kind, preset):
+    """Presets 4-9 (liblzma's optimal-parse presets) take the optimal-parse
+    coder: its streams equal the serial restatement's byte for byte
+    (tests/hostcore/xz_opt_ref.cpp) across 256 KiB segments, LZMA2 chunk
+    limits and stored chunks, and decode with liblzma."""
+    from test_hostcore import xz_opt_ref
+    from zarr_amd.compression import Xz
+    if kind == "quant":
+        import sys
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        from bench import quant_chunk
+        arrays = [quant_chunk(i).view(np.uint8) for i in range(2)]
+    else:
+        arrays = [_data(kind, 600001, seed=s) for s in range(2)]
+    D = arrays[0].nbytes
+    meta = ArrayMetadata.new([D * 2], [D], "u1", Xz(preset))
+    st, outs = encode_batch(meta, arrays)
+    assert (st == 0).all()
+    lg = [18, 20, 21, 22, 22, 23, 23, 24, 25, 26][preset]
+    for a, s in zip(arrays, outs):
+        ref = xz_opt_ref(a.tobytes(), lg)
+        if s != ref:
+            k = next((i for i in range(min(len(s), len(ref))) if s[i] != ref[i]), min(len(s), len(ref)))
+            raise AssertionError(f"xz stream differs from the restatement at byte {k} (len {len(s)} vs {len(ref)})")
+        check_xz_stream(s, a.tobytes(), preset)
+
+
+def test_xz_encode_quant_ratio():
+    """C2 "quant" chunks at preset 6: >= 97 % of liblzma preset 6's ratio
+    (>= 6.66 against liblzma's 6.87)."""
+    import lzma
+    import sys
+    from zarr_amd.compression import Xz
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from bench import quant_chunk
+    arrays = [quant_chunk(i) for i in range(4)]
+    meta = ArrayMetadata.new([256 * 4, 256, 4], [256, 256, 4], "<f4", Xz(6))
+    st, outs = encode_batch(meta, arrays)
+    assert (st == 0).all()
+    tot = sum(a.nbytes for a in arrays)
+    ours = sum(len(s) for s in outs)
+    ref = sum(len(lzma.compress(a.tobytes(), format=lzma.FORMAT_XZ, check=lzma.CHECK_CRC64, preset=6))
+              for a in arrays)
+    for a, s in zip(arrays, outs):
+        check_xz_stream(s, a.tobytes(), 6)
+    assert tot / ours >= 6.66 and tot / ours >= 0.97 * tot / ref, (tot / ours, tot / ref)
+
+
 # ---- Bzip2 (bzip.rs:36-45: bzip2-rs BzEncoder = libbz2 BZ2_bzCompressInit(block_size)) ----
 def check_bz2_stream(stream: bytes, content: bytes, level: int):
     """A single bzip2 stream for this level that libbz2 (Python bz2 = the
