@@ -40,6 +40,10 @@ struct XzHostIO {
         pos += len;
     }
     void finish() {}
+    void apply_delta(uint64_t a, uint64_t b, uint32_t dist) {
+        for (uint64_t i = a; i < b; i++)
+            if (i >= a + dist) dst[i] = (uint8_t)(dst[i] + dst[i - dist]);
+    }
     uint64_t check(uint32_t id, uint64_t a, uint64_t b) const {
         if (id == 4) {
             uint64_t c = ~0ull;

@@ -83,12 +83,47 @@ def test_xz_corruption_sweep():
             check_many("xz", streams, "u1", D)
 
 
+@pytest.mark.parametrize("dist", [1, 2, 4, 7, 64, 256])
+def test_xz_delta_filter(dist):
+    """delta + LZMA2 chains (liblzma's delta decoder after LZMA2, history zero
+    at the block start): whole and partial reads, CRC32/CRC64/no check, and a
+    corruption sweep, against the oracle's liblzma."""
+    rng = np.random.default_rng(dist)
+    for k, payload in enumerate([rw(200001, seed=dist).tobytes(),
+                                 (np.arange(150000) * 3 % 256).astype(np.uint8).tobytes(),
+                                 rng.integers(0, 256, 30000, dtype=np.uint8).tobytes(), b"\x05"]):
+        s = lzma.compress(payload, format=lzma.FORMAT_XZ,
+                          check=(lzma.CHECK_CRC64, lzma.CHECK_CRC32, lzma.CHECK_NONE)[k % 3],
+                          filters=[{"id": lzma.FILTER_DELTA, "dist": dist}, {"id": lzma.FILTER_LZMA2, "preset": 6}])
+        for D in sorted({len(payload), max(1, len(payload) // 3), len(payload) + 5}):
+            check("xz", s, "u1", D)
+    payload = rw(40000, seed=3).tobytes()
+    s = lzma.compress(payload, format=lzma.FORMAT_XZ, filters=[{"id": lzma.FILTER_DELTA, "dist": dist},
+                                                               {"id": lzma.FILTER_LZMA2}])
+    streams = [s[:int(t)] for t in rng.integers(0, len(s), 32)]
+    for _ in range(96):
+        b = bytearray(s)
+        b[int(rng.integers(0, len(b)))] ^= int(rng.integers(1, 256))
+        streams.append(bytes(b))
+    check_many("xz", streams, "u1", len(payload))
+
+
+def test_xz_delta_filter_dtypes():
+    """A delta filter over multi-byte elements ('>' byte order applied after
+    the filter)."""
+    for dt, dist in ((">i2", 2), ("<f4", 4), (">u8", 8)):
+        v = (np.cumsum(np.random.default_rng(4).integers(-3, 4, 50000)) % 1000).astype(dt)
+        s = lzma.compress(v.tobytes(), format=lzma.FORMAT_XZ,
+                          filters=[{"id": lzma.FILTER_DELTA, "dist": dist}, {"id": lzma.FILTER_LZMA2}])
+        check("xz", s, dt, v.nbytes)
+
+
 def test_xz_unsupported_filter_chain_fails_loudly():
     from zarr_amd import ArrayMetadata, DefaultChunk, NativeUnavailable
     from zarr_amd.compression import Xz
     payload = rw(5000).tobytes()
     s = lzma.compress(payload, format=lzma.FORMAT_XZ,
-                      filters=[{"id": lzma.FILTER_DELTA, "dist": 2}, {"id": lzma.FILTER_LZMA2}])
+                      filters=[{"id": lzma.FILTER_X86}, {"id": lzma.FILTER_LZMA2}])
     meta = ArrayMetadata.new([len(payload)], [len(payload)], "u1", Xz(6))
     with pytest.raises(NativeUnavailable):
         DefaultChunk.read_chunk(s, meta, [0], np.uint8)

@@ -81,6 +81,26 @@ def test_xz_core_fuzz_vs_liblzma(seed):
             same(bytes(b), Ds[int(rng.integers(0, 3))])
 
 
+@pytest.mark.parametrize("dist", [1, 2, 3, 4, 8, 100, 256])
+def test_xz_core_delta_filter_vs_liblzma(dist):
+    """delta + LZMA2 chains: the core's block-end delta decode (and the one at
+    an early stop) against liblzma, whole / partial / overlong reads, and
+    corruptions."""
+    rng = np.random.default_rng(dist)
+    for k in range(4):
+        raw = _data(rng, k, int(rng.choice([1, 5, 300, 40000, 120000])))
+        s = lzma.compress(raw, format=lzma.FORMAT_XZ, check=[lzma.CHECK_CRC64, lzma.CHECK_CRC32][k % 2],
+                          filters=[{"id": lzma.FILTER_DELTA, "dist": dist}, {"id": lzma.FILTER_LZMA2, "preset": 6}])
+        for D in (len(raw), max(1, len(raw) // 3), len(raw) + 1):
+            same(s, D)
+        for t in rng.integers(0, len(s), 4):
+            same(s[:int(t)], len(raw))
+        for _ in range(20):
+            b = bytearray(s)
+            b[int(rng.integers(0, len(b)))] ^= int(rng.integers(1, 256))
+            same(bytes(b), len(raw))
+
+
 def test_xz_core_reference_vectors():
     """doc-spec vector (xz.rs:52-75) and the oracle's xz2-style encodes."""
     from golden_util import doc_spec

@@ -122,6 +122,36 @@ struct XzDevIO {
     __device__ __forceinline__ void finish() {
         if (gfl != pos) flush(pos);
     }
+    // delta filter decode of dst[a, b) in place (out[i] += out[i - dist]),
+    // wave-parallel: rows of `dist` bytes, 64 rows per step, one wave scan
+    // per column with the column's running sum carried in LDS (the model's
+    // probabilities are free between blocks and after the last one)
+    __device__ void apply_delta(u64 a, u64 b, u32 dist) {
+        for (u32 c = lane; c < dist; c += 64) probs[c] = 0;
+        __syncthreads();
+        const u64 len = b > a ? b - a : 0;
+        const u64 rows = (len + dist - 1) / dist;
+        for (u64 r0 = 0; r0 < rows; r0 += 64) {
+            const u64 r = r0 + (u64)lane;
+            for (u32 c = 0; c < dist; c++) {
+                const u64 i = a + r * dist + c;
+                const bool in = r < rows && i < b;
+                u32 x = in ? (u32)dst[i] : 0u;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const u32 y = (u32)__shfl_up((int)x, o, 64);
+                    if (lane >= o) x += y;
+                }
+                x += (u32)probs[c];
+                if (in) dst[i] = (u8)x;
+                const u32 carry = (u32)__builtin_amdgcn_readlane((int)x, 63) & 0xFF;
+                __syncthreads();
+                if (lane == 0) probs[c] = (u16)carry;
+                __syncthreads();
+            }
+        }
+        __threadfence_block();
+    }
     __device__ __forceinline__ u64 check(u32 id, u64 a, u64 b) {
         if (id == 4) return wave_crc<u64, CRC64_POLY>((const u8*)dst, a, b);
         return (u64)wave_crc<u32, CRC32_POLY>((const u8*)dst, a, b);

@@ -26,8 +26,8 @@
 // validating headers/sizes/checks up to that window's end and stops there
 // with OK.  Truncation before D bytes is UNEXPECTED_EOF.
 //
-// Not restated: filter chains other than a single LZMA2 filter (delta/BCJ;
-// liblzma accepts them, the kernel reports UNSUPPORTED), and the SHA-256
+// Not restated: filter chains other than a single LZMA2 filter or delta +
+// LZMA2 (BCJ, LZMA1; liblzma accepts them, the kernel reports UNSUPPORTED), and the SHA-256
 // check (the block check is skipped for check ID 10, as for the IDs liblzma
 // does not know).  xz2's XzEncoder writes a single LZMA2 filter with CRC64.
 #pragma once
@@ -431,8 +431,31 @@ out:
 //   void copy_in(u64 ip, u32 len);       append input bytes [ip, ip+len)
 //   u64 check(u32 id, u64 a, u64 b);     CRC32 (id 1) / CRC64 (id 4) of out[a,b)
 //   void finish();                       make all output visible in dst
+//   void apply_delta(u64 a, u64 b, u32 dist);  delta filter decode of out[a,b) in place
+// A block whose chain is delta + LZMA2 (liblzma's delta decoder passes the
+// LZMA2 output through, then adds the byte `dist` back: out[i] += out[i-dist],
+// history zero at the block start) is delta-decoded when it ends (before its
+// check, which covers the filtered bytes) or, if decoding stops inside it, by
+// xz_decode's wrapper.  LZMA2 matches read the unfiltered dictionary, which a
+// block never shares with the next (its first chunk resets the dictionary).
+struct DeltaPending {
+    u64 start;
+    u32 dist;  // 0: none
+};
+template <class IO>
+ZX_INL int xz_decode_blocks(IO& io, DeltaPending& dp);
 template <class IO>
 ZX_INL int xz_decode(IO& io) {
+    DeltaPending dp = {0, 0};
+    const int r = xz_decode_blocks(io, dp);
+    if (dp.dist) {
+        io.finish();
+        io.apply_delta(dp.start, io.pos, dp.dist);
+    }
+    return r;
+}
+template <class IO>
+ZX_INL int xz_decode_blocks(IO& io, DeltaPending& dp) {
     const u64 n = io.n;
     const u64 D = io.D;
     u64 ip = 0;       // input position
@@ -514,7 +537,7 @@ ZX_INL int xz_decode(IO& io) {
         }
         const u32 nfilt = (bflags & 3) + 1;
         u64 fid[4];
-        u32 dict_prop = 0;
+        u32 dict_prop = 0, delta_dist = 0;
         bool unsupported_chain = false;
         for (u32 f = 0; f < nfilt; f++) {
             u64 id = 0, psz = 0;
@@ -528,9 +551,10 @@ ZX_INL int xz_decode(IO& io) {
                 if (psz != 1) return ST_INVALID;
                 dict_prop = io.in(hp);
                 if (dict_prop > 40) return ST_INVALID;
-            } else if (id == 0x03) {  // delta
+            } else if (id == 0x03) {  // delta: distance = property + 1
                 if (psz != 1) return ST_INVALID;
-                unsupported_chain = true;
+                delta_dist = io.in(hp) + 1;
+                if (f != 0 || nfilt != 2) unsupported_chain = true;  // only delta + LZMA2
             } else if (id >= 0x04 && id <= 0x09) {  // BCJ filters
                 if (psz != 0 && psz != 4) return ST_INVALID;
                 unsupported_chain = true;
@@ -554,6 +578,7 @@ ZX_INL int xz_decode(IO& io) {
         ip = h0 + hsize;
         const u64 cstart = ip;             // block compressed data start
         const u64 ustart = io.pos;         // block uncompressed data start
+        if (delta_dist) { dp.start = ustart; dp.dist = delta_dist; }
         const u64 climit = (dec_csize != VLI_UNKNOWN) ? dec_csize
                                                        : (VLI_MAX & ~3ull) - hsize - csz_check;
         const u64 c_end = (climit > n) ? ~0ull : cstart + climit;  // compressed bytes < c_end
@@ -674,6 +699,11 @@ ZX_INL int xz_decode(IO& io) {
             }
         }
         // ---- block end (block_decoder.c SEQ_CODE -> PADDING -> CHECK) ----
+        if (dp.dist) {  // the delta filter's output is what the check covers
+            io.finish();
+            io.apply_delta(dp.start, io.pos, dp.dist);
+            dp.dist = 0;
+        }
         const u64 actual_c = ip - cstart;
         const u64 actual_u = io.pos - ustart;
         if (dec_csize != VLI_UNKNOWN && actual_c != dec_csize) return ST_INVALID;
