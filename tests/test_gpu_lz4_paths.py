@@ -97,3 +97,37 @@ def test_decoder_frame_variants(frame, flags):
             assert ost == st[i], (frame, D, i)
             if ost == 0:
                 assert bytes(out[i]) == ref, (frame, D, i)
+
+
+def test_side_by_side_batch_agrees():
+    """4 096 chunks = 65 536 blocks: the default runs the lane and the wave
+    decoders side by side on two streams (lanes for the first 55 % of the
+    chunks); statuses and bytes must equal the lane decoder's alone, valid and
+    corrupted frames alike."""
+    import torch
+    D = 1 << 20
+    pays = _payloads()
+    streams = [zref.encode(zref.LZ4, 65536, np.frombuffer(p, np.uint8))[1] for p in pays]
+    rng = np.random.default_rng(9)
+    while len(streams) < 64:
+        b = bytearray(streams[int(rng.integers(0, 4))])
+        b[int(rng.integers(7, len(b)))] ^= int(rng.integers(1, 256))
+        streams.append(bytes(b))
+    meta = ArrayMetadata.new([D * 4096], [D], "u1", Lz4(65536))
+    packed = PackedStreams(streams, D, "cuda:0", slot_copies=64)
+    assert packed.n == 4096
+    codec = BatchCodec(0)
+    codec.decode(meta, packed, flags=FLAG_LANE)
+    torch.cuda.synchronize()
+    st_lane, out_lane = packed.status.clone(), packed.dst.clone()
+    packed.dst.zero_()
+    codec.decode(meta, packed, flags=0)
+    torch.cuda.synchronize()
+    assert torch.equal(packed.status, st_lane)
+    ok = (st_lane == 0).view(-1, 1)
+    assert torch.equal(packed.dst.view(4096, -1) * ok, out_lane.view(4096, -1) * ok)
+    del out_lane
+    for i in range(4):  # the valid payloads, wherever their copies landed
+        rows = [g for g in range(4096) if g % 64 == i][:8]
+        for g in rows:
+            assert bytes(packed.dst.view(4096, -1)[g].cpu().numpy()) == pays[i]

@@ -16,9 +16,10 @@ streams = [lz4rs_frame(v.tobytes()) for v in vals]
 meta = ArrayMetadata.new([128, 64, 64], [128, 64, 64], "<i2", Lz4(65536))
 ref = torch.from_numpy(np.stack([v.view(np.uint8) for v in vals])).to("cuda:0")
 codec = BatchCodec(0)
+paths = os.environ.get("LZ4_PATHS", "default,lane,wave").split(",")
 for n in [int(x) for x in sys.argv[1:]] or [8192]:
     packed = PackedStreams(streams, 1 << 20, "cuda:0", slot_copies=n // pool)
-    for tag, fl in (("default", 0), ("lane", 0x1000), ("wave", 0x800)):
+    for tag, fl in [(t, {"default": 0, "lane": 0x1000, "wave": 0x800}[t]) for t in paths]:
         packed.dst.zero_()
         codec.decode(meta, packed, flags=fl)
         torch.cuda.synchronize()

@@ -132,7 +132,20 @@ namespace {
 std::mutex g_dev_mu;
 std::map<int, uint32_t> g_dev_cus;
 std::map<std::pair<const void*, int>, hipError_t> g_lds_attr;
+std::map<int, hipStream_t> g_side;
 }  // namespace
+
+hipStream_t side_stream() {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::lock_guard<std::mutex> lk(g_dev_mu);
+    auto it = g_side.find(dev);
+    if (it != g_side.end()) return it->second;
+    hipStream_t st = nullptr;
+    if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) st = nullptr;
+    g_side[dev] = st;
+    return st;
+}
 
 uint32_t device_cu_count() {
     int dev = 0;

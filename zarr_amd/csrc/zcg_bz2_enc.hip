@@ -459,6 +459,165 @@ __global__ void bze_update(u32 n, u32 h2, const u64* __restrict__ keys, const u3
     flags[j] = (!(head && nhead) && h2 < len) ? 1 : 0;
 }
 
+
+// ---- 4b. small groups sorted in LDS --------------------------------------------------
+// After the first (4-byte) sort, a workgroup takes the groups whose heads lie
+// in its tile of BZE_LC SA positions (a group may run past the tile; one
+// larger than BZE_LN stays for the global rounds) and refines them in LDS:
+// 8 more bytes of each unresolved rotation per round (cyclic within its
+// block), a bitonic sort by (tie run, bytes), new tie runs — up to
+// BZE_LROUNDS rounds.  Resolved positions get their final SA slot and rank;
+// rotations still tied afterwards keep their run head as rank and stay
+// flagged for the global prefix-doubling rounds (whose ranks only need to be
+// at least 4-byte accurate, which refined ranks are).  A tie that reaches
+// the block length is an equal rotation: any order decodes the same.
+constexpr u32 BZE_LC = 2048;
+constexpr u32 BZE_LN = 2 * BZE_LC;
+constexpr u32 BZE_LROUNDS = 8;
+
+__device__ __forceinline__ u64 bze_key8(const u8* __restrict__ text, u32 s, u32 len, u32 loc) {
+    u64 v = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        v = (v << 8) | text[s + loc];
+        loc = (loc + 1 == len) ? 0u : loc + 1;
+    }
+    return v;
+}
+
+__global__ __launch_bounds__(BZE_T) void bze_lds_sort(u32 T, const u8* __restrict__ text,
+                                                      const u32* __restrict__ blkof, const BzeBlk* __restrict__ gb,
+                                                      const u32* __restrict__ headpos, u32* __restrict__ sa,
+                                                      u32* __restrict__ rank, u8* __restrict__ flags) {
+    __shared__ u64 K[BZE_LN];
+    __shared__ u32 R[BZE_LN];
+    __shared__ u32 P[BZE_LN];
+    __shared__ u32 part[BZE_T];
+    __shared__ u32 s_a, s_last, s_b, s_tied;
+    const u32 tid = threadIdx.x;
+    const u32 t0 = blockIdx.x * BZE_LC;
+    const u32 t1 = (T - t0) < BZE_LC ? T : t0 + BZE_LC;
+    if (tid == 0) { s_a = 0xFFFFFFFFu; s_last = 0; s_b = 0xFFFFFFFFu; }
+    __syncthreads();
+    for (u32 p = t0 + tid; p < t1; p += BZE_T)
+        if (headpos[p] == p) { atomicMin(&s_a, p); atomicMax(&s_last, p); }
+    __syncthreads();
+    const u32 a = s_a;
+    if (a == 0xFFFFFFFFu) return;  // inside a group that started before the tile
+    {
+        const u32 lim = (T - a) < BZE_LN ? T : a + BZE_LN;  // b may be at most a + BZE_LN
+        for (u32 p = t1 + tid; p <= lim; p += BZE_T)
+            if (p == T || headpos[p] == p) atomicMin(&s_b, p);
+    }
+    __syncthreads();
+    const u32 b = s_b != 0xFFFFFFFFu ? s_b : s_last;  // else the last group is too large: leave it
+    const u32 n = b - a;
+    if (n < 2) return;
+    u32 N = 2;
+    while (N < n) N <<= 1;
+    for (u32 k = tid; k < N; k += BZE_T) {
+        if (k < n) {
+            const u32 p = a + k, pos = sa[p];
+            P[k] = pos;
+            if (flags[p]) {
+                const u32 bi = blkof[pos], st = gb[bi].start, len = gb[bi].len;
+                R[k] = headpos[p] - a;
+                K[k] = bze_key8(text, st, len, (pos - st + 4) % len);
+            } else {
+                R[k] = k;
+                K[k] = 0;
+            }
+        } else {
+            R[k] = 0xFFFFFFFFu;
+            K[k] = ~0ull;
+            P[k] = 0;
+        }
+    }
+    __syncthreads();
+    u32 depth = 4;
+    for (u32 round = 0; round < BZE_LROUNDS; round++) {
+        // bitonic sort by (R, K)
+        for (u32 kk = 2; kk <= N; kk <<= 1)
+            for (u32 j = kk >> 1; j > 0; j >>= 1) {
+                for (u32 i = tid; i < N; i += BZE_T) {
+                    const u32 x = i ^ j;
+                    if (x > i) {
+                        const bool up = (i & kk) == 0;
+                        const bool gt = R[i] > R[x] || (R[i] == R[x] && K[i] > K[x]);
+                        const bool lt = R[i] < R[x] || (R[i] == R[x] && K[i] < K[x]);
+                        if (up ? gt : lt) {
+                            const u32 r = R[i]; R[i] = R[x]; R[x] = r;
+                            const u64 q = K[i]; K[i] = K[x]; K[x] = q;
+                            const u32 w = P[i]; P[i] = P[x]; P[x] = w;
+                        }
+                    }
+                }
+                __syncthreads();
+            }
+        // tie runs: head index by a block max-scan over 16 elements per thread
+        const u32 per = (N + BZE_T - 1) / BZE_T;
+        const u32 k0 = tid * per;
+        u32 m = 0;
+        for (u32 q = 0; q < per; q++) {
+            const u32 k = k0 + q;
+            if (k < n && (k == 0 || R[k] != R[k - 1] || K[k] != K[k - 1])) m = k;
+        }
+        part[tid] = m;
+        __syncthreads();
+        u32 carry = 0;
+        for (u32 t = 0; t < tid; t++) carry = part[t] > carry ? part[t] : carry;
+        __syncthreads();
+        if (tid == 0) s_tied = 0;
+        __syncthreads();
+        // new run id = run head index; tied = the run has >= 2 members and
+        // its rotations are not yet compared over their whole length
+        // (run heads and tie bits packed in one register per 16 elements)
+        u32 hd = carry, tiebits = 0;
+        u32 hdq[16];
+#pragma unroll
+        for (u32 q = 0; q < 16; q++) {
+            const u32 k = k0 + q;
+            if (q < per && k < n) {
+                if (k == 0 || R[k] != R[k - 1] || K[k] != K[k - 1]) hd = k;
+                const bool next_same = k + 1 < n && R[k + 1] == R[k] && K[k + 1] == K[k];
+                if ((hd != k || next_same) && depth + 8 < gb[blkof[P[k]]].len) tiebits |= 1u << q;
+            }
+            hdq[q] = hd;
+        }
+        __syncthreads();
+#pragma unroll
+        for (u32 q = 0; q < 16; q++) {
+            const u32 k = k0 + q;
+            if (q >= per || k >= n) continue;
+            const u32 heads_q = hdq[q];
+            if ((tiebits >> q) & 1u) {
+                const u32 pos = P[k], bi = blkof[pos], st = gb[bi].start, len = gb[bi].len;
+                R[k] = heads_q;
+                K[k] = bze_key8(text, st, len, (pos - st + depth + 8) % len);
+                s_tied = 1;
+            } else {
+                R[k] = k;
+                K[k] = 0;
+            }
+        }
+        __syncthreads();
+        depth += 8;
+        if (!s_tied) break;
+        __syncthreads();
+    }
+    // write back: SA order, ranks (run heads for ties), flags
+    for (u32 k = tid; k < n; k += BZE_T) {
+        const u32 p = a + k, pos = P[k];
+        const bool was = flags[p] != 0;  // (flagged groups keep their SA ranges)
+        sa[p] = pos;
+        if (was) {
+            const bool t = R[k] != k || (k + 1 < n && R[k + 1] == k);
+            rank[pos] = a + R[k];
+            flags[p] = t ? 1 : 0;
+        }
+    }
+}
+
 // ---- 5. per-block: BWT column, MTF/RLE2, Huffman tables, bit stream -------------------
 struct BzeBlkShared {
     u32 inuse[8];
@@ -1057,8 +1216,10 @@ hipError_t launch_bzip2_encode(const zcg_array* a, const zcg_chunk* d_chunks, ui
             if ((e = hipcub::DeviceScan::InclusiveScan(cub, cb, sA, sB, MaxU32(), (int)T, s)) != hipSuccess) return e;
             hipLaunchKernelGGL(bze_rank0, dim3((T + TB - 1) / TB), dim3(TB), 0, s, T, dk.Current(), dv.Current(), sB,
                                blkof, gb, rank, sa, flags);
+            hipLaunchKernelGGL(bze_lds_sort, dim3((T + BZE_LC - 1) / BZE_LC), dim3(BZE_T), 0, s, T, text, blkof, gb, sB,
+                               sa, rank, flags);
             cb = y.cub_bytes;
-            if ((e = hipcub::DeviceSelect::Flagged(cub, cb, dv.Current(), flags, U, d_nsel, (int)T, s)) != hipSuccess)
+            if ((e = hipcub::DeviceSelect::Flagged(cub, cb, sa, flags, U, d_nsel, (int)T, s)) != hipSuccess)
                 return e;
             u32 cntU = 0;
             if ((e = hipMemcpyAsync(&cntU, d_nsel, 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;

@@ -253,6 +253,9 @@ const char* cfg_region();
 // device's CU count, and a kernel's dynamic-LDS limit raised to `bytes`.
 uint32_t device_cu_count();
 hipError_t lds_attr_once(const void* kernel, int bytes);
+// a second stream of the current device (created once; nullptr if that failed):
+// kernels of one call that may run side by side are forked onto it
+hipStream_t side_stream();
 hipError_t launch_raw(const zcg_array* a, const zcg_chunk* d_chunks, uint32_t n, int32_t* d_status,
                       uint64_t* d_out_len, int encode, hipStream_t s);
 hipError_t launch_lz4_decode(const zcg_array* a, const zcg_chunk* d_chunks, uint32_t n,

@@ -753,6 +753,18 @@ constexpr u32 LZ_LPC = LZ_LRB / 2;  // flush granularity = longest piece written
 constexpr u32 LZ_LRM = LZ_LRB - 1;
 constexpr u32 LZ_LWG = 64;          // lanes (blocks) per workgroup
 constexpr u64 LZ_LANE_MIN_BLOCKS = 131072;
+// Between the two (measured at 8 192 C4 chunks = 131 072 blocks: lanes 50.6 ms,
+// waves 54.3 ms, 55 % lanes + 45 % waves side by side 45.0 ms) both kernels run
+// at once on two streams; from 262 144 blocks up the lanes alone are faster.
+#ifndef LZ_CORUN_PCT
+#define LZ_CORUN_PCT 55  // percent of the chunks decoded by lanes in a side-by-side batch
+#endif
+#ifndef LZ_CORUN_LO
+#define LZ_CORUN_LO 65536
+#endif
+#ifndef LZ_CORUN_HI
+#define LZ_CORUN_HI 262144
+#endif
 
 // The ring is written and read with byte-unaligned ds_write_b128 /
 // ds_read_b128 (gfx950 LDS runs in the unaligned alignment mode;
@@ -1111,14 +1123,41 @@ hipError_t launch_lz4_decode(const zcg_array* a, const zcg_chunk* d_chunks, uint
         // one lane per block needs ~16 waves per CU of blocks to hide its
         // latency; smaller batches run one wave per block
         const u32 fl = a->compression.flags;
+        const bool forced = (fl & (ZCG_FLAG_LZ4_WAVE_PER_BLOCK | ZCG_FLAG_LZ4_LANE_PER_BLOCK)) != 0;
+        const bool corun = !forced && waves >= LZ_CORUN_LO && waves < LZ_CORUN_HI;
         const bool wave = (fl & ZCG_FLAG_LZ4_WAVE_PER_BLOCK) ||
-                          (!(fl & ZCG_FLAG_LZ4_LANE_PER_BLOCK) && waves < LZ_LANE_MIN_BLOCKS);
-        if (wave)
+                          (!(fl & ZCG_FLAG_LZ4_LANE_PER_BLOCK) && !corun && waves < LZ_LANE_MIN_BLOCKS);
+        hipStream_t s2 = corun ? side_stream() : nullptr;
+        if (wave) {
             hipLaunchKernelGGL(lz4_blocks_kernel, dim3((u32)((waves + 3) / 4)), dim3(256), 0, s, d_chunks, n, D,
                                (u32)S, a->compression.flags, (const Lz4ChunkInfo*)info, slots);
-        else
+        } else if (s2) {
+            // lanes for the first chunks on `s`, waves for the rest on the side
+            // stream at the same time: the lane kernel is latency-bound and the
+            // wave kernel VALU-bound, so they share the CUs
+            const u32 n1 = (u32)((u64)n * LZ_CORUN_PCT / 100);
+            hipEvent_t fork = nullptr, join = nullptr;
+            hipError_t e = hipEventCreateWithFlags(&fork, hipEventDisableTiming);
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&join, hipEventDisableTiming);
+            if (e == hipSuccess) e = hipEventRecord(fork, s);
+            if (e == hipSuccess) e = hipStreamWaitEvent(s2, fork, 0);
+            if (e != hipSuccess) return e;
+            const u64 w2 = (u64)(n - n1) * S;
+            hipLaunchKernelGGL(lz4_blocks_kernel, dim3((u32)((w2 + 3) / 4)), dim3(256), 0, s2, d_chunks + n1, n - n1,
+                               D, (u32)S, a->compression.flags, (const Lz4ChunkInfo*)info + n1, slots + (u64)n1 * S);
+            const u64 w1 = (u64)n1 * S;
+            if (w1)
+                hipLaunchKernelGGL(lz4_lanes_kernel, dim3((u32)((w1 + LZ_LWG - 1) / LZ_LWG)), dim3(LZ_LWG), 0, s,
+                                   d_chunks, n1, D, (u32)S, a->compression.flags, (const Lz4ChunkInfo*)info, slots);
+            e = hipEventRecord(join, s2);
+            if (e == hipSuccess) e = hipStreamWaitEvent(s, join, 0);
+            (void)hipEventDestroy(fork);
+            (void)hipEventDestroy(join);
+            if (e != hipSuccess) return e;
+        } else {
             hipLaunchKernelGGL(lz4_lanes_kernel, dim3((u32)((waves + LZ_LWG - 1) / LZ_LWG)), dim3(LZ_LWG), 0, s,
                                d_chunks, n, D, (u32)S, a->compression.flags, (const Lz4ChunkInfo*)info, slots);
+        }
     }
     hipLaunchKernelGGL(lz4_finish_kernel, dim3(n), dim3(64), 0, s, d_chunks, n, D, t, a->compression.flags,
                        (u32)S, (const Lz4ChunkInfo*)info, (const Lz4Slot*)slots, d_status);

@@ -44,6 +44,10 @@ constexpr u32 XO_NICE = 64;        // stop walking at a match this long
 constexpr u32 XO_W2 = 64;          // 2-byte repeat search distance
 constexpr u32 XO_LENS = 8;         // lengths 2..XO_LENS of a range, then its last three
 constexpr u32 XO_MAXLEN = 273;
+#ifndef XO_HIST_BYTES
+#define XO_HIST_BYTES 0
+#endif
+constexpr u32 XO_HIST = XO_HIST_BYTES;  // bytes before a window kept in LDS (rep / matched-literal reads)
 constexpr u32 XO_PROBS = 1846 + 0x300;  // lc = lp = 0: one literal coder
 constexpr u32 XO_PROPS = (2 * 5 + 0) * 9 + 0;
 constexpr u64 XO_SEGCAP = XO_SEG + XO_SEG / 16 + 4096;  // a segment's LZMA2 chunks (bound)
@@ -52,6 +56,10 @@ constexpr u64 XO_SUB_BYTES = 128ull << 20;
 constexpr u64 XO_SUPER_BYTES = 1ull << 30;
 constexpr u32 XO_DMAX_LG = 23;  // candidate distances < 2^23 (they pack in 23 bits)
 constexpr u32 ARC_REP = 2, ARC_MATCH = 1100;  // arc ids: 0 literal, 1 short rep, 2 + r*274 + len, 1100 + len
+#ifndef XO_PROF
+#define XO_PROF 0  // 1 (A/B builds only): cycle and event counters, read by zcg__debug_xz_opt_counters
+#endif
+__device__ unsigned long long g_xo_prof[16];  // plan cycles, code cycles, nodes, symbols, windows, total cycles
 
 // -log2((i*16+8)/2048) in 1/16 bit, rounded (the price of a bit of probability p is c_xo_price[p >> 4])
 __constant__ u8 c_xo_price[128] = {
@@ -71,6 +79,13 @@ __device__ __forceinline__ u32 slot_of(u32 d) {
     return 2 * lg + ((d >> (lg - 1)) & 1);
 }
 __device__ __forceinline__ u32 ufl(u32 v) { return (u32)__builtin_amdgcn_readfirstlane((int)v); }
+// wave-local ordering point for LDS (and the compiler): one wave per
+// workgroup, whose LDS operations are performed in issue order
+__device__ __forceinline__ void wsync_lds() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 
 // ---------------------------------------------------------------- candidates
 __global__ void xo_cands(const zcg_chunk* __restrict__ chunks, u32 c0, u64 D, u64 tot, DType t, u64 dmax,
@@ -145,16 +160,118 @@ __global__ void xo_cands(const zcg_chunk* __restrict__ chunks, u32 c0, u64 D, u6
     c[2] = n == 3 ? k2 : 0u;
 }
 
+
+// Range-code `cnt` (<= N) bits whose probabilities sit at distinct indices:
+// every probability is loaded before the first bit is coded, so a symbol
+// costs one LDS round trip instead of one per bit.
+template <int N>
+__device__ __forceinline__ void xo_code(XeEnc& e, const u32 (&idx)[N], const u32 (&bits)[N], u32 cnt) {
+    u32 pr[N];
+#pragma unroll
+    for (int j = 0; j < N; j++) pr[j] = (u32)j < cnt ? (u32)e.probs[idx[j]] : 0u;
+#pragma unroll
+    for (int j = 0; j < N; j++) {
+        if ((u32)j >= cnt) break;
+        const u32 p = pr[j], bound = (e.range >> 11) * p;
+        u32 np;
+        if (bits[j] == 0) {
+            e.range = bound;
+            np = p + ((2048 - p) >> 5);
+        } else {
+            e.low += bound;
+            e.range -= bound;
+            np = p - (p >> 5);
+        }
+        e.probs[idx[j]] = (u16)np;
+        while (e.range < (1u << 24)) {
+            e.range <<= 8;
+            e.shift_low();
+        }
+    }
+}
+// an nb-bit tree symbol (MSB first) / reverse tree symbol (LSB first)
+template <int N>
+__device__ __forceinline__ void xo_tree(XeEnc& e, u32 base, u32 nb, u32 v) {
+    u32 idx[N], bits[N];
+#pragma unroll
+    for (int k = 0; k < N; k++) {
+        bits[k] = (u32)k < nb ? (v >> (nb - 1 - k)) & 1 : 0u;
+        idx[k] = base + ((1u << k) | ((u32)k < nb ? v >> (nb - k) : 0u));
+    }
+    xo_code<N>(e, idx, bits, nb);
+}
+template <int N>
+__device__ __forceinline__ void xo_rtree(XeEnc& e, u32 base, u32 nb, u32 v) {
+    u32 idx[N], bits[N], m = 1;
+#pragma unroll
+    for (int k = 0; k < N; k++) {
+        bits[k] = (v >> k) & 1;
+        idx[k] = base + m;
+        m = (m << 1) | bits[k];
+    }
+    xo_code<N>(e, idx, bits, nb);
+}
+__device__ __forceinline__ void xo_literal(XeEnc& e, u32 sym, bool matched, u32 mbyte) {
+    u32 idx[8], bits[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        bits[j] = (sym >> (7 - j)) & 1;
+        u32 x = E_LITERAL + ((1u << j) | (sym >> (8 - j)));
+        if (matched) {
+            const u32 off = (sym >> (8 - j)) == (mbyte >> (8 - j)) ? 0x100u : 0u;
+            x += off + (off ? ((mbyte >> (7 - j)) & 1) << 8 : 0u);
+        }
+        idx[j] = x;
+    }
+    xo_code<8>(e, idx, bits, 8);
+}
+__device__ __forceinline__ void xo_length(XeEnc& e, u32 lb, u32 l, u32 ps) {  // l = len - 2
+    u32 idx[10], bits[10], cnt;
+    if (l < 8) {
+        idx[0] = lb + EL_CHOICE; bits[0] = 0;
+        for (int k = 0; k < 3; k++) { bits[1 + k] = (l >> (2 - k)) & 1; idx[1 + k] = lb + EL_LOW + (ps << 3) + ((1u << k) | (l >> (3 - k))); }
+        cnt = 4;
+    } else if (l < 16) {
+        idx[0] = lb + EL_CHOICE; bits[0] = 1; idx[1] = lb + EL_CHOICE2; bits[1] = 0;
+        const u32 v = l - 8;
+        for (int k = 0; k < 3; k++) { bits[2 + k] = (v >> (2 - k)) & 1; idx[2 + k] = lb + EL_MID + (ps << 3) + ((1u << k) | (v >> (3 - k))); }
+        cnt = 5;
+    } else {
+        idx[0] = lb + EL_CHOICE; bits[0] = 1; idx[1] = lb + EL_CHOICE2; bits[1] = 1;
+        const u32 v = l - 16;
+        for (int k = 0; k < 8; k++) { bits[2 + k] = (v >> (7 - k)) & 1; idx[2 + k] = lb + EL_HIGH + ((1u << k) | (v >> (8 - k))); }
+        cnt = 10;
+    }
+    for (u32 k = cnt; k < 10; k++) { idx[k] = lb; bits[k] = 0; }
+    xo_code<10>(e, idx, bits, cnt);
+}
+__device__ __forceinline__ void xo_distance(XeEnc& e, u32 d, u32 len) {
+    const u32 lps = len - 2 < 3 ? len - 2 : 3, slot = slot_of(d);
+    xo_tree<6>(e, E_POS_SLOT + (lps << 6), 6, slot);
+    if (slot >= 4) {
+        const u32 nd = (slot >> 1) - 1, base = (2 | (slot & 1)) << nd, red = d - base;
+        if (slot < 14) {
+            xo_rtree<5>(e, E_SPEC_POS + base - slot - 1, nd, red);
+        } else {
+            e.direct(red >> 4, nd - 4);
+            xo_rtree<4>(e, E_ALIGN, 4, red & 15);
+        }
+    }
+}
+
 // ---------------------------------------------------------------- segments
 struct XoLds {
     u64 key[XO_WIN + 1];       // best (price << 20 | source << 11 | arc) of each window node
-    u32 nrep[XO_WIN + 1][4];   // reps of each node's best path
-    u32 wc[XO_WIN * XO_K];     // the window's candidates
-    u32 pth[XO_WIN];           // planned path, reversed: arc | len << 11
-    u32 pdist[XO_WIN];         //   and the match distance
+    union {
+        u32 nrep[XO_WIN + 1][4];  // planning: reps of each node's best path
+        struct {                  // coding: the planned path, reversed
+            u32 pth[XO_WIN];      //   arc | len << 11
+            u32 pdist[XO_WIN];    //   and the match distance
+        } path;
+    } nr;
     u16 probs[XO_PROBS];
     u8 nst[XO_WIN + 1];        // state of each node
-    u8 tile[XO_WIN];           // the window's bytes
+    u8 tile[XO_HIST + XO_WIN]; // the window's bytes and the XO_HIST before it
     u8 price[128];
 };
 
@@ -162,40 +279,58 @@ __device__ __forceinline__ u32 xo_pb(const XoLds& L, u32 i, u32 b) {
     const u32 p = L.probs[i];
     return L.price[(b ? 2048 - p : p) >> 4];
 }
-__device__ __forceinline__ u32 xo_ptree(const XoLds& L, u32 base, u32 nb, u32 v) {
-    u32 s = 0;
-    for (u32 k = 0; k < nb; k++) {
-        const u32 b = (v >> (nb - 1 - k)) & 1;
-        s += xo_pb(L, base + ((1u << k) | (v >> (nb - k))), b);
+// Price of a length code (l = len - 2, coder at lb, position state ps) and,
+// for a match, of distance d: every probability index is formed first (21
+// slots: choice, choice2, 8 tree levels; 6 slot levels, 5 reverse-tree
+// levels), then all probabilities are read, then all their prices, so the
+// arc costs two LDS round trips instead of two per tree level.
+__device__ __forceinline__ u32 xo_arc_price(const XoLds& L, u32 lb, u32 l, u32 ps, bool match, u32 d, u32 len) {
+    u32 idx[21], bit[21], use = 0;
+    idx[0] = lb + EL_CHOICE; bit[0] = l >= 8; use |= 1u;
+    idx[1] = lb + EL_CHOICE2; bit[1] = l >= 16; use |= (l >= 8 ? 1u : 0u) << 1;
+    const u32 tb = l < 8 ? EL_LOW + (ps << 3) : l < 16 ? EL_MID + (ps << 3) : EL_HIGH;
+    const u32 tv = l < 8 ? l : l < 16 ? l - 8 : l - 16, tn = l < 16 ? 3u : 8u;
+#pragma unroll
+    for (u32 k = 0; k < 8; k++) {
+        const bool u = k < tn;
+        bit[2 + k] = u ? (tv >> (tn - 1 - k)) & 1 : 0u;
+        idx[2 + k] = lb + tb + ((1u << k) | (u ? tv >> (tn - k) : 0u));
+        use |= (u ? 1u : 0u) << (2 + k);
     }
-    return s;
-}
-__device__ __forceinline__ u32 xo_prtree(const XoLds& L, u32 base, u32 nb, u32 v) {
-    u32 s = 0;
-    for (u32 k = 0; k < nb; k++) {
-        const u32 b = (v >> k) & 1;
-        // index after k bits: 1 followed by bits 0..k-1 in reverse order of arrival
+    u32 extra = 0;
+    {
+        const u32 lps = len - 2 < 3 ? len - 2 : 3, slot = slot_of(d);
+#pragma unroll
+        for (u32 k = 0; k < 6; k++) {
+            bit[10 + k] = (slot >> (5 - k)) & 1;
+            idx[10 + k] = E_POS_SLOT + (lps << 6) + ((1u << k) | (slot >> (6 - k)));
+            use |= (match ? 1u : 0u) << (10 + k);
+        }
+        u32 rb = 0, rn = 0, rv = 0;
+        if (match && slot >= 4) {
+            const u32 nd = (slot >> 1) - 1, base = (2 | (slot & 1)) << nd, red = d - base;
+            if (slot < 14) { rb = E_SPEC_POS + base - slot - 1; rn = nd; rv = red; }
+            else { rb = E_ALIGN; rn = 4; rv = red & 15; extra = (nd - 4) * 16; }
+        }
         u32 m = 1;
-        for (u32 j = 0; j < k; j++) m = (m << 1) | ((v >> j) & 1);
-        s += xo_pb(L, base + m, b);
+#pragma unroll
+        for (u32 k = 0; k < 5; k++) {
+            bit[16 + k] = (rv >> k) & 1;
+            idx[16 + k] = rb + m;
+            m = (m << 1) | bit[16 + k];
+            use |= (k < rn ? 1u : 0u) << (16 + k);
+        }
     }
-    return s;
-}
-__device__ __forceinline__ u32 xo_plen(const XoLds& L, u32 lb, u32 l, u32 ps) {
-    if (l < 8) return xo_pb(L, lb + EL_CHOICE, 0) + xo_ptree(L, lb + EL_LOW + (ps << 3), 3, l);
-    if (l < 16)
-        return xo_pb(L, lb + EL_CHOICE, 1) + xo_pb(L, lb + EL_CHOICE2, 0) + xo_ptree(L, lb + EL_MID + (ps << 3), 3, l - 8);
-    return xo_pb(L, lb + EL_CHOICE, 1) + xo_pb(L, lb + EL_CHOICE2, 1) + xo_ptree(L, lb + EL_HIGH, 8, l - 16);
-}
-__device__ __forceinline__ u32 xo_pdist(const XoLds& L, u32 d, u32 len) {
-    const u32 lps = len - 2 < 3 ? len - 2 : 3, slot = slot_of(d);
-    u32 s = xo_ptree(L, E_POS_SLOT + (lps << 6), 6, slot);
-    if (slot >= 4) {
-        const u32 nd = (slot >> 1) - 1, base = (2 | (slot & 1)) << nd, red = d - base;
-        if (slot < 14) s += xo_prtree(L, E_SPEC_POS + base - slot - 1, nd, red);
-        else s += (nd - 4) * 16 + xo_prtree(L, E_ALIGN, 4, red & 15);
+    u32 pr[21];
+#pragma unroll
+    for (u32 j = 0; j < 21; j++) pr[j] = (use >> j) & 1 ? (u32)L.probs[idx[j]] : 1024u;
+    u32 sum = extra;
+#pragma unroll
+    for (u32 j = 0; j < 21; j++) {
+        const u32 q = L.price[(bit[j] ? 2048 - pr[j] : pr[j]) >> 4];
+        sum += (use >> j) & 1 ? q : 0u;
     }
-    return s;
+    return sum;
 }
 
 // kept lengths of the range [a, Lr]: a..min(Lr, 8), then max(a, 9, Lr - 2)..Lr
@@ -211,12 +346,10 @@ __device__ __forceinline__ u32 xo_range_count(u32 a, u32 Lr, u32* c1, u32* hi0) 
 }
 
 // the distance of match arc `len` from node `src` (the first candidate whose clipped range holds it)
-__device__ __forceinline__ u32 xo_arc_dist(const XoLds& L, u32 src, u32 len, u32 room) {
-    for (u32 k = 0; k < XO_K; k++) {
-        const u32 c = L.wc[src * XO_K + k], Lk = c >> 23;
-        if (Lk && len <= (Lk < room ? Lk : room)) return c & 0x7FFFFFu;
-    }
-    return 0;
+__device__ __forceinline__ u32 xo_arc_dist(const u32* __restrict__ wc, u32 src, u32 len, u32 room) {
+    const u32 c0 = ufl(wc[src * XO_K]), c1 = ufl(wc[src * XO_K + 1]), c2 = ufl(wc[src * XO_K + 2]);
+    auto holds = [&](u32 c) { const u32 Lk = c >> 23; return Lk && len <= (Lk < room ? Lk : room); };
+    return (holds(c0) ? c0 : holds(c1) ? c1 : holds(c2) ? c2 : 0u) & 0x7FFFFFu;
 }
 
 __global__ __launch_bounds__(64) void xo_segment(const zcg_chunk* __restrict__ chunks, u32 c0, u64 D, DType t,
@@ -248,8 +381,12 @@ __global__ __launch_bounds__(64) void xo_segment(const zcg_chunk* __restrict__ c
     bool need_dict = k == 0, need_props = true, need_state = true;
     u32 state = 0, r0 = 0, r1 = 0, r2 = 0, r3 = 0;
     u64 p = s0;
-    auto sbyte = [&](u64 x, u64 wbase) -> u32 {  // serialised byte x (< the window end)
-        return x >= wbase ? (u32)L.tile[x - wbase] : e.sb(x);
+    u64 prof[5] = {0, 0, 0, 0, 0};
+    u64 prof2[6] = {0, 0, 0, 0, 0, 0};
+    const u64 tk0 = XO_PROF ? __builtin_readcyclecounter() : 0;
+    // serialised byte x (< the window end): from the tile when it is inside
+    auto sbyte = [&](u64 x, u64 wbase) -> u32 {
+        return x + XO_HIST >= wbase ? (u32)L.tile[x + XO_HIST - wbase] : e.sb(x);
     };
     while (p < s1) {
         // ---- one LZMA2 chunk ----
@@ -271,67 +408,104 @@ __global__ __launch_bounds__(64) void xo_segment(const zcg_chunk* __restrict__ c
         u64 wb = 0;     // the planned window's first position
         while (p < s1 && (e.pos - data0) + e.cache_size + 5 < XE_CMAX) {
             if (npath == 0) {
+                const u64 tp0 = XO_PROF ? __builtin_readcyclecounter() : 0;
                 // ================= plan a window [p, we) =================
                 const u64 we = (s1 - p) < XO_WIN ? s1 : p + XO_WIN;
                 const u32 W = (u32)(we - p);
                 wb = p;
                 __syncthreads();
                 for (u32 j = lane; j <= W; j += 64) L.key[j] = ~0ull;
-                for (u32 j = lane; j < W; j += 64) L.tile[j] = (u8)e.sb(p + j);
-                for (u32 j = lane; j < W * XO_K; j += 64) L.wc[j] = cbase[p * XO_K + j];
+                for (u32 j = lane; j < XO_HIST + W; j += 64)
+                    if (j + p >= XO_HIST) L.tile[j] = (u8)e.sb(p + j - XO_HIST);
+                const u32* __restrict__ wc = cbase + p * XO_K;  // the window's candidates (read-only)
                 __syncthreads();
                 if (lane == 0) {
                     L.key[0] = 0;
                     L.nst[0] = (u8)state;
-                    L.nrep[0][0] = r0; L.nrep[0][1] = r1; L.nrep[0][2] = r2; L.nrep[0][3] = r3;
+                    L.nr.nrep[0][0] = r0; L.nr.nrep[0][1] = r1; L.nr.nrep[0][2] = r2; L.nr.nrep[0][3] = r3;
                 }
                 __syncthreads();
-                for (u32 i = 0; i < W; i++) {
-                    const u64 a = L.key[i];
-                    const u32 alo = ufl((u32)a), ahi = ufl((u32)(a >> 32));
-                    u32 st, q0, q1, q2, q3;
-                    if (i == 0) {
-                        st = state; q0 = r0; q1 = r1; q2 = r2; q3 = r3;
-                    } else {
-                        const u32 src = (alo >> 11) & 511, arc = alo & 2047;
-                        const u32 bst = ufl(L.nst[src]);
-                        const u32 b0 = ufl(L.nrep[src][0]), b1 = ufl(L.nrep[src][1]), b2 = ufl(L.nrep[src][2]),
-                                  b3 = ufl(L.nrep[src][3]);
-                        if (arc == 0) { st = st_lit(bst); q0 = b0; q1 = b1; q2 = b2; q3 = b3; }
-                        else if (arc == 1) { st = st_short(bst); q0 = b0; q1 = b1; q2 = b2; q3 = b3; }
-                        else if (arc < ARC_MATCH) {
-                            const u32 r = (arc - ARC_REP) / 274;
-                            st = st_rep(bst);
-                            q0 = r == 0 ? b0 : r == 1 ? b1 : r == 2 ? b2 : b3;
-                            q1 = r == 0 ? b1 : b0;
-                            q2 = r <= 1 ? b2 : b1;
-                            q3 = r <= 2 ? b3 : b2;
-                        } else {
-                            st = st_match(bst);
-                            q0 = ufl(xo_arc_dist(L, src, arc - ARC_MATCH, W - src));
-                            q1 = b0; q2 = b1; q3 = b2;
+                // Nodes in order, software-pipelined by one: node t's literal and
+                // short-rep keys (its only arcs to t + 1) are resolved in registers,
+                // so node t + 1 is final before node t's longer arcs are priced;
+                // node t + 1's rep-byte loads are issued before that pricing and
+                // land while it runs.
+                u32 cst = state, cq0 = r0, cq1 = r1, cq2 = r2, cq3 = r3, cP = 0;
+                u32 i_sym = 0, i_w0 = 0, i_w1 = 0, i_w2 = 0, i_rb = 0, i_mine = 0;
+                bool i_valid = false;
+                auto issue = [&](u32 t, u32 q0_, u32 q1_, u32 q2_, u32 q3_) {
+                    const u64 at = p + t;
+                    const u32 room = W - t, mx = room < XO_MAXLEN ? room : XO_MAXLEN;
+                    const u32 r = (u32)lane >> 4, tb = (u32)lane & 15;
+                    const u32 rd = r == 0 ? q0_ : r == 1 ? q1_ : r == 2 ? q2_ : q3_;
+                    i_sym = L.tile[XO_HIST + t];
+                    i_w0 = wc[t * XO_K];
+                    i_w1 = wc[t * XO_K + 1];
+                    i_w2 = wc[t * XO_K + 2];
+                    i_valid = at > rd && tb < mx;
+                    i_rb = i_valid ? sbyte(at - rd - 1 + tb, p) : 0u;
+                    i_mine = tb < mx ? (u32)L.tile[XO_HIST + t + tb] : 0u;
+                };
+                // The window's flag-bit prices and plain-literal prices, read
+                // per node with v_readlane (no LDS round trip): lane st*4+ps
+                // holds is_match / is_rep0_long of (state, pos state), lane st
+                // the is_rep / rep_g0-2 pairs, lane l the literals l + 64 k.
+                u32 pIM0, pIM1, pRL0, pRL1, pIR0, pIR1, pG00, pG01, pG10, pG11, pG20, pG21, pL0, pL1, pL2, pL3;
+                {
+                    const u32 sp = (u32)lane < 48 ? (u32)lane : 0u, st4 = sp >> 2, ps4 = sp & 3;
+                    pIM0 = xo_pb(L, E_IS_MATCH + (st4 << 4) + ps4, 0);
+                    pIM1 = xo_pb(L, E_IS_MATCH + (st4 << 4) + ps4, 1);
+                    pRL0 = xo_pb(L, E_IS_REP0_LONG + (st4 << 4) + ps4, 0);
+                    pRL1 = xo_pb(L, E_IS_REP0_LONG + (st4 << 4) + ps4, 1);
+                    const u32 s1 = (u32)lane < 12 ? (u32)lane : 0u;
+                    pIR0 = xo_pb(L, E_IS_REP + s1, 0);
+                    pIR1 = xo_pb(L, E_IS_REP + s1, 1);
+                    pG00 = xo_pb(L, E_IS_REP_G0 + s1, 0);
+                    pG01 = xo_pb(L, E_IS_REP_G0 + s1, 1);
+                    pG10 = xo_pb(L, E_IS_REP_G1 + s1, 0);
+                    pG11 = xo_pb(L, E_IS_REP_G1 + s1, 1);
+                    pG20 = xo_pb(L, E_IS_REP_G2 + s1, 0);
+                    pG21 = xo_pb(L, E_IS_REP_G2 + s1, 1);
+                    auto plain = [&](u32 sym) {
+                        u32 sum = 0;
+#pragma unroll
+                        for (u32 j = 0; j < 8; j++) sum += xo_pb(L, E_LITERAL + ((1u << j) | (sym >> (8 - j))), (sym >> (7 - j)) & 1);
+                        return sum;
+                    };
+                    pL0 = plain((u32)lane);
+                    pL1 = plain((u32)lane + 64);
+                    pL2 = plain((u32)lane + 128);
+                    pL3 = plain((u32)lane + 192);
+                }
+                issue(0, cq0, cq1, cq2, cq3);
+                for (u32 t = 0; t < W; t++) {
+                    u64 tq = XO_PROF >= 2 ? __builtin_readcyclecounter() : 0;
+                    auto stamp = [&](int slot) {
+                        if (XO_PROF >= 2) {
+                            const u64 t2 = __builtin_readcyclecounter();
+                            prof2[slot] += t2 - tq;
+                            tq = t2;
                         }
-                        if (lane == 0) {
-                            L.nst[i] = (u8)st;
-                            L.nrep[i][0] = q0; L.nrep[i][1] = q1; L.nrep[i][2] = q2; L.nrep[i][3] = q3;
-                        }
-                    }
-                    const u32 P = (alo >> 20) | (ahi << 12);
-                    const u64 at = p + i;
+                    };
+                    const u64 at = p + t;
                     const u32 ps = (u32)at & 3;
-                    const u32 room = W - i, mx = room < XO_MAXLEN ? room : XO_MAXLEN;
-                    const u32 sym = L.tile[i];
-                    const u32 mbyte = at > q0 ? ufl(sbyte(at - q0 - 1, p)) : 0u;
-                    // ---- rep lengths: lane = rep * 16 + byte of the round ----
+                    const u32 room = W - t, mx = room < XO_MAXLEN ? room : XO_MAXLEN;
+                    const u32 st = cst, q0 = cq0, q1 = cq1, q2 = cq2, q3 = cq3, P = cP;
+                    // ---- node t: rep lengths (lane = rep * 16 + byte), first round issued ----
+                    const u32 sym = ufl(i_sym);
+                    const u32 wk[XO_K] = {ufl(i_w0), ufl(i_w1), ufl(i_w2)};
                     u32 rl0 = 0, rl1 = 0, rl2 = 0, rl3 = 0, open = 0xF;
                     {
                         const u32 r = (u32)lane >> 4, tb = (u32)lane & 15;
                         const u32 rd = r == 0 ? q0 : r == 1 ? q1 : r == 2 ? q2 : q3;
+                        bool ok = i_valid && i_mine == i_rb;
                         for (u32 base = 0; open; base += 16) {
-                            const u32 o = base + tb;
-                            bool ok = false;
-                            if (((open >> r) & 1) && at > rd && o < mx)
-                                ok = L.tile[i + o] == sbyte(at - rd - 1 + o, p);
+                            if (base) {
+                                const u32 o = base + tb;
+                                ok = false;
+                                if (((open >> r) & 1) && at > rd && o < mx)
+                                    ok = L.tile[XO_HIST + t + o] == sbyte(at - rd - 1 + o, p);
+                            }
                             const u64 miss = __ballot(!ok);
                             u32 done = 0;
                             for (u32 rr = 0; rr < 4; rr++) {
@@ -346,85 +520,123 @@ __global__ __launch_bounds__(64) void xo_segment(const zcg_chunk* __restrict__ c
                             open &= ~done;
                         }
                     }
-                    // ---- literal bit prices (lanes 0-7) and flag prices (lanes 8-19) ----
-                    u32 pv = 0;
-                    if (lane < 8) {
-                        const u32 j = (u32)lane, b = (sym >> (7 - j)) & 1, m = (1u << j) | (sym >> (8 - j));
-                        u32 idx = E_LITERAL + m;
-                        if (st >= 7) {
+                    const u32 mbyte = at > q0 ? (u32)__builtin_amdgcn_readlane((int)i_rb, 0) : 0u;
+                    stamp(1);
+                    // ---- node t: literal price (matched literals: lanes 0-7) and flag prices ----
+                    u32 litp;
+                    if (st < 7) {
+                        const u32 hi = sym >> 6, lo = sym & 63;
+                        const u32 v = hi == 0 ? pL0 : hi == 1 ? pL1 : hi == 2 ? pL2 : pL3;
+                        litp = (u32)__builtin_amdgcn_readlane((int)v, (int)lo);
+                    } else {
+                        u32 pv = 0;
+                        if (lane < 8) {
+                            const u32 j = (u32)lane, b = (sym >> (7 - j)) & 1, m = (1u << j) | (sym >> (8 - j));
                             const u32 off = (sym >> (8 - j)) == (mbyte >> (8 - j)) ? 0x100u : 0u;
                             const u32 mbit = off ? ((mbyte >> (7 - j)) & 1) << 8 : 0u;
-                            idx += off + mbit;
+                            pv = xo_pb(L, E_LITERAL + m + off + mbit, b);
                         }
-                        pv = xo_pb(L, idx, b);
-                    } else if (lane < 20) {
-                        const u32 f = (u32)lane - 8, b = f & 1;
-                        const u32 idx = f < 2 ? E_IS_MATCH + (st << 4) + ps
-                                      : f < 4 ? E_IS_REP + st
-                                      : f < 6 ? E_IS_REP_G0 + st
-                                      : f < 8 ? E_IS_REP_G1 + st
-                                      : f < 10 ? E_IS_REP_G2 + st
-                                      : E_IS_REP0_LONG + (st << 4) + ps;
-                        pv = xo_pb(L, idx, b);
+                        litp = 0;
+                        for (int j = 0; j < 8; j++) litp += (u32)__builtin_amdgcn_readlane((int)pv, j);
                     }
-                    u32 litp = 0;
-                    for (int j = 0; j < 8; j++) litp += (u32)__builtin_amdgcn_readlane((int)pv, j);
-                    u32 f[12];
-                    for (int j = 0; j < 12; j++) f[j] = (u32)__builtin_amdgcn_readlane((int)pv, 8 + j);
-                    // ---- arcs: literal, short rep, rep ranges, candidate ranges ----
+                    const int sps = (int)(st * 4 + ps), sst = (int)st;
+                    const u32 f[12] = {(u32)__builtin_amdgcn_readlane((int)pIM0, sps), (u32)__builtin_amdgcn_readlane((int)pIM1, sps),
+                                       (u32)__builtin_amdgcn_readlane((int)pIR0, sst), (u32)__builtin_amdgcn_readlane((int)pIR1, sst),
+                                       (u32)__builtin_amdgcn_readlane((int)pG00, sst), (u32)__builtin_amdgcn_readlane((int)pG01, sst),
+                                       (u32)__builtin_amdgcn_readlane((int)pG10, sst), (u32)__builtin_amdgcn_readlane((int)pG11, sst),
+                                       (u32)__builtin_amdgcn_readlane((int)pG20, sst), (u32)__builtin_amdgcn_readlane((int)pG21, sst),
+                                       (u32)__builtin_amdgcn_readlane((int)pRL0, sps), (u32)__builtin_amdgcn_readlane((int)pRL1, sps)};
+                    stamp(2);
+                    // ---- node t + 1: final key (min with node t's literal / short rep), state, reps ----
                     const bool sr = at > q0 && sym == mbyte;
                     const u32 rbase = P + f[1] + f[3];
+                    {
+                        const u64 kl = ((u64)(P + f[0] + litp) << 20) | ((u64)t << 11);
+                        const u64 ks = sr ? ((u64)(rbase + f[4] + f[10]) << 20) | ((u64)t << 11) | 1u : ~0ull;
+                        u64 nk = L.key[t + 1];
+                        nk = ((u64)ufl((u32)(nk >> 32)) << 32) | ufl((u32)nk);
+                        nk = nk < kl ? nk : kl;
+                        nk = nk < ks ? nk : ks;
+                        wsync_lds();
+                        if (lane == 0) L.key[t + 1] = nk;
+                        cP = (u32)(nk >> 20);
+                        if (t + 1 < W) {
+                            const u32 alo = (u32)nk, src = (alo >> 11) & 511, arc = alo & 2047;
+                            u32 bst, b0, b1, b2, b3;
+                            if (src == t) {
+                                bst = st; b0 = q0; b1 = q1; b2 = q2; b3 = q3;
+                            } else {
+                                bst = ufl(L.nst[src]);
+                                b0 = ufl(L.nr.nrep[src][0]); b1 = ufl(L.nr.nrep[src][1]);
+                                b2 = ufl(L.nr.nrep[src][2]); b3 = ufl(L.nr.nrep[src][3]);
+                            }
+                            if (arc == 0) { cst = st_lit(bst); cq0 = b0; cq1 = b1; cq2 = b2; cq3 = b3; }
+                            else if (arc == 1) { cst = st_short(bst); cq0 = b0; cq1 = b1; cq2 = b2; cq3 = b3; }
+                            else if (arc < ARC_MATCH) {
+                                const u32 r = (arc - ARC_REP) / 274;
+                                cst = st_rep(bst);
+                                cq0 = r == 0 ? b0 : r == 1 ? b1 : r == 2 ? b2 : b3;
+                                cq1 = r == 0 ? b1 : b0;
+                                cq2 = r <= 1 ? b2 : b1;
+                                cq3 = r <= 2 ? b3 : b2;
+                            } else {
+                                cst = st_match(bst);
+                                cq0 = ufl(xo_arc_dist(wc, src, arc - ARC_MATCH, W - src));
+                                cq1 = b0; cq2 = b1; cq3 = b2;
+                            }
+                            if (lane == 0) {
+                                L.nst[t + 1] = (u8)cst;
+                                L.nr.nrep[t + 1][0] = cq0; L.nr.nrep[t + 1][1] = cq1; L.nr.nrep[t + 1][2] = cq2; L.nr.nrep[t + 1][3] = cq3;
+                            }
+                            issue(t + 1, cq0, cq1, cq2, cq3);
+                        }
+                    }
+                    stamp(0);
+                    // ---- node t: rep and candidate arcs (lengths >= 2, targets >= t + 2) ----
                     const u32 rb[4] = {rbase + f[4] + f[11], rbase + f[5] + f[6], rbase + f[5] + f[7] + f[8],
                                        rbase + f[5] + f[7] + f[9]};
                     const u32 rl[4] = {rl0, rl1, rl2, rl3};
-                    u32 cnt[9], ga[9], gc1[9], gh[9], gd[9];
-                    cnt[0] = 1; cnt[1] = sr ? 1u : 0u;
+                    u32 cnt[7], ga[7], gc1[7], gh[7], gd[7];
                     for (u32 r = 0; r < 4; r++) {
-                        ga[2 + r] = 2;
-                        cnt[2 + r] = rl[r] >= 2 ? xo_range_count(2, rl[r], &gc1[2 + r], &gh[2 + r]) : 0u;
-                        gd[2 + r] = 0;
+                        ga[r] = 2;
+                        cnt[r] = rl[r] >= 2 ? xo_range_count(2, rl[r], &gc1[r], &gh[r]) : 0u;
+                        gd[r] = 0;
                     }
                     u32 lprev = 1;
                     for (u32 c = 0; c < XO_K; c++) {
-                        const u32 w = L.wc[i * XO_K + c], Lk = w >> 23;
+                        const u32 w = wk[c], Lk = w >> 23;
                         const u32 Lr = Lk < mx ? Lk : mx;
                         const u32 a0 = lprev + 1 > 2 ? lprev + 1 : 2;
-                        ga[6 + c] = a0;
-                        gd[6 + c] = w & 0x7FFFFFu;
-                        cnt[6 + c] = Lk ? xo_range_count(a0, Lr, &gc1[6 + c], &gh[6 + c]) : 0u;
+                        ga[4 + c] = a0;
+                        gd[4 + c] = w & 0x7FFFFFu;
+                        cnt[4 + c] = Lk ? xo_range_count(a0, Lr, &gc1[4 + c], &gh[4 + c]) : 0u;
                         if (Lk && Lr > lprev) lprev = Lr;
                     }
                     u32 N = 0;
-                    for (u32 g = 0; g < 9; g++) N += cnt[g];
+                    for (u32 g = 0; g < 7; g++) N += cnt[g];
                     const u32 mb0 = P + f[1] + f[2];
+                    stamp(3);
                     for (u32 base = 0; base < N; base += 64) {
                         const u32 j = base + (u32)lane;
                         if (j < N) {
                             u32 g = 0, acc = 0;
                             while (j >= acc + cnt[g]) { acc += cnt[g]; g++; }
                             const u32 el = j - acc;
-                            u32 len = 1, price, arc;
-                            if (g == 0) {
-                                price = P + f[0] + litp;
-                                arc = 0;
-                            } else if (g == 1) {
-                                price = rbase + f[4] + f[10];
-                                arc = 1;
+                            const u32 len = el < gc1[g] ? ga[g] + el : gh[g] + (el - gc1[g]);
+                            u32 price, arc;
+                            if (g < 4) {
+                                price = rb[g] + xo_arc_price(L, E_REP_LEN, len - 2, ps, false, 0, len);
+                                arc = ARC_REP + g * 274 + len;
                             } else {
-                                len = el < gc1[g] ? ga[g] + el : gh[g] + (el - gc1[g]);
-                                if (g < 6) {
-                                    price = rb[g - 2] + xo_plen(L, E_REP_LEN, len - 2, ps);
-                                    arc = ARC_REP + (g - 2) * 274 + len;
-                                } else {
-                                    price = mb0 + xo_plen(L, E_LEN, len - 2, ps) + xo_pdist(L, gd[g], len);
-                                    arc = ARC_MATCH + len;
-                                }
+                                price = mb0 + xo_arc_price(L, E_LEN, len - 2, ps, true, gd[g], len);
+                                arc = ARC_MATCH + len;
                             }
-                            const u64 key = ((u64)price << 20) | ((u64)i << 11) | arc;
-                            atomicMin((unsigned long long*)&L.key[i + len], (unsigned long long)key);
+                            const u64 key = ((u64)price << 20) | ((u64)t << 11) | arc;
+                            atomicMin((unsigned long long*)&L.key[t + len], (unsigned long long)key);
                         }
                     }
-                    __syncthreads();
+                    wsync_lds();
+                    stamp(4);
                 }
                 // ---- the path to the window end (reversed) ----
                 {
@@ -433,10 +645,10 @@ __global__ __launch_bounds__(64) void xo_segment(const zcg_chunk* __restrict__ c
                         const u64 a = L.key[j];
                         const u32 alo = ufl((u32)a);
                         const u32 src = (alo >> 11) & 511, arc = alo & 2047, len = j - src;
-                        const u32 d = arc >= ARC_MATCH ? xo_arc_dist(L, src, len, W - src) : 0u;
+                        const u32 d = arc >= ARC_MATCH ? xo_arc_dist(wc, src, len, W - src) : 0u;
                         if (lane == 0) {
-                            L.pth[np] = arc | (len << 11);
-                            L.pdist[np] = d;
+                            L.nr.path.pth[np] = arc | (len << 11);
+                            L.nr.path.pdist[np] = d;
                         }
                         np++;
                         j = src;
@@ -444,27 +656,21 @@ __global__ __launch_bounds__(64) void xo_segment(const zcg_chunk* __restrict__ c
                     npath = np;
                     __syncthreads();
                 }
+                if (XO_PROF) {
+                    prof[0] += __builtin_readcyclecounter() - tp0;
+                    prof[2] += W;
+                    prof[4] += 1;
+                }
             }
+            if (XO_PROF) prof[3] += 1;
             // ---- code the next symbol of the path ----
             npath--;
-            const u32 w = ufl(L.pth[npath]);
+            const u32 w = ufl(L.nr.path.pth[npath]);
             const u32 arc = w & 2047, len = w >> 11, ps = (u32)p & 3;
             if (arc == 0) {
-                const u32 sym = L.tile[p - wb];
+                const u32 sym = L.tile[XO_HIST + p - wb];
                 e.bit(E_IS_MATCH + (state << 4) + ps, 0);
-                if (state < 7) {
-                    e.tree(E_LITERAL, 8, sym);
-                } else {
-                    u32 mb = p > r0 ? ufl(sbyte(p - r0 - 1, wb)) : 0u, off = 0x100, m = 1;
-                    for (int q = 7; q >= 0; q--) {
-                        const u32 b = (sym >> q) & 1;
-                        mb <<= 1;
-                        const u32 mbit = mb & off;
-                        e.bit(E_LITERAL + off + mbit + m, b);
-                        m = (m << 1) | b;
-                        off &= b ? mbit : ~mbit;
-                    }
-                }
+                xo_literal(e, sym, state >= 7, state >= 7 && p > r0 ? ufl(sbyte(p - r0 - 1, wb)) : 0u);
                 state = st_lit(state);
             } else if (arc == 1) {
                 e.bit(E_IS_MATCH + (state << 4) + ps, 1);
@@ -493,14 +699,14 @@ __global__ __launch_bounds__(64) void xo_segment(const zcg_chunk* __restrict__ c
                     r1 = r0;
                     r0 = d;
                 }
-                e.length(E_REP_LEN, len - 2, ps);
+                xo_length(e, E_REP_LEN, len - 2, ps);
                 state = st_rep(state);
             } else {
-                const u32 d = ufl(L.pdist[npath]);
+                const u32 d = ufl(L.nr.path.pdist[npath]);
                 e.bit(E_IS_MATCH + (state << 4) + ps, 1);
                 e.bit(E_IS_REP + state, 0);
-                e.length(E_LEN, len - 2, ps);
-                e.distance(d, len);
+                xo_length(e, E_LEN, len - 2, ps);
+                xo_distance(e, d, len);
                 r3 = r2; r2 = r1; r1 = r0; r0 = d;
                 state = st_match(state);
             }
@@ -533,6 +739,16 @@ __global__ __launch_bounds__(64) void xo_segment(const zcg_chunk* __restrict__ c
     }
     e.out_flush();
     if (lane == 0) seglen[sid] = e.over ? 0xFFFFFFFFu : (u32)e.pos;
+    if (XO_PROF && lane == 0) {
+        const u64 tot = __builtin_readcyclecounter() - tk0;
+        atomicAdd(&g_xo_prof[0], (unsigned long long)prof[0]);
+        atomicAdd(&g_xo_prof[1], (unsigned long long)(tot - prof[0]));
+        atomicAdd(&g_xo_prof[2], (unsigned long long)prof[2]);
+        atomicAdd(&g_xo_prof[3], (unsigned long long)prof[3]);
+        atomicAdd(&g_xo_prof[4], (unsigned long long)prof[4]);
+        atomicAdd(&g_xo_prof[5], (unsigned long long)tot);
+        for (int q = 0; q < 6; q++) atomicAdd(&g_xo_prof[8 + q], (unsigned long long)prof2[q]);
+    }
 }
 
 // ---------------------------------------------------------------- assembly
@@ -654,6 +870,15 @@ XoLayout xo_layout(u64 D, u32 n) {
 }
 
 }  // namespace
+
+extern "C" int zcg__debug_xz_opt_counters(unsigned long long* out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_xo_prof), sizeof(unsigned long long) * 16) != hipSuccess) return -1;
+    if (reset) {
+        unsigned long long z[16] = {0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_xo_prof), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return 0;
+}
 
 uint64_t xz_opt_ws_bytes(const zcg_array* a, uint32_t n) {
     const DType t = make_dtype(a->dtype);
