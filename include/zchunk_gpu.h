@@ -86,8 +86,8 @@ enum zcg_status {
 #define ZCG_FLAG_XZ_RING_32K 0x400u
 /* LZ4 block decoder choice (bit-identical): one wave per block (speculative
  * parse, byte-parallel resolve) or one lane per block; by default the batch
- * size picks: waves below 65 536 blocks, both side by side (on a second
- * stream) up to 262 144, lanes above. */
+ * size picks: waves below 131 072 blocks, both side by side (on a second
+ * stream) below 196 608, lanes from there. */
 #define ZCG_FLAG_LZ4_WAVE_PER_BLOCK 0x800u
 #define ZCG_FLAG_LZ4_LANE_PER_BLOCK 0x1000u
 /* Gzip decode kernel choice (all bit-identical).  By default a batch of at

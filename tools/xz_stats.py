@@ -58,12 +58,14 @@ ms = float(np.median(ts))
 res = {"n": n, "ms": round(ms, 2), "gibs": round(n * D / 2**30 / (ms * 1e-3), 3), "ratio": round(ratio, 4),
        "status_ok": int((st == 0).sum()), "sample_decodes": ok}
 if prof and cnt[5]:
-    segs = n * ((D + (1 << 18) - 1) >> 18)
+    segs = n * ((D + (352 << 10) - 1) // (352 << 10))
     res["prof"] = {"plan_share": round(cnt[0] / cnt[5], 3), "code_share": round(cnt[1] / cnt[5], 3),
                    "cycles_per_node_plan": round(cnt[0] / max(1, cnt[2]), 1),
                    "cycles_per_symbol_code": round(cnt[1] / max(1, cnt[3]), 1),
                    "nodes": cnt[2], "symbols": cnt[3], "windows": cnt[4],
-                   "kcycles_per_segment": round(cnt[5] / segs / 1e3, 1)}
+                   "kcycles_per_segment": round(cnt[5] / segs / 1e3, 1),
+                   "segment_ms": round(cnt[6] / segs / 1e5, 2),
+                   "effective_ghz": round(cnt[5] / max(1, cnt[6]) / 10, 3)}
     if cnt[8]:
         names = ["next_node_and_issue", "reps", "lit_flags", "arc_setup", "arc_price_relax", "unused"]
         res["prof"]["node_cycles"] = {k: round(cnt[8 + q] / max(1, cnt[2]), 1) for q, k in enumerate(names)}

@@ -465,15 +465,17 @@ __global__ void bze_update(u32 n, u32 h2, const u64* __restrict__ keys, const u3
 // in its tile of BZE_LC SA positions (a group may run past the tile; one
 // larger than BZE_LN stays for the global rounds) and refines them in LDS:
 // 8 more bytes of each unresolved rotation per round (cyclic within its
-// block), a bitonic sort by (tie run, bytes), new tie runs — up to
-// BZE_LROUNDS rounds.  Resolved positions get their final SA slot and rank;
+// block), a bitonic sort by (tie run, bytes) — or, once every tie run is
+// short, an insertion sort of each run by its head thread — and new tie
+// runs, for up to BZE_LROUNDS rounds.  Resolved positions get their final SA slot and rank;
 // rotations still tied afterwards keep their run head as rank and stay
 // flagged for the global prefix-doubling rounds (whose ranks only need to be
 // at least 4-byte accurate, which refined ranks are).  A tie that reaches
 // the block length is an equal rotation: any order decodes the same.
 constexpr u32 BZE_LC = 2048;
 constexpr u32 BZE_LN = 2 * BZE_LC;
-constexpr u32 BZE_LROUNDS = 8;
+constexpr u32 BZE_LROUNDS = 4;  // (depth 4 + 32 bytes; deeper ties go to the global rounds)
+constexpr u32 BZE_ISORT = 64;   // tie runs up to this long are insertion-sorted by one thread
 
 __device__ __forceinline__ u64 bze_key8(const u8* __restrict__ text, u32 s, u32 len, u32 loc) {
     u64 v = 0;
@@ -493,7 +495,7 @@ __global__ __launch_bounds__(BZE_T) void bze_lds_sort(u32 T, const u8* __restric
     __shared__ u32 R[BZE_LN];
     __shared__ u32 P[BZE_LN];
     __shared__ u32 part[BZE_T];
-    __shared__ u32 s_a, s_last, s_b, s_tied;
+    __shared__ u32 s_a, s_last, s_b, s_tied, s_maxrun;
     const u32 tid = threadIdx.x;
     const u32 t0 = blockIdx.x * BZE_LC;
     const u32 t1 = (T - t0) < BZE_LC ? T : t0 + BZE_LC;
@@ -535,7 +537,26 @@ __global__ __launch_bounds__(BZE_T) void bze_lds_sort(u32 T, const u8* __restric
     }
     __syncthreads();
     u32 depth = 4;
+    if (tid == 0) s_maxrun = 0xFFFFFFFFu;
+    __syncthreads();
     for (u32 round = 0; round < BZE_LROUNDS; round++) {
+        if (s_maxrun <= BZE_ISORT) {
+            // every tie run is short: its head thread insertion-sorts it by K
+            for (u32 k = tid; k < n; k += BZE_T) {
+                if (R[k] != k || k + 1 >= n || R[k + 1] != k) continue;
+                u32 e = k + 1;
+                while (e < n && R[e] == k) e++;
+                for (u32 i = k + 1; i < e; i++) {
+                    const u64 kv = K[i];
+                    const u32 pv = P[i];
+                    u32 j = i;
+                    while (j > k && K[j - 1] > kv) { K[j] = K[j - 1]; P[j] = P[j - 1]; j--; }
+                    K[j] = kv;
+                    P[j] = pv;
+                }
+            }
+            __syncthreads();
+        } else
         // bitonic sort by (R, K)
         for (u32 kk = 2; kk <= N; kk <<= 1)
             for (u32 j = kk >> 1; j > 0; j >>= 1) {
@@ -603,6 +624,15 @@ __global__ __launch_bounds__(BZE_T) void bze_lds_sort(u32 T, const u8* __restric
         __syncthreads();
         depth += 8;
         if (!s_tied) break;
+        // the longest tie run (capped) picks the next round's sort
+        if (tid == 0) s_maxrun = 0;
+        __syncthreads();
+        for (u32 k = tid; k < n; k += BZE_T) {
+            if (R[k] != k || k + 1 >= n || R[k + 1] != k) continue;
+            u32 e = k + 1;
+            while (e < n && R[e] == k && e - k <= BZE_ISORT) e++;
+            atomicMax(&s_maxrun, e - k);
+        }
         __syncthreads();
     }
     // write back: SA order, ranks (run heads for ties), flags

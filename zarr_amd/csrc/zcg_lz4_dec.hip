@@ -753,17 +753,19 @@ constexpr u32 LZ_LPC = LZ_LRB / 2;  // flush granularity = longest piece written
 constexpr u32 LZ_LRM = LZ_LRB - 1;
 constexpr u32 LZ_LWG = 64;          // lanes (blocks) per workgroup
 constexpr u64 LZ_LANE_MIN_BLOCKS = 131072;
-// Between the two (measured at 8 192 C4 chunks = 131 072 blocks: lanes 50.6 ms,
-// waves 54.3 ms, 55 % lanes + 45 % waves side by side 45.0 ms) both kernels run
-// at once on two streams; from 262 144 blocks up the lanes alone are faster.
+// From 131 072 blocks (measured at 8 192 C4 chunks: lanes 50.6 ms, waves 54.3
+// ms, 55 % lanes + 45 % waves side by side 45.0 ms) both kernels run at once on
+// two streams; below it the waves alone are faster (4 096 chunks: waves 27.8,
+// side by side 43.9; 6 144: 41.1 / 44.7), and from 262 144 blocks the lanes
+// alone (16 384 chunks: 61.4 vs 79.2).
 #ifndef LZ_CORUN_PCT
 #define LZ_CORUN_PCT 55  // percent of the chunks decoded by lanes in a side-by-side batch
 #endif
 #ifndef LZ_CORUN_LO
-#define LZ_CORUN_LO 65536
+#define LZ_CORUN_LO 131072
 #endif
 #ifndef LZ_CORUN_HI
-#define LZ_CORUN_HI 262144
+#define LZ_CORUN_HI 196608
 #endif
 
 // The ring is written and read with byte-unaligned ds_write_b128 /

@@ -16,10 +16,10 @@
 //      close matches price well on numeric data) to the strictly-longer
 //      chain matches (16 links, < 2^23 back) and keeps the 3 longest,
 //      packed len << 23 | dist;
-//   2. xo_segment (one wave per 256 KiB segment of a chunk): each segment is
+//   2. xo_segment (one wave per 352 KiB segment of a chunk): each segment is
 //      an independent LZMA2 run — its first LZMA chunk resets the state and
 //      sets the properties (lc=0 lp=0 pb=2: 2.6 K probabilities in LDS), the
-//      dictionary is shared — so a 1 MiB chunk is coded by 4 waves at once.
+//      dictionary is shared — so a 1 MiB chunk is coded by 3 waves at once.
 //      The parse plans windows of <= 256 positions: node i's arcs (literal,
 //      short rep, rep0-3, candidate matches; lengths 2..8 and the last three
 //      of each range) are priced lane-parallel from the probabilities at the
@@ -36,7 +36,7 @@ namespace zcg {
 
 namespace {
 
-constexpr u32 XO_SEG = 1u << 18;   // bytes per independently coded segment
+constexpr u32 XO_SEG = 352u << 10;  // bytes per independently coded segment (a 1 MiB chunk: 3 waves)
 constexpr u32 XO_WIN = 256;        // parse window (positions)
 constexpr u32 XO_K = 3;            // candidates kept per position
 constexpr u32 XO_DEPTH = 16;       // hash-chain links walked
@@ -189,6 +189,49 @@ __device__ __forceinline__ void xo_code(XeEnc& e, const u32 (&idx)[N], const u32
         }
     }
 }
+
+// Like xo_code, for N fixed slots of which `use` (bit j = slot j) are coded,
+// in slot order: one LDS round trip for a whole symbol's modelled bits.
+template <int N>
+__device__ __forceinline__ void xo_code_m(XeEnc& e, const u32 (&idx)[N], const u32 (&bits)[N], u32 use) {
+    u32 pr[N];
+#pragma unroll
+    for (int j = 0; j < N; j++) pr[j] = (use >> j) & 1 ? (u32)e.probs[idx[j]] : 0u;
+#pragma unroll
+    for (int j = 0; j < N; j++) {
+        if (!((use >> j) & 1)) continue;
+        const u32 p = pr[j], bound = (e.range >> 11) * p;
+        u32 np;
+        if (bits[j] == 0) {
+            e.range = bound;
+            np = p + ((2048 - p) >> 5);
+        } else {
+            e.low += bound;
+            e.range -= bound;
+            np = p - (p >> 5);
+        }
+        e.probs[idx[j]] = (u16)np;
+        while (e.range < (1u << 24)) {
+            e.range <<= 8;
+            e.shift_low();
+        }
+    }
+}
+// the 10 length-code slots (choice, choice2, 8 tree levels) of l = len - 2 at o
+template <int N>
+__device__ __forceinline__ void xo_len_slots(u32 (&idx)[N], u32 (&bits)[N], u32& use, int o, u32 lb, u32 l, u32 ps) {
+    idx[o] = lb + EL_CHOICE; bits[o] = l >= 8; use |= 1u << o;
+    idx[o + 1] = lb + EL_CHOICE2; bits[o + 1] = l >= 16; use |= (l >= 8 ? 1u : 0u) << (o + 1);
+    const u32 tb = l < 8 ? EL_LOW + (ps << 3) : l < 16 ? EL_MID + (ps << 3) : EL_HIGH;
+    const u32 tv = l < 8 ? l : l < 16 ? l - 8 : l - 16, tn = l < 16 ? 3u : 8u;
+#pragma unroll
+    for (u32 k = 0; k < 8; k++) {
+        const bool u = k < tn;
+        bits[o + 2 + k] = u ? (tv >> (tn - 1 - k)) & 1 : 0u;
+        idx[o + 2 + k] = lb + tb + ((1u << k) | (u ? tv >> (tn - k) : 0u));
+        use |= (u ? 1u : 0u) << (o + 2 + k);
+    }
+}
 // an nb-bit tree symbol (MSB first) / reverse tree symbol (LSB first)
 template <int N>
 __device__ __forceinline__ void xo_tree(XeEnc& e, u32 base, u32 nb, u32 v) {
@@ -263,14 +306,18 @@ __device__ __forceinline__ void xo_distance(XeEnc& e, u32 d, u32 len) {
 struct XoLds {
     u64 key[XO_WIN + 1];       // best (price << 20 | source << 11 | arc) of each window node
     union {
-        u32 nrep[XO_WIN + 1][4];  // planning: reps of each node's best path
-        struct {                  // coding: the planned path, reversed
-            u32 pth[XO_WIN];      //   arc | len << 11
-            u32 pdist[XO_WIN];    //   and the match distance
+        struct {                   // planning: the window's price tables (from the probabilities at its start)
+            u16 len[2][4][272];    //   match / rep length codes by position state and len - 2
+            u16 slot[4][64];       //   position slots by length state
+            u16 spec[128];         //   the reverse-tree low bits of distances 4..127
+            u16 align[16];         //   the 4 align bits
+        } pt;
+        struct {                   // coding: the planned path, reversed
+            u32 pth[XO_WIN];       //   arc | len << 11
+            u32 pdist[XO_WIN];     //   and the match distance
         } path;
     } nr;
     u16 probs[XO_PROBS];
-    u8 nst[XO_WIN + 1];        // state of each node
     u8 tile[XO_HIST + XO_WIN]; // the window's bytes and the XO_HIST before it
     u8 price[128];
 };
@@ -384,6 +431,7 @@ __global__ __launch_bounds__(64) void xo_segment(const zcg_chunk* __restrict__ c
     u64 prof[5] = {0, 0, 0, 0, 0};
     u64 prof2[6] = {0, 0, 0, 0, 0, 0};
     const u64 tk0 = XO_PROF ? __builtin_readcyclecounter() : 0;
+    const u64 rt0 = XO_PROF ? __builtin_amdgcn_s_memrealtime() : 0;  // 100 MHz reference clock
     // serialised byte x (< the window end): from the tile when it is inside
     auto sbyte = [&](u64 x, u64 wbase) -> u32 {
         return x + XO_HIST >= wbase ? (u32)L.tile[x + XO_HIST - wbase] : e.sb(x);
@@ -419,11 +467,7 @@ __global__ __launch_bounds__(64) void xo_segment(const zcg_chunk* __restrict__ c
                     if (j + p >= XO_HIST) L.tile[j] = (u8)e.sb(p + j - XO_HIST);
                 const u32* __restrict__ wc = cbase + p * XO_K;  // the window's candidates (read-only)
                 __syncthreads();
-                if (lane == 0) {
-                    L.key[0] = 0;
-                    L.nst[0] = (u8)state;
-                    L.nr.nrep[0][0] = r0; L.nr.nrep[0][1] = r1; L.nr.nrep[0][2] = r2; L.nr.nrep[0][3] = r3;
-                }
+                if (lane == 0) L.key[0] = 0;
                 __syncthreads();
                 // Nodes in order, software-pipelined by one: node t's literal and
                 // short-rep keys (its only arcs to t + 1) are resolved in registers,
@@ -477,6 +521,75 @@ __global__ __launch_bounds__(64) void xo_segment(const zcg_chunk* __restrict__ c
                     pL2 = plain((u32)lane + 128);
                     pL3 = plain((u32)lane + 192);
                 }
+                // length / distance price tables of the window (lane-parallel)
+                for (u32 q = lane; q < 2 * 4 * 272; q += 64) {
+                    const u32 coder = q / 1088, ps4 = (q / 272) & 3, l = q % 272;
+                    (&L.nr.pt.len[0][0][0])[q] = (u16)xo_arc_price(L, coder ? E_REP_LEN : E_LEN, l, ps4, false, 0, 2);
+                }
+                for (u32 q = lane; q < 4 * 64; q += 64) {
+                    const u32 lps = q >> 6, sl = q & 63;
+                    u32 sum = 0;
+#pragma unroll
+                    for (u32 k = 0; k < 6; k++)
+                        sum += xo_pb(L, E_POS_SLOT + (lps << 6) + ((1u << k) | (sl >> (6 - k))), (sl >> (5 - k)) & 1);
+                    L.nr.pt.slot[lps][sl] = (u16)sum;
+                }
+                for (u32 q = lane; q < 128 + 16; q += 64) {
+                    u32 sum = 0, m = 1;
+                    if (q < 128) {
+                        if (q >= 4) {
+                            const u32 sl = slot_of(q), nd = (sl >> 1) - 1, base = (2 | (sl & 1)) << nd, red = q - base;
+                            for (u32 k = 0; k < nd; k++) {
+                                const u32 b = (red >> k) & 1;
+                                sum += xo_pb(L, E_SPEC_POS + base - sl - 1 + m, b);
+                                m = (m << 1) | b;
+                            }
+                        }
+                        L.nr.pt.spec[q] = (u16)sum;
+                    } else {
+                        const u32 a = q - 128;
+                        for (u32 k = 0; k < 4; k++) {
+                            const u32 b = (a >> k) & 1;
+                            sum += xo_pb(L, E_ALIGN + m, b);
+                            m = (m << 1) | b;
+                        }
+                        L.nr.pt.align[a] = (u16)sum;
+                    }
+                }
+                __syncthreads();
+                // Each node's state and reps live in registers: node i in lane
+                // i & 63 of row i >> 6 (nodes 0..255 are the arcs' sources).
+                u32 nS[4] = {0, 0, 0, 0}, nR0[4] = {0, 0, 0, 0}, nR1[4] = {0, 0, 0, 0}, nR2[4] = {0, 0, 0, 0},
+                    nR3[4] = {0, 0, 0, 0};
+                auto node_put = [&](u32 i, u32 st_, u32 a0, u32 a1, u32 a2, u32 a3) {
+                    const u32 row = i >> 6;
+                    const int ln = (int)(i & 63);
+#pragma unroll
+                    for (u32 rr = 0; rr < 4; rr++) {
+                        if (rr != row) continue;
+                        const bool me = lane == ln;
+                        nS[rr] = me ? st_ : nS[rr];
+                        nR0[rr] = me ? a0 : nR0[rr];
+                        nR1[rr] = me ? a1 : nR1[rr];
+                        nR2[rr] = me ? a2 : nR2[rr];
+                        nR3[rr] = me ? a3 : nR3[rr];
+                    }
+                };
+                auto node_get = [&](u32 i, u32& st_, u32& a0, u32& a1, u32& a2, u32& a3) {
+                    const u32 row = i >> 6;
+                    const int ln = (int)(i & 63);
+                    const u32 vS = row == 0 ? nS[0] : row == 1 ? nS[1] : row == 2 ? nS[2] : nS[3];
+                    const u32 v0 = row == 0 ? nR0[0] : row == 1 ? nR0[1] : row == 2 ? nR0[2] : nR0[3];
+                    const u32 v1 = row == 0 ? nR1[0] : row == 1 ? nR1[1] : row == 2 ? nR1[2] : nR1[3];
+                    const u32 v2 = row == 0 ? nR2[0] : row == 1 ? nR2[1] : row == 2 ? nR2[2] : nR2[3];
+                    const u32 v3 = row == 0 ? nR3[0] : row == 1 ? nR3[1] : row == 2 ? nR3[2] : nR3[3];
+                    st_ = (u32)__builtin_amdgcn_readlane((int)vS, ln);
+                    a0 = (u32)__builtin_amdgcn_readlane((int)v0, ln);
+                    a1 = (u32)__builtin_amdgcn_readlane((int)v1, ln);
+                    a2 = (u32)__builtin_amdgcn_readlane((int)v2, ln);
+                    a3 = (u32)__builtin_amdgcn_readlane((int)v3, ln);
+                };
+                node_put(0, state, r0, r1, r2, r3);
                 issue(0, cq0, cq1, cq2, cq3);
                 for (u32 t = 0; t < W; t++) {
                     u64 tq = XO_PROF >= 2 ? __builtin_readcyclecounter() : 0;
@@ -566,9 +679,7 @@ __global__ __launch_bounds__(64) void xo_segment(const zcg_chunk* __restrict__ c
                             if (src == t) {
                                 bst = st; b0 = q0; b1 = q1; b2 = q2; b3 = q3;
                             } else {
-                                bst = ufl(L.nst[src]);
-                                b0 = ufl(L.nr.nrep[src][0]); b1 = ufl(L.nr.nrep[src][1]);
-                                b2 = ufl(L.nr.nrep[src][2]); b3 = ufl(L.nr.nrep[src][3]);
+                                node_get(src, bst, b0, b1, b2, b3);
                             }
                             if (arc == 0) { cst = st_lit(bst); cq0 = b0; cq1 = b1; cq2 = b2; cq3 = b3; }
                             else if (arc == 1) { cst = st_short(bst); cq0 = b0; cq1 = b1; cq2 = b2; cq3 = b3; }
@@ -584,10 +695,7 @@ __global__ __launch_bounds__(64) void xo_segment(const zcg_chunk* __restrict__ c
                                 cq0 = ufl(xo_arc_dist(wc, src, arc - ARC_MATCH, W - src));
                                 cq1 = b0; cq2 = b1; cq3 = b2;
                             }
-                            if (lane == 0) {
-                                L.nst[t + 1] = (u8)cst;
-                                L.nr.nrep[t + 1][0] = cq0; L.nr.nrep[t + 1][1] = cq1; L.nr.nrep[t + 1][2] = cq2; L.nr.nrep[t + 1][3] = cq3;
-                            }
+                            node_put(t + 1, cst, cq0, cq1, cq2, cq3);
                             issue(t + 1, cq0, cq1, cq2, cq3);
                         }
                     }
@@ -625,10 +733,14 @@ __global__ __launch_bounds__(64) void xo_segment(const zcg_chunk* __restrict__ c
                             const u32 len = el < gc1[g] ? ga[g] + el : gh[g] + (el - gc1[g]);
                             u32 price, arc;
                             if (g < 4) {
-                                price = rb[g] + xo_arc_price(L, E_REP_LEN, len - 2, ps, false, 0, len);
+                                price = rb[g] + L.nr.pt.len[1][ps][len - 2];
                                 arc = ARC_REP + g * 274 + len;
                             } else {
-                                price = mb0 + xo_arc_price(L, E_LEN, len - 2, ps, true, gd[g], len);
+                                const u32 d = gd[g], lps = len - 2 < 3 ? len - 2 : 3, sl = slot_of(d);
+                                u32 dp = L.nr.pt.slot[lps][sl];
+                                if (sl >= 14) dp += (((sl >> 1) - 1) - 4) * 16 + L.nr.pt.align[d & 15];
+                                else if (sl >= 4) dp += L.nr.pt.spec[d];
+                                price = mb0 + L.nr.pt.len[0][ps][len - 2] + dp;
                                 arc = ARC_MATCH + len;
                             }
                             const u64 key = ((u64)price << 20) | ((u64)t << 11) | arc;
@@ -669,44 +781,73 @@ __global__ __launch_bounds__(64) void xo_segment(const zcg_chunk* __restrict__ c
             const u32 arc = w & 2047, len = w >> 11, ps = (u32)p & 3;
             if (arc == 0) {
                 const u32 sym = L.tile[XO_HIST + p - wb];
-                e.bit(E_IS_MATCH + (state << 4) + ps, 0);
-                xo_literal(e, sym, state >= 7, state >= 7 && p > r0 ? ufl(sbyte(p - r0 - 1, wb)) : 0u);
+                const bool matched = state >= 7;
+                const u32 mb = matched && p > r0 ? ufl(sbyte(p - r0 - 1, wb)) : 0u;
+                u32 idx[9], bits[9];
+                idx[0] = E_IS_MATCH + (state << 4) + ps;
+                bits[0] = 0;
+#pragma unroll
+                for (int j = 0; j < 8; j++) {
+                    bits[1 + j] = (sym >> (7 - j)) & 1;
+                    u32 x = E_LITERAL + ((1u << j) | (sym >> (8 - j)));
+                    if (matched) {
+                        const u32 off = (sym >> (8 - j)) == (mb >> (8 - j)) ? 0x100u : 0u;
+                        x += off + (off ? ((mb >> (7 - j)) & 1) << 8 : 0u);
+                    }
+                    idx[1 + j] = x;
+                }
+                xo_code_m<9>(e, idx, bits, 0x1FFu);
                 state = st_lit(state);
             } else if (arc == 1) {
-                e.bit(E_IS_MATCH + (state << 4) + ps, 1);
-                e.bit(E_IS_REP + state, 1);
-                e.bit(E_IS_REP_G0 + state, 0);
-                e.bit(E_IS_REP0_LONG + (state << 4) + ps, 0);
+                const u32 idx[4] = {E_IS_MATCH + (state << 4) + ps, E_IS_REP + state, E_IS_REP_G0 + state,
+                                    E_IS_REP0_LONG + (state << 4) + ps};
+                const u32 bits[4] = {1, 1, 0, 0};
+                xo_code_m<4>(e, idx, bits, 0xFu);
                 state = st_short(state);
             } else if (arc < ARC_MATCH) {
                 const u32 r = (arc - ARC_REP) / 274;
-                e.bit(E_IS_MATCH + (state << 4) + ps, 1);
-                e.bit(E_IS_REP + state, 1);
-                if (r == 0) {
-                    e.bit(E_IS_REP_G0 + state, 0);
-                    e.bit(E_IS_REP0_LONG + (state << 4) + ps, 1);
-                } else {
-                    e.bit(E_IS_REP_G0 + state, 1);
-                    if (r == 1) {
-                        e.bit(E_IS_REP_G1 + state, 0);
-                    } else {
-                        e.bit(E_IS_REP_G1 + state, 1);
-                        e.bit(E_IS_REP_G2 + state, r - 2);
-                    }
+                // slots: is_match, is_rep, rep_g0, rep0_long (r = 0), rep_g1, rep_g2 (r >= 2), length
+                u32 idx[16], bits[16], use = 0x7u;
+                idx[0] = E_IS_MATCH + (state << 4) + ps; bits[0] = 1;
+                idx[1] = E_IS_REP + state; bits[1] = 1;
+                idx[2] = E_IS_REP_G0 + state; bits[2] = r != 0;
+                idx[3] = E_IS_REP0_LONG + (state << 4) + ps; bits[3] = 1; use |= (r == 0 ? 1u : 0u) << 3;
+                idx[4] = E_IS_REP_G1 + state; bits[4] = r >= 2; use |= (r >= 1 ? 1u : 0u) << 4;
+                idx[5] = E_IS_REP_G2 + state; bits[5] = r >= 3; use |= (r >= 2 ? 1u : 0u) << 5;
+                xo_len_slots<16>(idx, bits, use, 6, E_REP_LEN, len - 2, ps);
+                xo_code_m<16>(e, idx, bits, use);
+                if (r != 0) {
                     const u32 d = r == 1 ? r1 : r == 2 ? r2 : r3;
                     if (r == 3) r3 = r2;
                     if (r >= 2) r2 = r1;
                     r1 = r0;
                     r0 = d;
                 }
-                xo_length(e, E_REP_LEN, len - 2, ps);
                 state = st_rep(state);
             } else {
                 const u32 d = ufl(L.nr.path.pdist[npath]);
-                e.bit(E_IS_MATCH + (state << 4) + ps, 1);
-                e.bit(E_IS_REP + state, 0);
-                xo_length(e, E_LEN, len - 2, ps);
-                xo_distance(e, d, len);
+                // slots: is_match, is_rep, length, position slot; then the slot's low bits
+                const u32 lps = len - 2 < 3 ? len - 2 : 3, slot = slot_of(d);
+                u32 idx[18], bits[18], use = 0x3u;
+                idx[0] = E_IS_MATCH + (state << 4) + ps; bits[0] = 1;
+                idx[1] = E_IS_REP + state; bits[1] = 0;
+                xo_len_slots<18>(idx, bits, use, 2, E_LEN, len - 2, ps);
+#pragma unroll
+                for (u32 k = 0; k < 6; k++) {
+                    bits[12 + k] = (slot >> (5 - k)) & 1;
+                    idx[12 + k] = E_POS_SLOT + (lps << 6) + ((1u << k) | (slot >> (6 - k)));
+                }
+                use |= 0x3Fu << 12;
+                xo_code_m<18>(e, idx, bits, use);
+                if (slot >= 4) {
+                    const u32 nd = (slot >> 1) - 1, base = (2 | (slot & 1)) << nd, red = d - base;
+                    if (slot < 14) {
+                        xo_rtree<5>(e, E_SPEC_POS + base - slot - 1, nd, red);
+                    } else {
+                        e.direct(red >> 4, nd - 4);
+                        xo_rtree<4>(e, E_ALIGN, 4, red & 15);
+                    }
+                }
                 r3 = r2; r2 = r1; r1 = r0; r0 = d;
                 state = st_match(state);
             }
@@ -748,6 +889,7 @@ __global__ __launch_bounds__(64) void xo_segment(const zcg_chunk* __restrict__ c
         atomicAdd(&g_xo_prof[4], (unsigned long long)prof[4]);
         atomicAdd(&g_xo_prof[5], (unsigned long long)tot);
         for (int q = 0; q < 6; q++) atomicAdd(&g_xo_prof[8 + q], (unsigned long long)prof2[q]);
+        atomicAdd(&g_xo_prof[6], (unsigned long long)(__builtin_amdgcn_s_memrealtime() - rt0));
     }
 }
 
