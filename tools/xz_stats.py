@@ -66,7 +66,11 @@ if prof and cnt[5]:
                    "kcycles_per_segment": round(cnt[5] / segs / 1e3, 1),
                    "segment_ms": round(cnt[6] / segs / 1e5, 2),
                    "effective_ghz": round(cnt[5] / max(1, cnt[6]) / 10, 3)}
+    if cnt[15]:
+        t0 = (~cnt[14]) & (2**64 - 1)
+        res["prof"].update({"max_wave_ms": round(cnt[7] / 1e5, 2), "start_spread_ms": round((cnt[13] - t0) / 1e5, 2),
+                            "span_ms": round((cnt[15] - t0) / 1e5, 2)})
     if cnt[8]:
-        names = ["next_node_and_issue", "reps", "lit_flags", "arc_setup", "arc_price_relax", "unused"]
+        names = ["next_node_and_issue", "reps", "lit_flags", "arc_setup", "arc_price_relax"]
         res["prof"]["node_cycles"] = {k: round(cnt[8 + q] / max(1, cnt[2]), 1) for q, k in enumerate(names)}
 print(json.dumps(res), flush=True)

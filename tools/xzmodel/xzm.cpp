@@ -39,7 +39,8 @@ int g_lens = 0;
 u32 g_seg = 0;
 int g_k3 = 0;
 u32 g_w2 = 0;
-u32 g_kmax = 0;  // > 0: the nearest 2-byte repeat only within this distance  // 1: the chain key is the exact 3-byte prefix  // > 0: a state reset every g_seg input bytes (matches may cross)  // > 0: a match's lengths relaxed: 2..g_lens and the last three
+u32 g_kmax = 0;
+u32 g_group = 64;  // > 0: the nearest 2-byte repeat only within this distance  // 1: the chain key is the exact 3-byte prefix  // > 0: a state reset every g_seg input bytes (matches may cross)  // > 0: a match's lengths relaxed: 2..g_lens and the last three
 struct Coder;
 Coder* g_frz = nullptr;
 u16 g_dump[1846 + (0x300u << 4)];
@@ -247,6 +248,7 @@ struct Node {
 // Encode `n` bytes into an .xz stream (CRC64); returns the stream length
 // (out must hold n + n/8 + 4096 bytes).  mode 0: GPU parse, 1: optimal parse.
 extern "C" void xzm_lclp(u32 lc, u32 lp, u32 kmax) { LC = lc; LP = lp; g_kmax = kmax; }
+extern "C" void xzm_group(u32 g) { g_group = g; }
 extern "C" void xzm_set(int shortm, int lens, u32 seg, int k3, u32 w2) { g_short = shortm; g_lens = lens; g_seg = seg; g_k3 = k3; g_w2 = w2; }
 extern "C" u64 xzm_encode(const u8* s, u32 n, u8* outp, int mode, u32 depth, u32 nice, u32 window) {
     init_tabs();
@@ -407,18 +409,17 @@ extern "C" u64 xzm_encode(const u8* s, u32 n, u8* outp, int mode, u32 depth, u32
                     path_i = 0;
                 }
                 // ---- mode 1: optimal parse of a window starting at p ----
-                if ((mode == 1 || mode == 3) && path_i >= path.size()) {
+                auto plan = [&](u32 p0, u32 W, u32 st0, const u32* reps0, std::vector<Node>& outp) {
                     const Coder& PC = mode == 3 ? *g_frz : C;
-                    const u32 W = std::min<u32>(window, n - p);
                     opt.assign(W + 1, Node{0xFFFFFFFFu, 0, 0, 0, 0, 0, {0, 0, 0, 0}});
                     opt[0].price = 0;
-                    opt[0].state = state;
-                    memcpy(opt[0].reps, reps, sizeof(reps));
+                    opt[0].state = st0;
+                    memcpy(opt[0].reps, reps0, sizeof(reps));
                     u32 lim = W;
                     for (u32 i = 0; i < lim && i < W; i++) {
                         const Node& nd = opt[i];
                         if (nd.price == 0xFFFFFFFFu) continue;
-                        const u32 at = p + i;
+                        const u32 at = p0 + i;
                         const u32 aps = at & ((1u << PB) - 1);
                         const u32 st = nd.state;
                         const u32* rp = nd.reps;
@@ -456,7 +457,7 @@ extern "C" u64 xzm_encode(const u8* s, u32 n, u8* outp, int mode, u32 depth, u32
                         // short rep
                         if (at > rp[0] && s[at] == s[at - rp[0] - 1]) {
                             const u32 pr = rbase + PC.pb(E_IS_REP_G0 + st, 0) + PC.pb(E_IS_REP0_LONG + (st << 4) + aps, 0);
-                            relax(i + 1, pr, 1, 1, 0, st_short(st), rp);
+                            relax(i + 1, pr, 1, 1, rp[0], st_short(st), rp);
                         }
                         // rep matches
                         for (u32 r = 0; r < 4; r++) {
@@ -472,7 +473,7 @@ extern "C" u64 xzm_encode(const u8* s, u32 n, u8* outp, int mode, u32 depth, u32
                             u32 nrep[4];
                             nrep[0] = rp[r];
                             for (u32 k = 0, t = 1; k < 4; k++) if (k != r) nrep[t++] = rp[k];
-                            for (u32 l = 2; l <= rl; l++) relax(i + l, pr + PC.plen(E_REP_LEN, l - 2, aps), 2 + r, l, 0, st_rep(st), nrep);
+                            for (u32 l = 2; l <= rl; l++) relax(i + l, pr + PC.plen(E_REP_LEN, l - 2, aps), 2 + r, l, rp[r], st_rep(st), nrep);
                             if (i + rl > lim && rl >= 32) lim = std::min<u32>(W, i + rl);
                         }
                         // normal matches
@@ -493,10 +494,34 @@ extern "C" u64 xzm_encode(const u8* s, u32 n, u8* outp, int mode, u32 depth, u32
                     while (end > 0 && opt[end].price == 0xFFFFFFFFu) end--;
                     std::vector<Node> rev;
                     for (u32 j = end; j > 0; j = opt[j].prev) rev.push_back(opt[j]);
-                    path.assign(rev.rbegin(), rev.rend());
+                    outp.assign(rev.rbegin(), rev.rend());
+                };
+                if ((mode == 1 || mode == 3) && path_i >= path.size()) {
+                    plan(p, std::min<u32>(window, n - p), state, reps, path);
                     path_i = 0;
                 }
-                const Node& a = path[path_i++];
+                if (mode == 5 && path_i >= path.size()) {
+                    // G windows planned independently from the same start state / prices
+                    path.clear();
+                    const u32 se = g_seg ? std::min<u32>(n, (p / g_seg + 1) * g_seg) : n;
+                    for (u32 k = 0; k < g_group; k++) {
+                        const u32 p0 = p + k * window;
+                        if (p0 >= se) break;
+                        std::vector<Node> tmp;
+                        plan(p0, std::min<u32>(window, se - p0), state, reps, tmp);
+                        path.insert(path.end(), tmp.begin(), tmp.end());
+                    }
+                    path_i = 0;
+                }
+                Node a = path[path_i++];
+                if (mode == 5) {  // the plan's distances against the actual reps
+                    if (a.kind == 1 && !(p > reps[0] && reps[0] == a.dist)) a.kind = 0;
+                    else if (a.kind >= 2 && a.kind < 6) {
+                        u32 r = 4;
+                        for (u32 k = 0; k < 4 && r == 4; k++) if (reps[k] == a.dist) r = k;
+                        a.kind = r < 4 ? 2 + r : 6;
+                    }
+                }
                 if (a.kind == 0) {
                     enc_lit(p);
                     p += 1;

@@ -27,6 +27,7 @@ def lib():
         subprocess.run(["g++", "-O2", "-shared", "-fPIC", "-o", so, src], check=True)
     L = ctypes.CDLL(so)
     L.xzm_encode.restype = ctypes.c_uint64
+    L.xzm_group.argtypes = [ctypes.c_uint32]
     L.xzm_lclp.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]
     L.xzm_set.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_uint32, ctypes.c_int, ctypes.c_uint32]
     L.xzm_encode.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_int, ctypes.c_uint32,
@@ -45,6 +46,7 @@ def main():
     for sp in specs:
         f = [int(x) for x in sp.split(":")]
         mode, depth, nice, window = f[:4]
+        L.xzm_group(f[12] if len(f) > 12 else 64)
         L.xzm_lclp(f[9] if len(f) > 9 else 3, f[10] if len(f) > 10 else 0, f[11] if len(f) > 11 else 0)
         L.xzm_set(f[4] if len(f) > 4 else 1, f[5] if len(f) > 5 else 0, f[6] if len(f) > 6 else 0, f[7] if len(f) > 7 else 0, f[8] if len(f) > 8 else 0)
         clen = 0

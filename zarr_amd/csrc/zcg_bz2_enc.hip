@@ -472,7 +472,7 @@ __global__ void bze_update(u32 n, u32 h2, const u64* __restrict__ keys, const u3
 // flagged for the global prefix-doubling rounds (whose ranks only need to be
 // at least 4-byte accurate, which refined ranks are).  A tie that reaches
 // the block length is an equal rotation: any order decodes the same.
-constexpr u32 BZE_LC = 2048;
+constexpr u32 BZE_LC = 1024;
 constexpr u32 BZE_LN = 2 * BZE_LC;
 constexpr u32 BZE_LROUNDS = 4;  // (depth 4 + 32 bytes; deeper ties go to the global rounds)
 constexpr u32 BZE_ISORT = 64;   // tie runs up to this long are insertion-sorted by one thread
@@ -537,7 +537,15 @@ __global__ __launch_bounds__(BZE_T) void bze_lds_sort(u32 T, const u8* __restric
     }
     __syncthreads();
     u32 depth = 4;
-    if (tid == 0) s_maxrun = 0xFFFFFFFFu;
+    // the longest group (capped) picks the first round's sort too
+    if (tid == 0) s_maxrun = 0;
+    __syncthreads();
+    for (u32 k = tid; k < n; k += BZE_T) {
+        if (R[k] != k || k + 1 >= n || R[k + 1] != k) continue;
+        u32 e = k + 1;
+        while (e < n && R[e] == k && e - k <= BZE_ISORT) e++;
+        atomicMax(&s_maxrun, e - k);
+    }
     __syncthreads();
     for (u32 round = 0; round < BZE_LROUNDS; round++) {
         if (s_maxrun <= BZE_ISORT) {

@@ -888,8 +888,13 @@ __global__ __launch_bounds__(64) void xo_segment(const zcg_chunk* __restrict__ c
         atomicAdd(&g_xo_prof[3], (unsigned long long)prof[3]);
         atomicAdd(&g_xo_prof[4], (unsigned long long)prof[4]);
         atomicAdd(&g_xo_prof[5], (unsigned long long)tot);
-        for (int q = 0; q < 6; q++) atomicAdd(&g_xo_prof[8 + q], (unsigned long long)prof2[q]);
-        atomicAdd(&g_xo_prof[6], (unsigned long long)(__builtin_amdgcn_s_memrealtime() - rt0));
+        for (int q = 0; q < 5; q++) atomicAdd(&g_xo_prof[8 + q], (unsigned long long)prof2[q]);
+        const u64 rt1 = __builtin_amdgcn_s_memrealtime();
+        atomicAdd(&g_xo_prof[6], (unsigned long long)(rt1 - rt0));
+        atomicMax(&g_xo_prof[7], (unsigned long long)(rt1 - rt0));   // longest wave
+        atomicMax(&g_xo_prof[13], (unsigned long long)rt0);          // last wave start
+        atomicMax(&g_xo_prof[14], (unsigned long long)~rt0);         // ~first wave start
+        atomicMax(&g_xo_prof[15], (unsigned long long)rt1);          // last wave end
     }
 }
 
