@@ -25,7 +25,12 @@
 //      of each range) are priced lane-parallel from the probabilities at the
 //      window start and relaxed by 64-bit LDS atomic minima of
 //      (price, source node, arc), which is the serial restatement's
-//      first-best tie rule; the path is then range-coded symbol by symbol;
+//      first-best tie rule (lanes 16 g .. 16 g + 15 price rep g's lengths,
+//      then candidate g's); the path is then range-coded symbol by symbol.
+//      Residency: LDS is 9.75 KB per wave (the length-price table keeps one
+//      copy of the position-state-free high lengths), so the 138 VGPRs
+//      (3 waves per SIMD, 12 per CU) bind; at 12.8 KB LDS only 11 waves per
+//      CU were admitted and a 1 024-chunk batch (3 072 waves) ran in two rounds;
 //   3. xo_assemble (one wave per chunk): stream and block headers, the
 //      segments' LZMA2 chunks back to back, end mark, padding, CRC64 of the
 //      serialised chunk, index and footer.
@@ -56,6 +61,9 @@ constexpr u64 XO_SUB_BYTES = 128ull << 20;
 constexpr u64 XO_SUPER_BYTES = 1ull << 30;
 constexpr u32 XO_DMAX_LG = 23;  // candidate distances < 2^23 (they pack in 23 bits)
 constexpr u32 ARC_REP = 2, ARC_MATCH = 1100;  // arc ids: 0 literal, 1 short rep, 2 + r*274 + len, 1100 + len
+#ifndef XO_WPE
+#define XO_WPE 3  // waves per SIMD the coder's register allocation targets (LDS admits 4)
+#endif
 #ifndef XO_PROF
 #define XO_PROF 0  // 1 (A/B builds only): cycle and event counters, read by zcg__debug_xz_opt_counters
 #endif
@@ -307,7 +315,8 @@ struct XoLds {
     u64 key[XO_WIN + 1];       // best (price << 20 | source << 11 | arc) of each window node
     union {
         struct {                   // planning: the window's price tables (from the probabilities at its start)
-            u16 len[2][4][272];    //   match / rep length codes by position state and len - 2
+            u16 len[640];          //   match / rep length codes (xo_lenix): l = len - 2 < 16 by position
+                                   //   state, l >= 16 (choice, choice2, high tree: no position state) shared
             u16 slot[4][64];       //   position slots by length state
             u16 spec[128];         //   the reverse-tree low bits of distances 4..127
             u16 align[16];         //   the 4 align bits
@@ -322,6 +331,10 @@ struct XoLds {
     u8 price[128];
 };
 
+// index of length code l = len - 2 of coder c (0 match, 1 rep) at position state ps in XoLds::pt.len
+__device__ __forceinline__ u32 xo_lenix(u32 c, u32 ps, u32 l) {
+    return l < 16 ? (c << 6) + (ps << 4) + l : 128 + (c << 8) + (l - 16);
+}
 __device__ __forceinline__ u32 xo_pb(const XoLds& L, u32 i, u32 b) {
     const u32 p = L.probs[i];
     return L.price[(b ? 2048 - p : p) >> 4];
@@ -399,7 +412,7 @@ __device__ __forceinline__ u32 xo_arc_dist(const u32* __restrict__ wc, u32 src, 
     return (holds(c0) ? c0 : holds(c1) ? c1 : holds(c2) ? c2 : 0u) & 0x7FFFFFu;
 }
 
-__global__ __launch_bounds__(64) void xo_segment(const zcg_chunk* __restrict__ chunks, u32 c0, u64 D, DType t,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(XO_WPE))) void xo_segment(const zcg_chunk* __restrict__ chunks, u32 c0, u64 D, DType t,
                                                  u32 nseg, const u32* __restrict__ cand, u8* __restrict__ segbuf,
                                                  u32* __restrict__ seglen) {
     __shared__ XoLds L;
@@ -522,9 +535,10 @@ __global__ __launch_bounds__(64) void xo_segment(const zcg_chunk* __restrict__ c
                     pL3 = plain((u32)lane + 192);
                 }
                 // length / distance price tables of the window (lane-parallel)
-                for (u32 q = lane; q < 2 * 4 * 272; q += 64) {
-                    const u32 coder = q / 1088, ps4 = (q / 272) & 3, l = q % 272;
-                    (&L.nr.pt.len[0][0][0])[q] = (u16)xo_arc_price(L, coder ? E_REP_LEN : E_LEN, l, ps4, false, 0, 2);
+                for (u32 q = lane; q < 640; q += 64) {
+                    const u32 coder = q < 128 ? q >> 6 : (q - 128) >> 8, ps4 = q < 128 ? (q >> 4) & 3 : 0u,
+                              l = q < 128 ? q & 15 : 16 + ((q - 128) & 255);
+                    L.nr.pt.len[q] = (u16)xo_arc_price(L, coder ? E_REP_LEN : E_LEN, l, ps4, false, 0, 2);
                 }
                 for (u32 q = lane; q < 4 * 64; q += 64) {
                     const u32 lps = q >> 6, sl = q & 63;
@@ -701,49 +715,46 @@ __global__ __launch_bounds__(64) void xo_segment(const zcg_chunk* __restrict__ c
                     }
                     stamp(0);
                     // ---- node t: rep and candidate arcs (lengths >= 2, targets >= t + 2) ----
-                    const u32 rb[4] = {rbase + f[4] + f[11], rbase + f[5] + f[6], rbase + f[5] + f[7] + f[8],
-                                       rbase + f[5] + f[7] + f[9]};
-                    const u32 rl[4] = {rl0, rl1, rl2, rl3};
-                    u32 cnt[7], ga[7], gc1[7], gh[7], gd[7];
-                    for (u32 r = 0; r < 4; r++) {
-                        ga[r] = 2;
-                        cnt[r] = rl[r] >= 2 ? xo_range_count(2, rl[r], &gc1[r], &gh[r]) : 0u;
-                        gd[r] = 0;
+                    // Lanes 16 r .. 16 r + 15 price rep r's kept lengths (at most 10),
+                    // then lanes 16 c .. 16 c + 15 candidate c's (c < 3); every
+                    // lane's group is fixed, so no lane searches for its arc.
+                    const u32 gl = (u32)lane >> 4, el = (u32)lane & 15;
+                    {
+                        const u32 rlg = gl == 0 ? rl0 : gl == 1 ? rl1 : gl == 2 ? rl2 : rl3;
+                        const u32 rbg = rbase + (gl == 0 ? f[4] + f[11] : gl == 1 ? f[5] + f[6] : f[5] + f[7] + (gl == 2 ? f[8] : f[9]));
+                        u32 c1, h;
+                        const u32 cn = rlg >= 2 ? xo_range_count(2, rlg, &c1, &h) : 0u;
+                        if (el < cn) {
+                            const u32 len = el < c1 ? 2 + el : h + (el - c1);
+                            const u32 price = rbg + L.nr.pt.len[xo_lenix(1, ps, len - 2)];
+                            const u64 key = ((u64)price << 20) | ((u64)t << 11) | (ARC_REP + gl * 274 + len);
+                            atomicMin((unsigned long long*)&L.key[t + len], (unsigned long long)key);
+                        }
                     }
-                    u32 lprev = 1;
-                    for (u32 c = 0; c < XO_K; c++) {
-                        const u32 w = wk[c], Lk = w >> 23;
-                        const u32 Lr = Lk < mx ? Lk : mx;
-                        const u32 a0 = lprev + 1 > 2 ? lprev + 1 : 2;
-                        ga[4 + c] = a0;
-                        gd[4 + c] = w & 0x7FFFFFu;
-                        cnt[4 + c] = Lk ? xo_range_count(a0, Lr, &gc1[4 + c], &gh[4 + c]) : 0u;
-                        if (Lk && Lr > lprev) lprev = Lr;
-                    }
-                    u32 N = 0;
-                    for (u32 g = 0; g < 7; g++) N += cnt[g];
-                    const u32 mb0 = P + f[1] + f[2];
                     stamp(3);
-                    for (u32 base = 0; base < N; base += 64) {
-                        const u32 j = base + (u32)lane;
-                        if (j < N) {
-                            u32 g = 0, acc = 0;
-                            while (j >= acc + cnt[g]) { acc += cnt[g]; g++; }
-                            const u32 el = j - acc;
-                            const u32 len = el < gc1[g] ? ga[g] + el : gh[g] + (el - gc1[g]);
-                            u32 price, arc;
-                            if (g < 4) {
-                                price = rb[g] + L.nr.pt.len[1][ps][len - 2];
-                                arc = ARC_REP + g * 274 + len;
-                            } else {
-                                const u32 d = gd[g], lps = len - 2 < 3 ? len - 2 : 3, sl = slot_of(d);
-                                u32 dp = L.nr.pt.slot[lps][sl];
-                                if (sl >= 14) dp += (((sl >> 1) - 1) - 4) * 16 + L.nr.pt.align[d & 15];
-                                else if (sl >= 4) dp += L.nr.pt.spec[d];
-                                price = mb0 + L.nr.pt.len[0][ps][len - 2] + dp;
-                                arc = ARC_MATCH + len;
-                            }
-                            const u64 key = ((u64)price << 20) | ((u64)t << 11) | arc;
+                    {
+                        // candidate c's lengths start past the longer ones before it
+                        u32 a0[XO_K], lr[XO_K], lprev = 1;
+#pragma unroll
+                        for (u32 c = 0; c < XO_K; c++) {
+                            const u32 Lk = wk[c] >> 23;
+                            lr[c] = Lk < mx ? Lk : mx;
+                            a0[c] = lprev + 1 > 2 ? lprev + 1 : 2;
+                            if (Lk && lr[c] > lprev) lprev = lr[c];
+                        }
+                        const u32 wg = gl == 0 ? wk[0] : gl == 1 ? wk[1] : wk[2];
+                        const u32 ag = gl == 0 ? a0[0] : gl == 1 ? a0[1] : a0[2];
+                        const u32 lg = gl == 0 ? lr[0] : gl == 1 ? lr[1] : lr[2];
+                        u32 c1, h;
+                        const u32 cn = gl < XO_K && (wg >> 23) ? xo_range_count(ag, lg, &c1, &h) : 0u;
+                        if (el < cn) {
+                            const u32 len = el < c1 ? ag + el : h + (el - c1);
+                            const u32 d = wg & 0x7FFFFFu, lps = len - 2 < 3 ? len - 2 : 3, sl = slot_of(d);
+                            u32 dp = L.nr.pt.slot[lps][sl];
+                            if (sl >= 14) dp += (((sl >> 1) - 1) - 4) * 16 + L.nr.pt.align[d & 15];
+                            else if (sl >= 4) dp += L.nr.pt.spec[d];
+                            const u32 price = P + f[1] + f[2] + L.nr.pt.len[xo_lenix(0, ps, len - 2)] + dp;
+                            const u64 key = ((u64)price << 20) | ((u64)t << 11) | (ARC_MATCH + len);
                             atomicMin((unsigned long long*)&L.key[t + len], (unsigned long long)key);
                         }
                     }
