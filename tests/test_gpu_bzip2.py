@@ -94,3 +94,24 @@ def test_bzip2_two_streams_one_context():
         out = p.dst.cpu().numpy().reshape(p.n, D)
         for i in range(p.n):
             assert out[i].tobytes() == vals[base + i % 3]
+
+
+def test_bzip2_mixed_batch():
+    """A 640-chunk batch of valid, truncated and corrupted streams (several
+    rounds' worth of pending / finished chunks side by side) vs the oracle."""
+    rng = np.random.default_rng(31)
+    payloads = [rw(60000, seed=s).tobytes() for s in range(4)] + [bytes(120000)]
+    base = [bz2.compress(p, 1 + 4 * (i % 3)) for i, p in enumerate(payloads)]
+    streams = []
+    for i in range(640):
+        s = base[i % len(base)]
+        u = rng.random()
+        if u < 0.15:
+            s = s[:int(rng.integers(0, len(s)))]
+        elif u < 0.35:
+            b = bytearray(s)
+            b[int(rng.integers(0, len(b)))] ^= int(rng.integers(1, 256))
+            s = bytes(b)
+        streams.append(s)
+    for D in (120000, 60000):
+        check_many("bzip2", streams, "u1", D)

@@ -415,7 +415,9 @@ __global__ void bze_rank0(u32 T, const u64* __restrict__ keys, const u32* __rest
     sa[p] = i;
     const bool head = (p == 0) || keys[p] != keys[p - 1];
     const bool nhead = (p + 1 == T) || keys[p + 1] != keys[p];
-    const u32 len = gb[blkof[i]].len;
+    // the keys lead with the block index, so SA position p lies in the same
+    // block as text position i: blkof[p] is a coalesced read, blkof[i] a gather
+    const u32 len = gb[blkof[p]].len;
     flags[p] = (!(head && nhead) && 4u < len) ? 1 : 0;
 }
 
@@ -425,11 +427,12 @@ __global__ void bze_keys(u32 n, u32 h, u32 rb, const u32* __restrict__ U, const 
     const u32 j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= n) return;
     const u32 i = U[j];
-    const u32 b = blkof[i];
+    const u32 ri = rank[i];
+    const u32 b = blkof[ri];  // the group head's SA position is in i's block (U is in SA order: ascending reads)
     const u32 s = gb[b].start, len = gb[b].len;
     u32 nx = i + h;  // h < len for every kept position
     if (nx >= s + len) nx -= len;
-    keys[j] = ((u64)rank[i] << rb) | rank[nx];
+    keys[j] = ((u64)ri << rb) | rank[nx];
     vals[j] = i;
 }
 
@@ -445,7 +448,7 @@ __global__ void bze_sapos(u32 n, u32 rb, const u64* __restrict__ keys, const u32
     out[j] = sub ? sp : 0u;
 }
 
-__global__ void bze_update(u32 n, u32 h2, const u64* __restrict__ keys, const u32* __restrict__ vals,
+__global__ void bze_update(u32 n, u32 h2, u32 rb, const u64* __restrict__ keys, const u32* __restrict__ vals,
                            const u32* __restrict__ newrank, const u32* __restrict__ blkof,
                            const BzeBlk* __restrict__ gb, u32* __restrict__ rank, u8* __restrict__ flags) {
     const u32 j = blockIdx.x * blockDim.x + threadIdx.x;
@@ -455,7 +458,7 @@ __global__ void bze_update(u32 n, u32 h2, const u64* __restrict__ keys, const u3
     const u64 k = keys[j];
     const bool head = (j == 0) || k != keys[j - 1];
     const bool nhead = (j + 1 == n) || keys[j + 1] != k;
-    const u32 len = gb[blkof[i]].len;
+    const u32 len = gb[blkof[(u32)(k >> rb)]].len;  // (the old group head: same block, ascending)
     flags[j] = (!(head && nhead) && h2 < len) ? 1 : 0;
 }
 
@@ -522,7 +525,7 @@ __global__ __launch_bounds__(BZE_T) void bze_lds_sort(u32 T, const u8* __restric
             const u32 p = a + k, pos = sa[p];
             P[k] = pos;
             if (flags[p]) {
-                const u32 bi = blkof[pos], st = gb[bi].start, len = gb[bi].len;
+                const u32 bi = blkof[p], st = gb[bi].start, len = gb[bi].len;  // (SA and text ranges of a block coincide)
                 R[k] = headpos[p] - a;
                 K[k] = bze_key8(text, st, len, (pos - st + 4) % len);
             } else {
@@ -609,7 +612,7 @@ __global__ __launch_bounds__(BZE_T) void bze_lds_sort(u32 T, const u8* __restric
             if (q < per && k < n) {
                 if (k == 0 || R[k] != R[k - 1] || K[k] != K[k - 1]) hd = k;
                 const bool next_same = k + 1 < n && R[k + 1] == R[k] && K[k + 1] == K[k];
-                if ((hd != k || next_same) && depth + 8 < gb[blkof[P[k]]].len) tiebits |= 1u << q;
+                if ((hd != k || next_same) && depth + 8 < gb[blkof[a + k]].len) tiebits |= 1u << q;
             }
             hdq[q] = hd;
         }
@@ -620,7 +623,7 @@ __global__ __launch_bounds__(BZE_T) void bze_lds_sort(u32 T, const u8* __restric
             if (q >= per || k >= n) continue;
             const u32 heads_q = hdq[q];
             if ((tiebits >> q) & 1u) {
-                const u32 pos = P[k], bi = blkof[pos], st = gb[bi].start, len = gb[bi].len;
+                const u32 pos = P[k], bi = blkof[a + k], st = gb[bi].start, len = gb[bi].len;
                 R[k] = heads_q;
                 K[k] = bze_key8(text, st, len, (pos - st + depth + 8) % len);
                 s_tied = 1;
@@ -1281,7 +1284,7 @@ hipError_t launch_bzip2_encode(const zcg_array* a, const zcg_chunk* d_chunks, ui
                 if ((e = hipcub::DeviceScan::InclusiveScan(cub, cb, sA, sB, MaxU32(), (int)cntU, s)) != hipSuccess)
                     return e;
                 const u32 h2 = (h >= 0x80000000u) ? 0xFFFFFFFFu : 2 * h;
-                hipLaunchKernelGGL(bze_update, dim3(G), dim3(TB), 0, s, cntU, h2, k2.Current(), v2.Current(), sB,
+                hipLaunchKernelGGL(bze_update, dim3(G), dim3(TB), 0, s, cntU, h2, rb, k2.Current(), v2.Current(), sB,
                                    blkof, gb, rank, flags);
                 cb = y.cub_bytes;
                 if ((e = hipcub::DeviceSelect::Flagged(cub, cb, v2.Current(), flags, U, d_nsel, (int)cntU, s)) !=
