@@ -11,7 +11,7 @@
 //     links, distances < the preset's dictionary and < 2^23) keeping strictly
 //     longer matches (>= 4; stop at 64 bytes or the maximum); the three
 //     longest candidates are kept (lengths ascending);
-//   * the chunk is coded in 352 KiB segments, each an independent LZMA2 run:
+//   * the chunk is coded in 256 KiB segments, each an independent LZMA2 run:
 //     a state reset (+ properties) at its first LZMA chunk, the dictionary
 //     shared (segment 0's first chunk resets it); LZMA lc=0 lp=0 pb=2;
 //   * the parse: windows of <= 256 positions (clipped to the segment end);
@@ -41,7 +41,10 @@ enum : u32 {
     E_LITERAL = 1846, XO_PROBS = 1846 + 0x300
 };
 enum : u32 { EL_CHOICE = 0, EL_CHOICE2 = 1, EL_LOW = 2, EL_MID = 130, EL_HIGH = 258 };
-constexpr u32 XO_SEG = 352u << 10, XO_WIN = 256, XO_K = 3, XO_DEPTH = 16, XO_NICE = 64, XO_W2 = 64, XO_LENS = 8;
+#ifndef XO_SEG_KB
+#define XO_SEG_KB 256
+#endif
+constexpr u32 XO_SEG = XO_SEG_KB << 10, XO_WIN = 256, XO_K = 3, XO_DEPTH = 16, XO_NICE = 64, XO_W2 = 64, XO_LENS = 8;
 constexpr u32 XO_CMAX = 65536 - 64, XO_MAXLEN = 273;
 constexpr u32 XO_PROPS = (2 * 5 + 0) * 9 + 0;  // pb=2 lp=0 lc=0
 

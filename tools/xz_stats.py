@@ -58,7 +58,8 @@ ms = float(np.median(ts))
 res = {"n": n, "ms": round(ms, 2), "gibs": round(n * D / 2**30 / (ms * 1e-3), 3), "ratio": round(ratio, 4),
        "status_ok": int((st == 0).sum()), "sample_decodes": ok}
 if prof and cnt[5]:
-    segs = n * ((D + (352 << 10) - 1) // (352 << 10))
+    seg = int(os.environ.get("XO_SEG_KB", "256")) << 10
+    segs = n * ((D + seg - 1) // seg)
     res["prof"] = {"plan_share": round(cnt[0] / cnt[5], 3), "code_share": round(cnt[1] / cnt[5], 3),
                    "cycles_per_node_plan": round(cnt[0] / max(1, cnt[2]), 1),
                    "cycles_per_symbol_code": round(cnt[1] / max(1, cnt[3]), 1),

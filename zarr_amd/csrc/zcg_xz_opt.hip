@@ -16,10 +16,10 @@
 //      close matches price well on numeric data) to the strictly-longer
 //      chain matches (16 links, < 2^23 back) and keeps the 3 longest,
 //      packed len << 23 | dist;
-//   2. xo_segment (one wave per 352 KiB segment of a chunk): each segment is
+//   2. xo_segment (one wave per 256 KiB segment of a chunk): each segment is
 //      an independent LZMA2 run — its first LZMA chunk resets the state and
 //      sets the properties (lc=0 lp=0 pb=2: 2.6 K probabilities in LDS), the
-//      dictionary is shared — so a 1 MiB chunk is coded by 3 waves at once.
+//      dictionary is shared — so a 1 MiB chunk is coded by 4 waves at once.
 //      The parse plans windows of <= 256 positions: node i's arcs (literal,
 //      short rep, rep0-3, candidate matches; lengths 2..8 and the last three
 //      of each range) are priced lane-parallel from the probabilities at the
@@ -27,10 +27,11 @@
 //      (price, source node, arc), which is the serial restatement's
 //      first-best tie rule (lanes 16 g .. 16 g + 15 price rep g's lengths,
 //      then candidate g's); the path is then range-coded symbol by symbol.
-//      Residency: LDS is 9.75 KB per wave (the length-price table keeps one
-//      copy of the position-state-free high lengths), so the 138 VGPRs
-//      (3 waves per SIMD, 12 per CU) bind; at 12.8 KB LDS only 11 waves per
-//      CU were admitted and a 1 024-chunk batch (3 072 waves) ran in two rounds;
+//      Residency: 9.75 KB of LDS per wave (the length-price table keeps one
+//      copy of the position-state-free high lengths) and 128 VGPRs (prices
+//      packed two per register) admit 4 waves per SIMD, so a 1 024-chunk
+//      batch (4 096 waves) is one generation; at 12.8 KB of LDS only 11
+//      waves per CU were admitted;
 //   3. xo_assemble (one wave per chunk): stream and block headers, the
 //      segments' LZMA2 chunks back to back, end mark, padding, CRC64 of the
 //      serialised chunk, index and footer.
@@ -41,7 +42,10 @@ namespace zcg {
 
 namespace {
 
-constexpr u32 XO_SEG = 352u << 10;  // bytes per independently coded segment (a 1 MiB chunk: 3 waves)
+#ifndef XO_SEG_KB
+#define XO_SEG_KB 256
+#endif
+constexpr u32 XO_SEG = XO_SEG_KB << 10;  // bytes per independently coded segment (a 1 MiB chunk: 4 waves)
 constexpr u32 XO_WIN = 256;        // parse window (positions)
 constexpr u32 XO_K = 3;            // candidates kept per position
 constexpr u32 XO_DEPTH = 16;       // hash-chain links walked
@@ -62,7 +66,7 @@ constexpr u64 XO_SUPER_BYTES = 1ull << 30;
 constexpr u32 XO_DMAX_LG = 23;  // candidate distances < 2^23 (they pack in 23 bits)
 constexpr u32 ARC_REP = 2, ARC_MATCH = 1100;  // arc ids: 0 literal, 1 short rep, 2 + r*274 + len, 1100 + len
 #ifndef XO_WPE
-#define XO_WPE 3  // waves per SIMD the coder's register allocation targets (LDS admits 4)
+#define XO_WPE 4  // waves per SIMD the coder's register allocation targets (LDS admits 4)
 #endif
 #ifndef XO_PROF
 #define XO_PROF 0  // 1 (A/B builds only): cycle and event counters, read by zcg__debug_xz_opt_counters
@@ -507,32 +511,26 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(XO_WPE))) vo
                 // per node with v_readlane (no LDS round trip): lane st*4+ps
                 // holds is_match / is_rep0_long of (state, pos state), lane st
                 // the is_rep / rep_g0-2 pairs, lane l the literals l + 64 k.
-                u32 pIM0, pIM1, pRL0, pRL1, pIR0, pIR1, pG00, pG01, pG10, pG11, pG20, pG21, pL0, pL1, pL2, pL3;
+                // (two 16-bit prices per register: bit value 0 low, 1 high; literals l and l + 64 (+ 128))
+                u32 pIM, pRL, pIR, pG0, pG1, pG2, pL01, pL23;
                 {
                     const u32 sp = (u32)lane < 48 ? (u32)lane : 0u, st4 = sp >> 2, ps4 = sp & 3;
-                    pIM0 = xo_pb(L, E_IS_MATCH + (st4 << 4) + ps4, 0);
-                    pIM1 = xo_pb(L, E_IS_MATCH + (st4 << 4) + ps4, 1);
-                    pRL0 = xo_pb(L, E_IS_REP0_LONG + (st4 << 4) + ps4, 0);
-                    pRL1 = xo_pb(L, E_IS_REP0_LONG + (st4 << 4) + ps4, 1);
+                    auto pair = [&](u32 i) { return xo_pb(L, i, 0) | (xo_pb(L, i, 1) << 16); };
+                    pIM = pair(E_IS_MATCH + (st4 << 4) + ps4);
+                    pRL = pair(E_IS_REP0_LONG + (st4 << 4) + ps4);
                     const u32 s1 = (u32)lane < 12 ? (u32)lane : 0u;
-                    pIR0 = xo_pb(L, E_IS_REP + s1, 0);
-                    pIR1 = xo_pb(L, E_IS_REP + s1, 1);
-                    pG00 = xo_pb(L, E_IS_REP_G0 + s1, 0);
-                    pG01 = xo_pb(L, E_IS_REP_G0 + s1, 1);
-                    pG10 = xo_pb(L, E_IS_REP_G1 + s1, 0);
-                    pG11 = xo_pb(L, E_IS_REP_G1 + s1, 1);
-                    pG20 = xo_pb(L, E_IS_REP_G2 + s1, 0);
-                    pG21 = xo_pb(L, E_IS_REP_G2 + s1, 1);
+                    pIR = pair(E_IS_REP + s1);
+                    pG0 = pair(E_IS_REP_G0 + s1);
+                    pG1 = pair(E_IS_REP_G1 + s1);
+                    pG2 = pair(E_IS_REP_G2 + s1);
                     auto plain = [&](u32 sym) {
                         u32 sum = 0;
 #pragma unroll
                         for (u32 j = 0; j < 8; j++) sum += xo_pb(L, E_LITERAL + ((1u << j) | (sym >> (8 - j))), (sym >> (7 - j)) & 1);
                         return sum;
                     };
-                    pL0 = plain((u32)lane);
-                    pL1 = plain((u32)lane + 64);
-                    pL2 = plain((u32)lane + 128);
-                    pL3 = plain((u32)lane + 192);
+                    pL01 = plain((u32)lane) | (plain((u32)lane + 64) << 16);
+                    pL23 = plain((u32)lane + 128) | (plain((u32)lane + 192) << 16);
                 }
                 // length / distance price tables of the window (lane-parallel)
                 for (u32 q = lane; q < 640; q += 64) {
@@ -653,8 +651,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(XO_WPE))) vo
                     u32 litp;
                     if (st < 7) {
                         const u32 hi = sym >> 6, lo = sym & 63;
-                        const u32 v = hi == 0 ? pL0 : hi == 1 ? pL1 : hi == 2 ? pL2 : pL3;
-                        litp = (u32)__builtin_amdgcn_readlane((int)v, (int)lo);
+                        const u32 v = (u32)__builtin_amdgcn_readlane((int)(hi < 2 ? pL01 : pL23), (int)lo);
+                        litp = (hi & 1) ? v >> 16 : v & 0xFFFFu;
                     } else {
                         u32 pv = 0;
                         if (lane < 8) {
@@ -667,12 +665,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(XO_WPE))) vo
                         for (int j = 0; j < 8; j++) litp += (u32)__builtin_amdgcn_readlane((int)pv, j);
                     }
                     const int sps = (int)(st * 4 + ps), sst = (int)st;
-                    const u32 f[12] = {(u32)__builtin_amdgcn_readlane((int)pIM0, sps), (u32)__builtin_amdgcn_readlane((int)pIM1, sps),
-                                       (u32)__builtin_amdgcn_readlane((int)pIR0, sst), (u32)__builtin_amdgcn_readlane((int)pIR1, sst),
-                                       (u32)__builtin_amdgcn_readlane((int)pG00, sst), (u32)__builtin_amdgcn_readlane((int)pG01, sst),
-                                       (u32)__builtin_amdgcn_readlane((int)pG10, sst), (u32)__builtin_amdgcn_readlane((int)pG11, sst),
-                                       (u32)__builtin_amdgcn_readlane((int)pG20, sst), (u32)__builtin_amdgcn_readlane((int)pG21, sst),
-                                       (u32)__builtin_amdgcn_readlane((int)pRL0, sps), (u32)__builtin_amdgcn_readlane((int)pRL1, sps)};
+                    const u32 fIM = (u32)__builtin_amdgcn_readlane((int)pIM, sps), fIR = (u32)__builtin_amdgcn_readlane((int)pIR, sst),
+                              fG0 = (u32)__builtin_amdgcn_readlane((int)pG0, sst), fG1 = (u32)__builtin_amdgcn_readlane((int)pG1, sst),
+                              fG2 = (u32)__builtin_amdgcn_readlane((int)pG2, sst), fRL = (u32)__builtin_amdgcn_readlane((int)pRL, sps);
+                    const u32 f[12] = {fIM & 0xFFFFu, fIM >> 16, fIR & 0xFFFFu, fIR >> 16, fG0 & 0xFFFFu, fG0 >> 16,
+                                       fG1 & 0xFFFFu, fG1 >> 16, fG2 & 0xFFFFu, fG2 >> 16, fRL & 0xFFFFu, fRL >> 16};
                     stamp(2);
                     // ---- node t + 1: final key (min with node t's literal / short rep), state, reps ----
                     const bool sr = at > q0 && sym == mbyte;
