@@ -463,6 +463,22 @@ def test_bzip2_encode_roundtrip(kind, level):
         assert back.tobytes() == content
 
 
+def test_bzip2_encode_many_blocks():
+    """More than 256 blocks in one sort sub-batch (level 1: ~11 blocks per
+    1 MiB chunk, 28 chunks): the first rotation sort keys then hold 2 prefix
+    bytes under 9+ block-index bits instead of 3 (zcg_bz2_enc.hip
+    bze_init_keys)."""
+    from zarr_amd.compression import Bzip2
+    D = 1 << 20
+    kinds = ["randwalk", "text", "mixed", "uniform"]
+    arrays = [_data(kinds[i % 4], D, seed=i) for i in range(28)]
+    meta = ArrayMetadata.new([D * 28], [D], "u1", Bzip2(1))
+    st, outs = encode_batch(meta, arrays)
+    assert (st == 0).all()
+    for a, s in zip(arrays, outs):
+        check_bz2_stream(s, a.tobytes(), 1)
+
+
 @pytest.mark.parametrize("nbytes", [1, 2, 3, 4, 5, 6, 255, 256, 259, 1000, 99981, 100000, 300001])
 def test_bzip2_encode_edge_sizes(nbytes):
     from zarr_amd.compression import Bzip2

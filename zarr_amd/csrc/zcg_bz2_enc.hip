@@ -172,6 +172,10 @@ u64 cub_temp_bytes(u64 tmax) {
     hipcub::DoubleBuffer<u64> k(nullptr, nullptr);
     hipcub::DoubleBuffer<u32> v(nullptr, nullptr);
     (void)hipcub::DeviceRadixSort::SortPairs(nullptr, b1, k, v, (int)tmax, 0, 62);
+    size_t b4 = 0;
+    hipcub::DoubleBuffer<u32> k32(nullptr, nullptr);
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, b4, k32, v, (int)tmax, 0, 32);
+    b1 = b1 > b4 ? b1 : b4;
     (void)hipcub::DeviceScan::InclusiveScan(nullptr, b2, (u32*)nullptr, (u32*)nullptr, MaxU32(), (int)tmax);
     (void)hipcub::DeviceSelect::Flagged(nullptr, b3, (u32*)nullptr, (u8*)nullptr, (u32*)nullptr,
                                         (u32*)nullptr, (int)tmax);
@@ -341,7 +345,7 @@ __global__ void bze_layout(u32 cnt, BzeLayout y, u8* __restrict__ ws) {
             g.chunk = c;
             g.orig = 0;
             g.nbits = 0;
-            g.sym_off = g.start + NB;  // room for the EOB symbol of every block
+            g.sym_off = g.start + NB + k;  // room for the EOB symbol of every block (nMTF <= len + 1)
             g.pad = 0;
             g.out_off = out;
             g.out_cap = ((u64)l.len * 17 / 8 + 24576 + 256) & ~15ull;
@@ -379,24 +383,30 @@ __global__ __launch_bounds__(BZE_T) void bze_compact(u32 cnt, BzeLayout y, u8* _
 }
 
 // ---- 4. prefix-doubling rotation sort -------------------------------------------------
+// The first sort's 32-bit key: the block index above the rotation's first
+// dpre bytes (dpre = 3 while the sub-batch has <= 256 blocks, fewer bytes
+// for more blocks), so one 4-pass radix sort of (u32, u32) pairs orders all
+// blocks' rotations by their prefixes.
 __global__ void bze_init_keys(u32 T, const u8* __restrict__ text, const u32* __restrict__ blkof,
-                              const BzeBlk* __restrict__ gb, u64* __restrict__ keys, u32* __restrict__ vals) {
+                              const BzeBlk* __restrict__ gb, u32 dpre, u32* __restrict__ keys,
+                              u32* __restrict__ vals) {
     const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= T) return;
     const u32 b = blkof[i];
     const u32 s = gb[b].start, n = gb[b].len;
     u32 loc = i - s;
     u32 v = 0;
-    for (int d = 0; d < 4; d++) {
+    for (u32 d = 0; d < dpre; d++) {
         v = (v << 8) | text[s + loc];
         loc = (loc + 1 == n) ? 0u : loc + 1;
     }
-    keys[i] = ((u64)b << 32) | v;
+    keys[i] = (b << (8 * dpre)) | v;
     vals[i] = i;
 }
 
 // head positions of equal-key runs (scanned with max -> first index of the run)
-__global__ void bze_heads(u32 n, const u64* __restrict__ keys, u32 shift, u32* __restrict__ out) {
+template <typename K>
+__global__ void bze_heads(u32 n, const K* __restrict__ keys, u32 shift, u32* __restrict__ out) {
     const u32 j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= n) return;
     const bool h = (j == 0) || ((keys[j] >> shift) != (keys[j - 1] >> shift));
@@ -404,9 +414,9 @@ __global__ void bze_heads(u32 n, const u64* __restrict__ keys, u32 shift, u32* _
 }
 
 // first sort: SA, ranks, and the unresolved positions
-__global__ void bze_rank0(u32 T, const u64* __restrict__ keys, const u32* __restrict__ vals,
+__global__ void bze_rank0(u32 T, const u32* __restrict__ keys, const u32* __restrict__ vals,
                           const u32* __restrict__ headpos, const u32* __restrict__ blkof,
-                          const BzeBlk* __restrict__ gb, u32* __restrict__ rank, u32* __restrict__ sa,
+                          const BzeBlk* __restrict__ gb, u32 dpre, u32* __restrict__ rank, u32* __restrict__ sa,
                           u8* __restrict__ flags) {
     const u32 p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= T) return;
@@ -418,7 +428,7 @@ __global__ void bze_rank0(u32 T, const u64* __restrict__ keys, const u32* __rest
     // the keys lead with the block index, so SA position p lies in the same
     // block as text position i: blkof[p] is a coalesced read, blkof[i] a gather
     const u32 len = gb[blkof[p]].len;
-    flags[p] = (!(head && nhead) && 4u < len) ? 1 : 0;
+    flags[p] = (!(head && nhead) && dpre < len) ? 1 : 0;
 }
 
 __global__ void bze_keys(u32 n, u32 h, u32 rb, const u32* __restrict__ U, const u32* __restrict__ rank,
@@ -492,8 +502,9 @@ __device__ __forceinline__ u64 bze_key8(const u8* __restrict__ text, u32 s, u32 
 
 __global__ __launch_bounds__(BZE_T) void bze_lds_sort(u32 T, const u8* __restrict__ text,
                                                       const u32* __restrict__ blkof, const BzeBlk* __restrict__ gb,
-                                                      const u32* __restrict__ headpos, u32* __restrict__ sa,
-                                                      u32* __restrict__ rank, u8* __restrict__ flags) {
+                                                      const u32* __restrict__ headpos, u32 dpre,
+                                                      u32* __restrict__ sa, u32* __restrict__ rank,
+                                                      u8* __restrict__ flags) {
     __shared__ u64 K[BZE_LN];
     __shared__ u32 R[BZE_LN];
     __shared__ u32 P[BZE_LN];
@@ -527,7 +538,7 @@ __global__ __launch_bounds__(BZE_T) void bze_lds_sort(u32 T, const u8* __restric
             if (flags[p]) {
                 const u32 bi = blkof[p], st = gb[bi].start, len = gb[bi].len;  // (SA and text ranges of a block coincide)
                 R[k] = headpos[p] - a;
-                K[k] = bze_key8(text, st, len, (pos - st + 4) % len);
+                K[k] = bze_key8(text, st, len, (pos - st + dpre) % len);
             } else {
                 R[k] = k;
                 K[k] = 0;
@@ -539,7 +550,7 @@ __global__ __launch_bounds__(BZE_T) void bze_lds_sort(u32 T, const u8* __restric
         }
     }
     __syncthreads();
-    u32 depth = 4;
+    u32 depth = dpre;
     // the longest group (capped) picks the first round's sort too
     if (tid == 0) s_maxrun = 0;
     __syncthreads();
@@ -1245,27 +1256,30 @@ hipError_t launch_bzip2_encode(const zcg_array* a, const zcg_chunk* d_chunks, ui
             while ((1u << nbits_blk) < NB) nbits_blk++;
             u32 rb = 1;
             while ((1ull << rb) < T) rb++;
-            hipLaunchKernelGGL(bze_init_keys, dim3((T + TB - 1) / TB), dim3(TB), 0, s, T, text, blkof, gb, ka, va);
+            if (nbits_blk > 24) return hipErrorInvalidValue;
+            const u32 dpre = (32 - nbits_blk) / 8 < 3 ? (32 - nbits_blk) / 8 : 3u;
+            hipLaunchKernelGGL(bze_init_keys, dim3((T + TB - 1) / TB), dim3(TB), 0, s, T, text, blkof, gb, dpre,
+                               (u32*)ka, va);
             size_t cb = y.cub_bytes;
-            hipcub::DoubleBuffer<u64> dk(ka, kb);
+            hipcub::DoubleBuffer<u32> dk((u32*)ka, (u32*)kb);
             hipcub::DoubleBuffer<u32> dv(va, vb);
-            if ((e = hipcub::DeviceRadixSort::SortPairs(cub, cb, dk, dv, (int)T, 0, (int)(32 + nbits_blk), s)) !=
+            if ((e = hipcub::DeviceRadixSort::SortPairs(cub, cb, dk, dv, (int)T, 0, (int)(8 * dpre + nbits_blk), s)) !=
                 hipSuccess)
                 return e;
-            hipLaunchKernelGGL(bze_heads, dim3((T + TB - 1) / TB), dim3(TB), 0, s, T, dk.Current(), 0u, sA);
+            hipLaunchKernelGGL(bze_heads<u32>, dim3((T + TB - 1) / TB), dim3(TB), 0, s, T, dk.Current(), 0u, sA);
             cb = y.cub_bytes;
             if ((e = hipcub::DeviceScan::InclusiveScan(cub, cb, sA, sB, MaxU32(), (int)T, s)) != hipSuccess) return e;
             hipLaunchKernelGGL(bze_rank0, dim3((T + TB - 1) / TB), dim3(TB), 0, s, T, dk.Current(), dv.Current(), sB,
-                               blkof, gb, rank, sa, flags);
+                               blkof, gb, dpre, rank, sa, flags);
             hipLaunchKernelGGL(bze_lds_sort, dim3((T + BZE_LC - 1) / BZE_LC), dim3(BZE_T), 0, s, T, text, blkof, gb, sB,
-                               sa, rank, flags);
+                               dpre, sa, rank, flags);
             cb = y.cub_bytes;
             if ((e = hipcub::DeviceSelect::Flagged(cub, cb, sa, flags, U, d_nsel, (int)T, s)) != hipSuccess)
                 return e;
             u32 cntU = 0;
             if ((e = hipMemcpyAsync(&cntU, d_nsel, 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
             if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
-            for (u32 h = 4; cntU > 0; h *= 2) {
+            for (u32 h = dpre; cntU > 0; h *= 2) {
                 const u32 G = (cntU + TB - 1) / TB;
                 hipLaunchKernelGGL(bze_keys, dim3(G), dim3(TB), 0, s, cntU, h, rb, U, rank, blkof, gb, ka, va);
                 hipcub::DoubleBuffer<u64> k2(ka, kb);
@@ -1274,7 +1288,7 @@ hipError_t launch_bzip2_encode(const zcg_array* a, const zcg_chunk* d_chunks, ui
                 if ((e = hipcub::DeviceRadixSort::SortPairs(cub, cb, k2, v2, (int)cntU, 0, (int)(2 * rb), s)) !=
                     hipSuccess)
                     return e;
-                hipLaunchKernelGGL(bze_heads, dim3(G), dim3(TB), 0, s, cntU, k2.Current(), rb, sA);
+                hipLaunchKernelGGL(bze_heads<u64>, dim3(G), dim3(TB), 0, s, cntU, k2.Current(), rb, sA);
                 cb = y.cub_bytes;
                 if ((e = hipcub::DeviceScan::InclusiveScan(cub, cb, sA, sB, MaxU32(), (int)cntU, s)) != hipSuccess)
                     return e;
