@@ -44,6 +44,15 @@ struct XzHostIO {
         for (uint64_t i = a; i < b; i++)
             if (i >= a + dist) dst[i] = (uint8_t)(dst[i] + dst[i - dist]);
     }
+    struct Buf {
+        uint8_t* p;
+        uint32_t get(uint64_t i) const { return p[i]; }
+        void set(uint64_t i, uint32_t v) { p[i] = (uint8_t)v; }
+    };
+    void apply_bcj(uint64_t a, uint64_t b, uint32_t id, uint32_t start) {
+        Buf buf{dst + a};
+        zx::bcj_serial(buf, b - a, id, start);
+    }
     uint64_t check(uint32_t id, uint64_t a, uint64_t b) const {
         if (id == 4) {
             uint64_t c = ~0ull;

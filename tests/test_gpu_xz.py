@@ -118,12 +118,40 @@ def test_xz_delta_filter_dtypes():
         check("xz", s, dt, v.nbytes)
 
 
+@pytest.mark.parametrize("name", ["X86", "ARM", "ARMTHUMB", "POWERPC", "SPARC", "IA64"])
+def test_xz_bcj_filters(name):
+    """BCJ + LZMA2 chains (liblzma simple/*.c) against the oracle's liblzma:
+    whole reads, reads past the end, reads that stop inside the block (at
+    the sizes the host core decodes exactly rather than UNSUPPORTED,
+    tests/test_hostcore.py), start offsets, and a corruption sweep."""
+    from test_hostcore import bcj_payload, host_xz
+    fid = getattr(lzma, "FILTER_" + name)
+    rng = np.random.default_rng(len(name) + 7)
+    for n in (5, 4097, 200001):
+        for so in (0, 1024):
+            raw = bcj_payload(rng, n, fid)
+            f0 = {"id": fid} if so == 0 else {"id": fid, "start_offset": so}
+            s = lzma.compress(raw, format=lzma.FORMAT_XZ, filters=[f0, {"id": lzma.FILTER_LZMA2}])
+            part = [D for D in range(max(1, n // 3), max(1, n // 3) + 4) if host_xz(s, D)[0] != 4]
+            for D in sorted({n, n + 5, *part}):
+                check("xz", s, "u1", D)
+    raw = bcj_payload(rng, 40000, fid)
+    s = lzma.compress(raw, format=lzma.FORMAT_XZ, filters=[{"id": fid}, {"id": lzma.FILTER_LZMA2}])
+    streams = [s[:int(t)] for t in rng.integers(0, len(s), 24)]
+    for _ in range(72):
+        b = bytearray(s)
+        b[int(rng.integers(0, len(b)))] ^= int(rng.integers(1, 256))
+        streams.append(bytes(b))
+    check_many("xz", streams, "u1", len(raw))
+
+
 def test_xz_unsupported_filter_chain_fails_loudly():
     from zarr_amd import ArrayMetadata, DefaultChunk, NativeUnavailable
     from zarr_amd.compression import Xz
     payload = rw(5000).tobytes()
     s = lzma.compress(payload, format=lzma.FORMAT_XZ,
-                      filters=[{"id": lzma.FILTER_X86}, {"id": lzma.FILTER_LZMA2}])
+                      filters=[{"id": lzma.FILTER_DELTA, "dist": 2}, {"id": lzma.FILTER_X86},
+                               {"id": lzma.FILTER_LZMA2}])
     meta = ArrayMetadata.new([len(payload)], [len(payload)], "u1", Xz(6))
     with pytest.raises(NativeUnavailable):
         DefaultChunk.read_chunk(s, meta, [0], np.uint8)

@@ -101,6 +101,89 @@ def test_xz_core_delta_filter_vs_liblzma(dist):
             same(bytes(b), len(raw))
 
 
+def bcj_payload(rng, n, fid):
+    """Random bytes with the filter's instruction patterns planted densely
+    (x86 E8/E9 + 0x00/0xFF high byte, ARM BL, Thumb BL pairs, PowerPC bl,
+    SPARC call), so conversions and their skip rules are exercised."""
+    b = rng.integers(0, 256, max(n, 16), dtype=np.uint8)
+    for _ in range(max(n, 16) // 12):
+        i = int(rng.integers(0, len(b) - 8))
+        if fid == lzma.FILTER_X86:
+            b[i] = 0xE8 if rng.random() < 0.5 else 0xE9
+            b[i + 4] = 0 if rng.random() < 0.5 else 0xFF
+        elif fid == lzma.FILTER_ARM:
+            b[(i & ~3) + 3] = 0xEB
+        elif fid == lzma.FILTER_ARMTHUMB:
+            i &= ~1
+            b[i + 1] = 0xF0 | (int(b[i + 1]) & 7)
+            b[i + 3] = 0xF8 | (int(b[i + 3]) & 7)
+        elif fid == lzma.FILTER_POWERPC:
+            i &= ~3
+            b[i] = 0x48 | (int(b[i]) & 3)
+            b[i + 3] = (int(b[i + 3]) & 0xFC) | 1
+        elif fid == lzma.FILTER_IA64:  # template 0x10 (slot 2 a branch slot), opcode 5, bits 9-11 zero
+            i &= ~15
+            if i + 16 <= len(b):
+                b[i] = (int(b[i]) & 0xE0) | 0x10
+                b[i + 15] = (int(b[i + 15]) & 0x0F) | 0x50
+                b[i + 12] = int(b[i + 12]) & 0xF8
+        elif fid == lzma.FILTER_SPARC:
+            i &= ~3
+            b[i] = 0x40 if rng.random() < 0.5 else 0x7F
+            b[i + 1] = (int(b[i + 1]) & 0x3F) | (0 if b[i] == 0x40 else 0xC0)
+    return b.tobytes()[:n]
+
+
+BCJ_FILTERS = ["X86", "ARM", "ARMTHUMB", "POWERPC", "SPARC", "IA64"]
+
+
+@pytest.mark.parametrize("name", BCJ_FILTERS)
+def test_xz_core_bcj_filters_vs_liblzma(name):
+    """BCJ + LZMA2 chains (liblzma simple/*.c): the core's block-end BCJ decode
+    against liblzma for whole reads, reads that stop inside the block (exact,
+    or UNSUPPORTED when the block's last bytes could start an instruction
+    the stop cut off), start offsets, and corruptions."""
+    fid = getattr(lzma, "FILTER_" + name)
+    rng = np.random.default_rng(len(name))
+    unsupported = 0
+    for n in (1, 3, 4, 5, 7, 100, 4097, 70001):
+        for so in (0, 16 if name == "IA64" else 4, 1024):
+            raw = bcj_payload(rng, n, fid)
+            f0 = {"id": fid} if so == 0 else {"id": fid, "start_offset": so}
+            s = lzma.compress(raw, format=lzma.FORMAT_XZ, filters=[f0, {"id": lzma.FILTER_LZMA2}])
+            st, out = host_xz(s, n)
+            assert st == 0 and out == raw
+            for D in (max(1, n // 3), n + 1):
+                r1 = zref.decode(zref.XZ, s, D)
+                r2 = host_xz(s, D)
+                if r2[0] == 4 and r1[0] == zref.OK:  # UNSUPPORTED: only for a stop inside the block
+                    assert D < n
+                    unsupported += 1
+                    continue
+                assert r1[0] == r2[0], (n, so, D, r1[0], r2[0])
+                if r1[0] == zref.OK:
+                    assert r1[1] == r2[1], (n, so, D)
+    raw = bcj_payload(rng, 30000, fid)
+    s = lzma.compress(raw, format=lzma.FORMAT_XZ, filters=[{"id": fid}, {"id": lzma.FILTER_LZMA2}])
+    for _ in range(30):
+        b = bytearray(s)
+        b[int(rng.integers(0, len(b)))] ^= int(rng.integers(1, 256))
+        r1, r2 = zref.decode(zref.XZ, bytes(b), len(raw)), host_xz(bytes(b), len(raw))
+        assert r1[0] == r2[0]
+        if r1[0] == zref.OK:
+            assert r1[1] == r2[1]
+
+
+def test_xz_core_longer_chain_unsupported():
+    """delta + BCJ + LZMA2 (liblzma decodes it) is reported UNSUPPORTED, not
+    decoded differently."""
+    raw = bcj_payload(np.random.default_rng(9), 20000, lzma.FILTER_X86)
+    s = lzma.compress(raw, format=lzma.FORMAT_XZ, filters=[{"id": lzma.FILTER_DELTA, "dist": 2},
+                                                           {"id": lzma.FILTER_X86}, {"id": lzma.FILTER_LZMA2}])
+    assert zref.decode(zref.XZ, s, len(raw))[0] == zref.OK
+    assert host_xz(s, len(raw))[0] == 4
+
+
 def test_xz_core_reference_vectors():
     """doc-spec vector (xz.rs:52-75) and the oracle's xz2-style encodes."""
     from golden_util import doc_spec

@@ -152,6 +152,107 @@ struct XzDevIO {
         }
         __threadfence_block();
     }
+    // BCJ decode of out[a, b) in HBM (zx::bcj_serial's result): the word
+    // filters (ARM, PowerPC, SPARC; IA-64 bundles) convert every aligned word
+    // independently, one per lane; x86 and ARM-Thumb walk their candidate positions in order
+    // (a wave ballot per 64 positions, the candidates handled wave-uniformly:
+    // a conversion skips the instruction's bytes, so the bytes a later
+    // candidate reads are never ones an earlier conversion wrote)
+    struct GBuf {
+        gu8* p;
+        __device__ __forceinline__ u32 get(u64 i) const { return __builtin_amdgcn_readfirstlane((u32)p[i]); }
+        __device__ __forceinline__ void set(u64 i, u32 v) { p[i] = (u8)v; }
+    };
+    struct LaneBuf {
+        gu8* p;
+        __device__ __forceinline__ u32 get(u64 i) const { return (u32)p[i]; }
+        __device__ __forceinline__ void set(u64 i, u32 v) { p[i] = (u8)v; }
+    };
+    __device__ void apply_bcj(u64 a, u64 b, u32 id, u32 start) {
+        const u64 len = b > a ? b - a : 0;
+        gu8* d = dst + a;
+        if (id == 7 || id == 5 || id == 9) {
+            LaneBuf lb{d};
+            for (u64 i = 4 * (u64)lane; i + 4 <= len; i += 4 * 64) zx::bcj_word(lb, i, id, start + (u32)i);
+        } else if (id == 6) {
+            LaneBuf lb{d};
+            for (u64 i = 16 * (u64)lane; i + 16 <= len; i += 16 * 64) zx::bcj_ia64_bundle(lb, i, start + (u32)i);
+        } else if (id == 4 && len >= 5) {
+            GBuf g{d};
+            const bool allowed[8] = {true, true, true, false, true, false, false, false};
+            const u32 bitnum[8] = {0, 1, 2, 2, 3, 3, 3, 3};
+            u32 prev_mask = 0, prev_pos = start - 5;
+            u64 next = 0;
+            const u64 limit = len - 5;
+            for (u64 base = 0; base <= limit; base += 64) {
+                const u64 p = base + (u64)lane;
+                const u32 x = p <= limit ? (u32)d[p] : 0u;
+                u64 m = __ballot(p <= limit && (x == 0xE8 || x == 0xE9));
+                while (m) {
+                    const u64 i = base + (u64)__builtin_ctzll(m);
+                    m &= m - 1;
+                    if (i < next) continue;
+                    const u32 now = start + (u32)i;
+                    const u32 off = now - prev_pos;
+                    prev_pos = now;
+                    if (off > 5) prev_mask = 0;
+                    else
+                        for (u32 k = 0; k < off; k++) prev_mask = (prev_mask & 0x77) << 1;
+                    const u32 b4 = g.get(i + 4);
+                    if (zx::bcj_x86_ms(b4) && allowed[(prev_mask >> 1) & 7] && (prev_mask >> 1) < 0x10) {
+                        u32 src = (b4 << 24) | (g.get(i + 3) << 16) | (g.get(i + 2) << 8) | g.get(i + 1);
+                        u32 dest;
+                        for (;;) {
+                            dest = src - (now + 5);
+                            if (prev_mask == 0) break;
+                            const u32 k = bitnum[prev_mask >> 1];
+                            if (!zx::bcj_x86_ms((dest >> (24 - k * 8)) & 0xFF)) break;
+                            src = dest ^ ((1u << (32 - k * 8)) - 1);
+                        }
+                        if (lane == 0) {
+                            d[i + 4] = (u8)(~(((dest >> 24) & 1) - 1));
+                            d[i + 3] = (u8)(dest >> 16);
+                            d[i + 2] = (u8)(dest >> 8);
+                            d[i + 1] = (u8)dest;
+                        }
+                        __threadfence_block();
+                        next = i + 5;
+                        prev_mask = 0;
+                    } else {
+                        prev_mask |= 1;
+                        if (zx::bcj_x86_ms(b4)) prev_mask |= 0x10;
+                    }
+                }
+            }
+        } else if (id == 8) {
+            GBuf g{d};
+            u64 next = 0;
+            for (u64 base = 0; base + 4 <= len; base += 128) {
+                const u64 i = base + 2 * (u64)lane;
+                const bool in = i + 4 <= len;
+                const u32 b1 = in ? (u32)d[i + 1] : 0u, b3 = in ? (u32)d[i + 3] : 0u;
+                u64 m = __ballot(in && (b1 & 0xF8) == 0xF0 && (b3 & 0xF8) == 0xF8);
+                while (m) {
+                    const u64 c = base + 2 * (u64)__builtin_ctzll(m);
+                    m &= m - 1;
+                    if (c < next) continue;
+                    const u32 c1 = g.get(c + 1), c3 = g.get(c + 3);
+                    u32 src = ((c1 & 7) << 19) | (g.get(c) << 11) | ((c3 & 7) << 8) | g.get(c + 2);
+                    src <<= 1;
+                    const u32 dest = (src - (start + (u32)c + 4)) >> 1;
+                    if (lane == 0) {
+                        d[c + 1] = (u8)(0xF0 | ((dest >> 19) & 7));
+                        d[c] = (u8)(dest >> 11);
+                        d[c + 3] = (u8)(0xF8 | ((dest >> 8) & 7));
+                        d[c + 2] = (u8)dest;
+                    }
+                    __threadfence_block();
+                    next = c + 4;
+                }
+            }
+        }
+        __threadfence_block();
+    }
     __device__ __forceinline__ u64 check(u32 id, u64 a, u64 b) {
         if (id == 4) return wave_crc<u64, CRC64_POLY>((const u8*)dst, a, b);
         return (u64)wave_crc<u32, CRC32_POLY>((const u8*)dst, a, b);

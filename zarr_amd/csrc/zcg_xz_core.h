@@ -26,8 +26,10 @@
 // validating headers/sizes/checks up to that window's end and stops there
 // with OK.  Truncation before D bytes is UNEXPECTED_EOF.
 //
-// Not restated: filter chains other than a single LZMA2 filter or delta +
-// LZMA2 (BCJ, LZMA1; liblzma accepts them, the kernel reports UNSUPPORTED), and the SHA-256
+// Not restated: filter chains other than a single LZMA2 filter, delta + LZMA2
+// or BCJ + LZMA2 (x86 / PowerPC / IA-64 / ARM / ARM-Thumb / SPARC) — LZMA1
+// and longer chains: liblzma accepts them, the kernel reports
+// UNSUPPORTED — and the SHA-256
 // check (the block check is skipped for check ID 10, as for the IDs liblzma
 // does not know).  xz2's XzEncoder writes a single LZMA2 filter with CRC64.
 #pragma once
@@ -432,30 +434,181 @@ out:
 //   u64 check(u32 id, u64 a, u64 b);     CRC32 (id 1) / CRC64 (id 4) of out[a,b)
 //   void finish();                       make all output visible in dst
 //   void apply_delta(u64 a, u64 b, u32 dist);  delta filter decode of out[a,b) in place
+//   void apply_bcj(u64 a, u64 b, u32 id, u32 start);  BCJ filter decode of out[a,b) (bcj_* below)
 // A block whose chain is delta + LZMA2 (liblzma's delta decoder passes the
 // LZMA2 output through, then adds the byte `dist` back: out[i] += out[i-dist],
-// history zero at the block start) is delta-decoded when it ends (before its
-// check, which covers the filtered bytes) or, if decoding stops inside it, by
-// xz_decode's wrapper.  LZMA2 matches read the unfiltered dictionary, which a
-// block never shares with the next (its first chunk resets the dictionary).
-struct DeltaPending {
+// history zero at the block start) or BCJ + LZMA2 (liblzma simple/*.c: branch
+// targets converted back from absolute to relative) is filter-decoded when
+// it ends (before its check, which covers the filtered bytes) or, if
+// decoding stops inside it, by xz_decode's wrapper.  LZMA2 matches read the
+// unfiltered dictionary, which a block never shares with the next (its first
+// chunk resets the dictionary).  A BCJ filter converts an instruction only
+// when all its bytes are known; liblzma's simple coder decodes past the
+// caller's output end to finish one, so when decoding stops inside a BCJ
+// block and its last bytes could start an instruction (bcj_tail_open), the
+// result is UNSUPPORTED rather than possibly different bytes.
+struct FilterPending {
     u64 start;
-    u32 dist;  // 0: none
+    u32 kind;   // 0 none, 3 delta, 4..9 BCJ x86 / PowerPC / IA-64 / ARM / ARM-Thumb / SPARC (the filter ids)
+    u32 param;  // delta distance / BCJ start offset
 };
+
+// ---- BCJ decoders, serial (liblzma simple/{x86,powerpc,ia64,arm,armthumb,sparc}.c
+// restated from the published algorithm): buf[0, len) is one block's output,
+// `pos0` its start offset; the whole block in one call equals liblzma's
+// incremental calls (each leaves the bytes of an unfinished instruction).
+// one aligned word of the ARM (BL), PowerPC (b/bl with AA=0 LK=1) or SPARC (call) filters
+template <class B>
+ZX_INL void bcj_word(B& buf, u64 i, u32 id, u32 now) {
+    const u32 b0 = buf.get(i), b1 = buf.get(i + 1), b2 = buf.get(i + 2), b3 = buf.get(i + 3);
+    if (id == 7) {  // ARM
+        if (b3 != 0xEB) return;
+        const u32 dest = (((b2 << 16) | (b1 << 8) | b0) << 2) - (now + 8);
+        const u32 d = dest >> 2;
+        buf.set(i + 2, (d >> 16) & 0xFF);
+        buf.set(i + 1, (d >> 8) & 0xFF);
+        buf.set(i, d & 0xFF);
+    } else if (id == 5) {  // PowerPC (big-endian)
+        if ((b0 >> 2) != 0x12 || (b3 & 3) != 1) return;
+        const u32 src = ((b0 & 3) << 24) | (b1 << 16) | (b2 << 8) | (b3 & ~3u);
+        const u32 dest = src - now;
+        buf.set(i, 0x48 | ((dest >> 24) & 3));
+        buf.set(i + 1, (dest >> 16) & 0xFF);
+        buf.set(i + 2, (dest >> 8) & 0xFF);
+        buf.set(i + 3, ((b3 & 3) | dest) & 0xFF);
+    } else if (id == 9) {  // SPARC
+        if (!((b0 == 0x40 && (b1 & 0xC0) == 0) || (b0 == 0x7F && (b1 & 0xC0) == 0xC0))) return;
+        u32 src = ((b0 << 24) | (b1 << 16) | (b2 << 8) | b3) << 2;
+        u32 dest = (src - now) >> 2;
+        dest = (((0u - ((dest >> 22) & 1)) << 22) & 0x3FFFFFFFu) | (dest & 0x3FFFFFu) | 0x40000000u;
+        buf.set(i, dest >> 24);
+        buf.set(i + 1, (dest >> 16) & 0xFF);
+        buf.set(i + 2, (dest >> 8) & 0xFF);
+        buf.set(i + 3, dest & 0xFF);
+    }
+}
+// one 16-byte IA-64 bundle: the template's branch slots, 41-bit slots from bit 5
+template <class B>
+ZX_INL void bcj_ia64_bundle(B& buf, u64 i, u32 now) {
+    const u32 branch[32] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
+                            4, 4, 6, 6, 0, 0, 7, 7, 4, 4, 0, 0, 4, 4, 0, 0};
+    const u32 mask = branch[buf.get(i) & 0x1F];
+    u32 bit_pos = 5;
+    for (u32 slot = 0; slot < 3; slot++, bit_pos += 41) {
+        if (((mask >> slot) & 1) == 0) continue;
+        const u32 byte_pos = bit_pos >> 3, bit_res = bit_pos & 7;
+        u64 instr = 0;
+        for (u32 j = 0; j < 6; j++) instr |= (u64)buf.get(i + j + byte_pos) << (8 * j);
+        u64 norm = instr >> bit_res;
+        if (((norm >> 37) & 0xF) != 0x5 || ((norm >> 9) & 0x7) != 0) continue;
+        u32 src = (u32)((norm >> 13) & 0xFFFFF);
+        src |= (u32)((norm >> 36) & 1) << 20;
+        src <<= 4;
+        const u32 dest = (src - now) >> 4;
+        norm &= ~((u64)0x8FFFFF << 13);
+        norm |= (u64)(dest & 0xFFFFF) << 13;
+        norm |= (u64)(dest & 0x100000) << (36 - 20);
+        instr &= (1ull << bit_res) - 1;
+        instr |= norm << bit_res;
+        for (u32 j = 0; j < 6; j++) buf.set(i + j + byte_pos, (u32)(instr >> (8 * j)) & 0xFF);
+    }
+}
+ZX_INL bool bcj_x86_ms(u32 b) { return b == 0 || b == 0xFF; }
+template <class B>
+ZX_INL void bcj_serial(B& buf, u64 len, u32 id, u32 pos0) {
+    if (id == 4) {  // x86: E8 (call) / E9 (jmp) rel32, with the prev_mask heuristic
+        if (len < 5) return;
+        const bool allowed[8] = {true, true, true, false, true, false, false, false};
+        const u32 bitnum[8] = {0, 1, 2, 2, 3, 3, 3, 3};
+        u32 prev_mask = 0, prev_pos = pos0 - 5;
+        for (u64 i = 0; i + 5 <= len;) {
+            const u32 b0 = buf.get(i);
+            if (b0 != 0xE8 && b0 != 0xE9) { i++; continue; }
+            const u32 now = pos0 + (u32)i;
+            const u32 off = now - prev_pos;
+            prev_pos = now;
+            if (off > 5) prev_mask = 0;
+            else
+                for (u32 k = 0; k < off; k++) prev_mask = (prev_mask & 0x77) << 1;
+            u32 b4 = buf.get(i + 4);
+            if (bcj_x86_ms(b4) && allowed[(prev_mask >> 1) & 7] && (prev_mask >> 1) < 0x10) {
+                u32 src = (b4 << 24) | (buf.get(i + 3) << 16) | (buf.get(i + 2) << 8) | buf.get(i + 1);
+                u32 dest;
+                for (;;) {
+                    dest = src - (now + 5);
+                    if (prev_mask == 0) break;
+                    const u32 k = bitnum[prev_mask >> 1];
+                    if (!bcj_x86_ms((dest >> (24 - k * 8)) & 0xFF)) break;
+                    src = dest ^ ((1u << (32 - k * 8)) - 1);
+                }
+                buf.set(i + 4, (~(((dest >> 24) & 1) - 1)) & 0xFF);
+                buf.set(i + 3, (dest >> 16) & 0xFF);
+                buf.set(i + 2, (dest >> 8) & 0xFF);
+                buf.set(i + 1, dest & 0xFF);
+                i += 5;
+                prev_mask = 0;
+            } else {
+                i++;
+                prev_mask |= 1;
+                if (bcj_x86_ms(b4)) prev_mask |= 0x10;
+            }
+        }
+    } else if (id == 8) {  // ARM-Thumb: BL pairs, 2-byte steps
+        for (u64 i = 0; i + 4 <= len; i += 2) {
+            const u32 b1 = buf.get(i + 1), b3 = buf.get(i + 3);
+            if ((b1 & 0xF8) != 0xF0 || (b3 & 0xF8) != 0xF8) continue;
+            u32 src = ((b1 & 7) << 19) | (buf.get(i) << 11) | ((b3 & 7) << 8) | buf.get(i + 2);
+            src <<= 1;
+            u32 dest = (src - (pos0 + (u32)i + 4)) >> 1;
+            buf.set(i + 1, 0xF0 | ((dest >> 19) & 7));
+            buf.set(i, (dest >> 11) & 0xFF);
+            buf.set(i + 3, 0xF8 | ((dest >> 8) & 7));
+            buf.set(i + 2, dest & 0xFF);
+            i += 2;
+        }
+    } else if (id == 6) {  // IA-64: 16-byte bundles, each independent
+        for (u64 i = 0; i + 16 <= len; i += 16) bcj_ia64_bundle(buf, i, pos0 + (u32)i);
+    } else {  // 4-byte words, each independent
+        for (u64 i = 0; i + 4 <= len; i += 4) bcj_word(buf, i, id, pos0 + (u32)i);
+    }
+}
+// After decoding stopped inside a BCJ block at io.pos: could its last bytes
+// start an instruction whose conversion depends on bytes not decoded?
 template <class IO>
-ZX_INL int xz_decode_blocks(IO& io, DeltaPending& dp);
+ZX_INL bool bcj_tail_open(IO& io, u64 a, u32 id) {
+    const u64 len = io.pos - a;
+    if (id == 4) {  // an E8/E9 in the last 4 bytes
+        for (u64 k = 0; k < 4 && k < len; k++) {
+            const u32 x = io.back(k);
+            if (x == 0xE8 || x == 0xE9) return true;
+        }
+        return false;
+    }
+    if (id == 8) return (len & 1) || (len >= 1 && (io.back(0) & 0xF8) == 0xF0);
+    if (id == 6) return (len & 15) != 0;  // a partial last bundle
+    return (len & 3) != 0;  // a partial last word
+}
+
+template <class IO>
+ZX_INL void apply_filter(IO& io, const FilterPending& fp) {
+    io.finish();
+    if (fp.kind == 3) io.apply_delta(fp.start, io.pos, fp.param);
+    else io.apply_bcj(fp.start, io.pos, fp.kind, fp.param);
+}
+template <class IO>
+ZX_INL int xz_decode_blocks(IO& io, FilterPending& fp);
 template <class IO>
 ZX_INL int xz_decode(IO& io) {
-    DeltaPending dp = {0, 0};
-    const int r = xz_decode_blocks(io, dp);
-    if (dp.dist) {
-        io.finish();
-        io.apply_delta(dp.start, io.pos, dp.dist);
+    FilterPending fp = {0, 0, 0};
+    const int r = xz_decode_blocks(io, fp);
+    if (fp.kind) {
+        if (r == ST_OK && fp.kind != 3 && bcj_tail_open(io, fp.start, fp.kind)) return ST_UNSUPPORTED;
+        apply_filter(io, fp);
     }
     return r;
 }
 template <class IO>
-ZX_INL int xz_decode_blocks(IO& io, DeltaPending& dp) {
+ZX_INL int xz_decode_blocks(IO& io, FilterPending& fp) {
     const u64 n = io.n;
     const u64 D = io.D;
     u64 ip = 0;       // input position
@@ -537,7 +690,7 @@ ZX_INL int xz_decode_blocks(IO& io, DeltaPending& dp) {
         }
         const u32 nfilt = (bflags & 3) + 1;
         u64 fid[4];
-        u32 dict_prop = 0, delta_dist = 0;
+        u32 dict_prop = 0, fkind = 0, fparam = 0;
         bool unsupported_chain = false;
         for (u32 f = 0; f < nfilt; f++) {
             u64 id = 0, psz = 0;
@@ -553,11 +706,14 @@ ZX_INL int xz_decode_blocks(IO& io, DeltaPending& dp) {
                 if (dict_prop > 40) return ST_INVALID;
             } else if (id == 0x03) {  // delta: distance = property + 1
                 if (psz != 1) return ST_INVALID;
-                delta_dist = io.in(hp) + 1;
+                fkind = 3;
+                fparam = io.in(hp) + 1;
                 if (f != 0 || nfilt != 2) unsupported_chain = true;  // only delta + LZMA2
-            } else if (id >= 0x04 && id <= 0x09) {  // BCJ filters
+            } else if (id >= 0x04 && id <= 0x09) {  // BCJ filters: optional 4-byte start offset
                 if (psz != 0 && psz != 4) return ST_INVALID;
-                unsupported_chain = true;
+                fkind = (u32)id;
+                fparam = psz == 4 ? io.in(hp) | (io.in(hp + 1) << 8) | (io.in(hp + 2) << 16) | (io.in(hp + 3) << 24) : 0u;
+                if (f != 0 || nfilt != 2) unsupported_chain = true;  // only BCJ + LZMA2
             } else if (id == 0x4000000000000001ull) {  // LZMA1
                 if (psz != 5) return ST_INVALID;
                 unsupported_chain = true;
@@ -578,7 +734,7 @@ ZX_INL int xz_decode_blocks(IO& io, DeltaPending& dp) {
         ip = h0 + hsize;
         const u64 cstart = ip;             // block compressed data start
         const u64 ustart = io.pos;         // block uncompressed data start
-        if (delta_dist) { dp.start = ustart; dp.dist = delta_dist; }
+        if (fkind) { fp.start = ustart; fp.kind = fkind; fp.param = fparam; }
         const u64 climit = (dec_csize != VLI_UNKNOWN) ? dec_csize
                                                        : (VLI_MAX & ~3ull) - hsize - csz_check;
         const u64 c_end = (climit > n) ? ~0ull : cstart + climit;  // compressed bytes < c_end
@@ -699,10 +855,9 @@ ZX_INL int xz_decode_blocks(IO& io, DeltaPending& dp) {
             }
         }
         // ---- block end (block_decoder.c SEQ_CODE -> PADDING -> CHECK) ----
-        if (dp.dist) {  // the delta filter's output is what the check covers
-            io.finish();
-            io.apply_delta(dp.start, io.pos, dp.dist);
-            dp.dist = 0;
+        if (fp.kind) {  // the filter's output is what the check covers
+            apply_filter(io, fp);
+            fp.kind = 0;
         }
         const u64 actual_c = ip - cstart;
         const u64 actual_u = io.pos - ustart;
