@@ -49,6 +49,7 @@ struct XzHostIO {
         uint32_t get(uint64_t i) const { return p[i]; }
         void set(uint64_t i, uint32_t v) { p[i] = (uint8_t)v; }
     };
+    uint32_t out_byte(uint64_t i) const { return dst[i]; }
     void apply_bcj(uint64_t a, uint64_t b, uint32_t id, uint32_t start) {
         Buf buf{dst + a};
         zx::bcj_serial(buf, b - a, id, start);

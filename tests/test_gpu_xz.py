@@ -145,13 +145,33 @@ def test_xz_bcj_filters(name):
     check_many("xz", streams, "u1", len(raw))
 
 
-def test_xz_unsupported_filter_chain_fails_loudly():
+@pytest.mark.parametrize("chain", [("DELTA", "X86"), ("X86", "DELTA"), ("ARM", "DELTA", "SPARC"), ("ARMTHUMB", "IA64")])
+def test_xz_filter_chains(chain):
+    """Two or three delta / BCJ filters before LZMA2, against the oracle."""
+    from test_hostcore import bcj_payload, host_xz
+    rng = np.random.default_rng(len(chain) * 5 + len(chain[-1]))
+    filters = [{"id": lzma.FILTER_DELTA, "dist": 4} if c == "DELTA" else {"id": getattr(lzma, "FILTER_" + c)}
+               for c in chain] + [{"id": lzma.FILTER_LZMA2}]
+    bcj = [c for c in chain if c != "DELTA"]
+    for n in (4097, 200001):
+        raw = bcj_payload(rng, n, getattr(lzma, "FILTER_" + bcj[0]))
+        s = lzma.compress(raw, format=lzma.FORMAT_XZ, filters=filters)
+        part = [D for D in range(n // 3, n // 3 + 4) if host_xz(s, D)[0] != 4]
+        for D in sorted({n, n + 5, *part}):
+            check("xz", s, "u1", D)
+
+
+def test_xz_unsupported_fails_loudly():
+    """A read that stops inside an x86 BCJ block whose last decoded bytes
+    could start a cut-off instruction (liblzma decodes past the end to finish
+    it) raises instead of returning bytes that might differ."""
+    from test_hostcore import bcj_payload, host_xz
     from zarr_amd import ArrayMetadata, DefaultChunk, NativeUnavailable
     from zarr_amd.compression import Xz
-    payload = rw(5000).tobytes()
-    s = lzma.compress(payload, format=lzma.FORMAT_XZ,
-                      filters=[{"id": lzma.FILTER_DELTA, "dist": 2}, {"id": lzma.FILTER_X86},
-                               {"id": lzma.FILTER_LZMA2}])
-    meta = ArrayMetadata.new([len(payload)], [len(payload)], "u1", Xz(6))
+    payload = bcj_payload(np.random.default_rng(5), 5000, lzma.FILTER_X86)
+    s = lzma.compress(payload, format=lzma.FORMAT_XZ, filters=[{"id": lzma.FILTER_X86}, {"id": lzma.FILTER_LZMA2}])
+    D = next(d for d in range(1000, 5000) if host_xz(s, d)[0] == 4)
+    assert zref.decode(zref.XZ, s, D)[0] == zref.OK
+    meta = ArrayMetadata.new([D], [D], "u1", Xz(6))
     with pytest.raises(NativeUnavailable):
         DefaultChunk.read_chunk(s, meta, [0], np.uint8)

@@ -174,14 +174,27 @@ def test_xz_core_bcj_filters_vs_liblzma(name):
             assert r1[1] == r2[1]
 
 
-def test_xz_core_longer_chain_unsupported():
-    """delta + BCJ + LZMA2 (liblzma decodes it) is reported UNSUPPORTED, not
-    decoded differently."""
-    raw = bcj_payload(np.random.default_rng(9), 20000, lzma.FILTER_X86)
-    s = lzma.compress(raw, format=lzma.FORMAT_XZ, filters=[{"id": lzma.FILTER_DELTA, "dist": 2},
-                                                           {"id": lzma.FILTER_X86}, {"id": lzma.FILTER_LZMA2}])
-    assert zref.decode(zref.XZ, s, len(raw))[0] == zref.OK
-    assert host_xz(s, len(raw))[0] == 4
+@pytest.mark.parametrize("chain", [("DELTA", "X86"), ("X86", "DELTA"), ("ARM", "DELTA", "SPARC"),
+                                   ("DELTA", "DELTA"), ("ARMTHUMB", "IA64")])
+def test_xz_core_filter_chains_vs_liblzma(chain):
+    """Chains of two or three delta / BCJ filters before LZMA2 (decoded in
+    reverse chain order, each over the previous one's output) against
+    liblzma, whole and partial reads."""
+    rng = np.random.default_rng(len(chain) * 7 + len(chain[0]))
+    filters = [{"id": lzma.FILTER_DELTA, "dist": 4} if c == "DELTA" else {"id": getattr(lzma, "FILTER_" + c)}
+               for c in chain] + [{"id": lzma.FILTER_LZMA2}]
+    bcj = [c for c in chain if c != "DELTA"]
+    for n in (3, 4097, 70001):
+        raw = bcj_payload(rng, n, getattr(lzma, "FILTER_" + bcj[0])) if bcj else rng.bytes(n)
+        s = lzma.compress(raw, format=lzma.FORMAT_XZ, filters=filters)
+        st, out = host_xz(s, n)
+        assert st == 0 and out == raw
+        for D in (max(1, n // 3), n + 1):
+            r1, r2 = zref.decode(zref.XZ, s, D), host_xz(s, D)
+            if r2[0] == 4 and r1[0] == zref.OK:
+                assert D < n
+                continue
+            assert r1[0] == r2[0] and (r1[0] != zref.OK or r1[1] == r2[1]), (n, D)
 
 
 def test_xz_core_reference_vectors():

@@ -168,6 +168,8 @@ struct XzDevIO {
         __device__ __forceinline__ u32 get(u64 i) const { return (u32)p[i]; }
         __device__ __forceinline__ void set(u64 i, u32 v) { p[i] = (u8)v; }
     };
+    // an output byte already in HBM (after finish()), wave-uniform
+    __device__ __forceinline__ u32 out_byte(u64 i) const { return __builtin_amdgcn_readfirstlane((u32)dst[i]); }
     __device__ void apply_bcj(u64 a, u64 b, u32 id, u32 start) {
         const u64 len = b > a ? b - a : 0;
         gu8* d = dst + a;

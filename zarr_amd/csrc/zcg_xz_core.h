@@ -26,10 +26,9 @@
 // validating headers/sizes/checks up to that window's end and stops there
 // with OK.  Truncation before D bytes is UNEXPECTED_EOF.
 //
-// Not restated: filter chains other than a single LZMA2 filter, delta + LZMA2
-// or BCJ + LZMA2 (x86 / PowerPC / IA-64 / ARM / ARM-Thumb / SPARC) — LZMA1
-// and longer chains: liblzma accepts them, the kernel reports
-// UNSUPPORTED — and the SHA-256
+// Not restated: LZMA1 (liblzma accepts it as the last filter, the kernel
+// reports UNSUPPORTED; delta and BCJ x86 / PowerPC / IA-64 / ARM / ARM-Thumb
+// / SPARC filters before LZMA2 are decoded), and the SHA-256
 // check (the block check is skipped for check ID 10, as for the IDs liblzma
 // does not know).  xz2's XzEncoder writes a single LZMA2 filter with CRC64.
 #pragma once
@@ -435,6 +434,7 @@ out:
 //   void finish();                       make all output visible in dst
 //   void apply_delta(u64 a, u64 b, u32 dist);  delta filter decode of out[a,b) in place
 //   void apply_bcj(u64 a, u64 b, u32 id, u32 start);  BCJ filter decode of out[a,b) (bcj_* below)
+//   u32 out_byte(u64 i);                 output byte i (after finish())
 // A block whose chain is delta + LZMA2 (liblzma's delta decoder passes the
 // LZMA2 output through, then adds the byte `dist` back: out[i] += out[i-dist],
 // history zero at the block start) or BCJ + LZMA2 (liblzma simple/*.c: branch
@@ -447,10 +447,13 @@ out:
 // caller's output end to finish one, so when decoding stops inside a BCJ
 // block and its last bytes could start an instruction (bcj_tail_open), the
 // result is UNSUPPORTED rather than possibly different bytes.
+// Chains of up to three such filters before LZMA2 (liblzma's limit) decode
+// in reverse chain order, each over the previous one's output.
 struct FilterPending {
     u64 start;
-    u32 kind;   // 0 none, 3 delta, 4..9 BCJ x86 / PowerPC / IA-64 / ARM / ARM-Thumb / SPARC (the filter ids)
-    u32 param;  // delta distance / BCJ start offset
+    u32 n;         // filters before LZMA2 (0: none)
+    u32 kind[3];   // chain order: 3 delta, 4..9 BCJ x86 / PowerPC / IA-64 / ARM / ARM-Thumb / SPARC (the filter ids)
+    u32 param[3];  // delta distance / BCJ start offset
 };
 
 // ---- BCJ decoders, serial (liblzma simple/{x86,powerpc,ia64,arm,armthumb,sparc}.c
@@ -578,33 +581,43 @@ template <class IO>
 ZX_INL bool bcj_tail_open(IO& io, u64 a, u32 id) {
     const u64 len = io.pos - a;
     if (id == 4) {  // an E8/E9 in the last 4 bytes
-        for (u64 k = 0; k < 4 && k < len; k++) {
-            const u32 x = io.back(k);
+        for (u64 k = 1; k <= 4 && k <= len; k++) {
+            const u32 x = io.out_byte(io.pos - k);
             if (x == 0xE8 || x == 0xE9) return true;
         }
         return false;
     }
-    if (id == 8) return (len & 1) || (len >= 1 && (io.back(0) & 0xF8) == 0xF0);
+    if (id == 8) return (len & 1) || (len >= 1 && (io.out_byte(io.pos - 1) & 0xF8) == 0xF0);
     if (id == 6) return (len & 15) != 0;  // a partial last bundle
     return (len & 3) != 0;  // a partial last word
 }
 
+// Decode the pending filters over [fp.start, io.pos); `partial`: decoding
+// stopped inside the block, so a BCJ stage whose input tail is open makes the
+// result UNSUPPORTED (checked on that stage's input, after the stages before it)
 template <class IO>
-ZX_INL void apply_filter(IO& io, const FilterPending& fp) {
+ZX_INL bool apply_filters(IO& io, const FilterPending& fp, bool partial) {
     io.finish();
-    if (fp.kind == 3) io.apply_delta(fp.start, io.pos, fp.param);
-    else io.apply_bcj(fp.start, io.pos, fp.kind, fp.param);
+    for (u32 k = fp.n; k-- > 0;) {
+        if (fp.kind[k] == 3) {
+            io.apply_delta(fp.start, io.pos, fp.param[k]);
+        } else {
+            if (partial && bcj_tail_open(io, fp.start, fp.kind[k])) return false;
+            io.apply_bcj(fp.start, io.pos, fp.kind[k], fp.param[k]);
+        }
+        io.finish();
+    }
+    return true;
 }
 template <class IO>
 ZX_INL int xz_decode_blocks(IO& io, FilterPending& fp);
 template <class IO>
 ZX_INL int xz_decode(IO& io) {
-    FilterPending fp = {0, 0, 0};
+    FilterPending fp;
+    fp.start = 0;
+    fp.n = 0;
     const int r = xz_decode_blocks(io, fp);
-    if (fp.kind) {
-        if (r == ST_OK && fp.kind != 3 && bcj_tail_open(io, fp.start, fp.kind)) return ST_UNSUPPORTED;
-        apply_filter(io, fp);
-    }
+    if (fp.n && !apply_filters(io, fp, r == ST_OK)) return ST_UNSUPPORTED;
     return r;
 }
 template <class IO>
@@ -690,7 +703,7 @@ ZX_INL int xz_decode_blocks(IO& io, FilterPending& fp) {
         }
         const u32 nfilt = (bflags & 3) + 1;
         u64 fid[4];
-        u32 dict_prop = 0, fkind = 0, fparam = 0;
+        u32 dict_prop = 0, nf = 0, fkind[3] = {0, 0, 0}, fparam[3] = {0, 0, 0};
         bool unsupported_chain = false;
         for (u32 f = 0; f < nfilt; f++) {
             u64 id = 0, psz = 0;
@@ -706,14 +719,15 @@ ZX_INL int xz_decode_blocks(IO& io, FilterPending& fp) {
                 if (dict_prop > 40) return ST_INVALID;
             } else if (id == 0x03) {  // delta: distance = property + 1
                 if (psz != 1) return ST_INVALID;
-                fkind = 3;
-                fparam = io.in(hp) + 1;
-                if (f != 0 || nfilt != 2) unsupported_chain = true;  // only delta + LZMA2
+                if (f < 3) { fkind[f] = 3; fparam[f] = io.in(hp) + 1; nf = f + 1; }
             } else if (id >= 0x04 && id <= 0x09) {  // BCJ filters: optional 4-byte start offset
                 if (psz != 0 && psz != 4) return ST_INVALID;
-                fkind = (u32)id;
-                fparam = psz == 4 ? io.in(hp) | (io.in(hp + 1) << 8) | (io.in(hp + 2) << 16) | (io.in(hp + 3) << 24) : 0u;
-                if (f != 0 || nfilt != 2) unsupported_chain = true;  // only BCJ + LZMA2
+                if (f < 3) {
+                    fkind[f] = (u32)id;
+                    fparam[f] = psz == 4 ? io.in(hp) | (io.in(hp + 1) << 8) | (io.in(hp + 2) << 16) | (io.in(hp + 3) << 24)
+                                         : 0u;
+                    nf = f + 1;
+                }
             } else if (id == 0x4000000000000001ull) {  // LZMA1
                 if (psz != 5) return ST_INVALID;
                 unsupported_chain = true;
@@ -734,7 +748,9 @@ ZX_INL int xz_decode_blocks(IO& io, FilterPending& fp) {
         ip = h0 + hsize;
         const u64 cstart = ip;             // block compressed data start
         const u64 ustart = io.pos;         // block uncompressed data start
-        if (fkind) { fp.start = ustart; fp.kind = fkind; fp.param = fparam; }
+        fp.start = ustart;
+        fp.n = nf;
+        for (u32 k = 0; k < 3; k++) { fp.kind[k] = fkind[k]; fp.param[k] = fparam[k]; }
         const u64 climit = (dec_csize != VLI_UNKNOWN) ? dec_csize
                                                        : (VLI_MAX & ~3ull) - hsize - csz_check;
         const u64 c_end = (climit > n) ? ~0ull : cstart + climit;  // compressed bytes < c_end
@@ -855,9 +871,9 @@ ZX_INL int xz_decode_blocks(IO& io, FilterPending& fp) {
             }
         }
         // ---- block end (block_decoder.c SEQ_CODE -> PADDING -> CHECK) ----
-        if (fp.kind) {  // the filter's output is what the check covers
-            apply_filter(io, fp);
-            fp.kind = 0;
+        if (fp.n) {  // the filters' output is what the check covers
+            apply_filters(io, fp, false);
+            fp.n = 0;
         }
         const u64 actual_c = ip - cstart;
         const u64 actual_u = io.pos - ustart;
