@@ -248,6 +248,8 @@ const char* cfg_inflate_par();
 const char* cfg_deflate();
 const char* cfg_raw();
 const char* cfg_region();
+const char* cfg_lz4_dec();
+const char* cfg_xz_opt();
 // Per-device facts and settings, made once per device under a lock (the
 // zcg_multi_* calls launch from one host thread per device): the current
 // device's CU count, and a kernel's dynamic-LDS limit raised to `bytes`.

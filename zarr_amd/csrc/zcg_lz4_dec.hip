@@ -371,9 +371,6 @@ constexpr u32 LZ_RING = 2048;  // 16-bit entries per wave
 constexpr u32 LZ_RMASK = LZ_RING - 1;
 constexpr u32 LZ_ROUND = 1024;
 constexpr u32 LZ_PTR = 0x8000u;
-#ifndef LZ_PREFETCH
-#define LZ_PREFETCH 1
-#endif
 
 __device__ __forceinline__ u32x4 gwin_load(const gu8* __restrict__ src, u32 q, u64 avail) {
     if (q + 16 <= avail) return *(const gu32x4_ua*)(src + q);
@@ -575,9 +572,7 @@ __device__ void lz4_block_wave(const gu8* __restrict__ s, u32 iend, u64 avail, g
         // the sequence after the last one in the window: an exit offset, or 255
         const u32 last_next = (u32)__builtin_amdgcn_readlane((int)__shfl((int)nx, (int)(pos & 63)), (int)(nseq - 1));
         const bool term = last_next == 0xFFFFFFFFu;
-#if LZ_PREFETCH
         const u32x4 wn = gwin_wave(s, term ? e : e + last_next, avail);  // next window, in flight during the copies
-#endif
         // gather the k-th sequence's fields
         const u32 sp = pos & 63;
         // (every shuffle runs on all lanes: a bpermute reads 0 from lanes outside EXEC)
@@ -663,11 +658,7 @@ __device__ void lz4_block_wave(const gu8* __restrict__ s, u32 iend, u64 avail, g
         op += total;
         if (term) break;
         e += last_next;
-#if LZ_PREFETCH
         w = wn;
-#else
-        w = gwin_wave(s, e, avail);
-#endif
     }
     if (dbg) {
         dc[7] = __builtin_readcyclecounter() - tstart;
@@ -1164,6 +1155,10 @@ hipError_t launch_lz4_decode(const zcg_array* a, const zcg_chunk* d_chunks, uint
     hipLaunchKernelGGL(lz4_finish_kernel, dim3(n), dim3(64), 0, s, d_chunks, n, D, t, a->compression.flags,
                        (u32)S, (const Lz4ChunkInfo*)info, (const Lz4Slot*)slots, d_status);
     return hipGetLastError();
+}
+
+const char* cfg_lz4_dec() {
+    return "lz4_dec:CORUN=" ZCG_STR(LZ_CORUN_PCT) "/" ZCG_STR(LZ_CORUN_LO) "/" ZCG_STR(LZ_CORUN_HI);
 }
 
 }  // namespace zcg

@@ -53,10 +53,7 @@ constexpr u32 XO_NICE = 64;        // stop walking at a match this long
 constexpr u32 XO_W2 = 64;          // 2-byte repeat search distance
 constexpr u32 XO_LENS = 8;         // lengths 2..XO_LENS of a range, then its last three
 constexpr u32 XO_MAXLEN = 273;
-#ifndef XO_HIST_BYTES
-#define XO_HIST_BYTES 0
-#endif
-constexpr u32 XO_HIST = XO_HIST_BYTES;  // bytes before a window kept in LDS (rep / matched-literal reads)
+constexpr u32 XO_HIST = 0;  // bytes before a window kept in the LDS tile (a 4 KiB history was slower: occupancy)
 constexpr u32 XO_PROBS = 1846 + 0x300;  // lc = lp = 0: one literal coder
 constexpr u32 XO_PROPS = (2 * 5 + 0) * 9 + 0;
 constexpr u64 XO_SEGCAP = XO_SEG + XO_SEG / 16 + 4096;  // a segment's LZMA2 chunks (bound)
@@ -1080,6 +1077,10 @@ hipError_t launch_xz_opt(const zcg_array* a, const zcg_chunk* d_chunks, uint32_t
         if (e != hipSuccess) return e;
     }
     return hipSuccess;
+}
+
+const char* cfg_xz_opt() {
+    return "xz_opt:SEG_KB=" ZCG_STR(XO_SEG_KB) ",WPE=" ZCG_STR(XO_WPE) ",PROF=" ZCG_STR(XO_PROF);
 }
 
 }  // namespace zcg
