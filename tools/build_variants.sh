@@ -12,7 +12,7 @@ base=$(basename "$SRC" .hip)
 for spec in "$@"; do
   name=${spec%%:*}; defs=${spec#*:}
   d=$R/variants/obj_$name; mkdir -p "$d"
-  /opt/rocm/bin/hipcc -O3 -fPIC -std=c++17 --offload-arch=gfx950 -munsafe-fp-atomics $defs -c "$C/$SRC" -o "$d/$base.o" &
+  /opt/rocm/bin/hipcc -O3 -fPIC -std=c++17 --offload-arch=gfx950 -munsafe-fp-atomics -I"$C" $defs -c "$C/$SRC" -o "$d/$base.o" &
 done
 wait
 for spec in "$@"; do

@@ -67,7 +67,18 @@ constexpr u32 IW_SEGMIN = 128;   // bits per lane segment
 constexpr u32 IW_SEGMAX = 4096;
 constexpr u32 IW_K = 4;          // decode steps between staged-token / mark flushes
 constexpr u32 IW_KH = 2;         // flush periods per outer step (reader loads at its top, absorbs at its bottom)
-constexpr u32 IW_TSTR = IW_TCAP + IW_K;          // token list stride (a flush writes IW_K words)
+#ifndef ZIW_G
+#define ZIW_G 4
+#endif
+constexpr u32 IW_G = ZIW_G;                      // lanes whose lists are interleaved by 16-byte blocks
+constexpr u32 IW_TSTR = IW_TCAP + 2 * IW_K;      // token list stride (a flush writes up to two aligned blocks)
+static_assert(IW_TSTR % 4 == 0 && 64 % IW_G == 0, "list blocks");
+// word offset of token j of lane l's list: lists of IW_G consecutive lanes
+// are interleaved by aligned 4-word blocks, so one flush of those lanes fills
+// whole cache lines ([lane / G][j / 4][lane % G][j % 4]; G = 1: [lane][j])
+__device__ __forceinline__ u32 iw_ta(u32 l, u32 j) {
+    return (l / IW_G) * (IW_G * IW_TSTR) + (((j >> 2) * IW_G + (l % IW_G)) << 2) + (j & 3);
+}
 constexpr u32 IW_MWIN = 8;                       // mark words a lane keeps in LDS between flushes
 #ifndef ZIW_MARKW
 #define ZIW_MARKW 32
@@ -130,7 +141,7 @@ struct IwLds {
         } h;
         struct {       // H round: marked extent (bits) of each segment, staged tokens, mark windows
             u32 mlim[65];
-            u32 tst[IW_K][64];
+            u32 tst[2 * IW_K][64];  // ring of two aligned list blocks (slot = token index % 8)
             u32 mwin[IW_MWIN][64];
         } hr;
         struct {       // L phase: the stage ring, its token-start bits (one word per lane block), the chain
@@ -294,6 +305,7 @@ __device__ __forceinline__ u32 iw_decode(const IwLds& L, u64 v, u32* adv) {
 }
 
 typedef __attribute__((address_space(1))) u32x4 gu32x4_a4 __attribute__((aligned(4)));
+typedef __attribute__((address_space(1))) u32x4 gu32x4_a16 __attribute__((aligned(16)));
 
 // tokens of a lane's list that start before word wi of its bitmap, plus the
 // marks in `part` (the bits of word wi below the position)
@@ -307,9 +319,8 @@ __device__ __forceinline__ u32 iw_rank(const gu32* mw, u32 wi, u32 part) {
 // stream bit of token j of the list of `lm` (segment start + bits before it)
 __device__ __forceinline__ u32 iw_pos(const gu32* gl, u32 lm, u32 j, u32 seg0) {
     const u32 lane = (u32)lane_id();
-    const gu32* lst = gl + (u64)lm * IW_TSTR;
     u32 s = 0;
-    for (u32 x = lane; x < j; x += 64) s += w_bits(lst[x]);
+    for (u32 x = lane; x < j; x += 64) s += w_bits(gl[iw_ta(lm, x)]);
     return seg0 + iw_wave_sum(s);
 }
 
@@ -559,8 +570,7 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
         slot = sl;
     }
     slot = __builtin_amdgcn_readfirstlane(slot);
-    gu32* const gl = pools + (u64)slot * IW_SLOT_WORDS;                 // token lists [lane][IW_TSTR]
-    gu32* const my = gl + (u64)lane * IW_TSTR;
+    gu32* const gl = pools + (u64)slot * IW_SLOT_WORDS;                 // token lists (iw_ta layout)
     gu32* const marks = gl + IW_LIST_WORDS;                             // token-start bitmaps [lane][IW_MWORDS]
     gu32* const mk = marks + (u64)lane * IW_MWORDS;
 
@@ -630,7 +640,7 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
             gr_init(bs, vbase, nvec, (active ? p : 0u) + a0b);
             if (!active) {
                 if (lane == 0) {  // the block body starts at the stream end
-                    my[0] = W_MARK | M_EXH;
+                    gl[iw_ta(0, 0)] = W_MARK | M_EXH;
                     nt = 1;
                     nxt = S_MARKER;
                 } else {
@@ -654,7 +664,7 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
                     u32 tk = iw_decode(L, bs.lo, &adv);
                     if (q + adv > total_bits) tk = W_MARK | M_EXH;
                     if (nt == IW_TCAP) { nxt = S_CAP; run = false; continue; }
-                    L.u.hr.tst[nt - nt0][lane] = tk;
+                    L.u.hr.tst[nt & (2 * IW_K - 1)][lane] = tk;
                     nt++;
                     const u32 off = q - p;  // (<= 5 words past w0 within one flush period)
                     atomicOr(&L.u.hr.mwin[(off >> 5) - w0][lane], 1u << (off & 31));
@@ -664,10 +674,21 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
                     it1++;
                     if (q >= pend) run = false;
                 }
-                // flush: IW_K staged words (those past nt are overwritten later)
-                // and the mark window (words past my position are still zero)
-                *(gu32x4_a4*)(my + nt0) = u32x4{L.u.hr.tst[0][lane], L.u.hr.tst[1][lane], L.u.hr.tst[2][lane],
-                                                 L.u.hr.tst[3][lane]};
+                // flush: the aligned block holding token nt0 (its words before
+                // nt0 are still in the ring from the last flush) and, when this
+                // period crossed into it, the next block (words past nt are
+                // overwritten later); then the mark window (words past my
+                // position are still zero)
+                {
+                    const u32 a0 = nt0 & ~3u, sb = a0 & 4u;
+                    *(gu32x4_a16*)(gl + iw_ta(lane, a0)) =
+                        u32x4{L.u.hr.tst[sb][lane], L.u.hr.tst[sb + 1][lane], L.u.hr.tst[sb + 2][lane],
+                              L.u.hr.tst[sb + 3][lane]};
+                    if (nt > a0 + 4)
+                        *(gu32x4_a16*)(gl + iw_ta(lane, a0 + 4)) =
+                            u32x4{L.u.hr.tst[sb ^ 4][lane], L.u.hr.tst[(sb ^ 4) + 1][lane],
+                                  L.u.hr.tst[(sb ^ 4) + 2][lane], L.u.hr.tst[(sb ^ 4) + 3][lane]};
+                }
                 nt0 = nt;
                 u32 mv[IW_MWIN];
 #pragma unroll
@@ -731,7 +752,7 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
                     u32 tk = iw_decode(L, bs.lo, &adv);
                     if (q + adv > total_bits) tk = W_MARK | M_EXH;
                     if (nt == IW_TCAP) { nxt = S_CAP; run2 = false; continue; }
-                    my[nt] = tk;
+                    gl[iw_ta(lane, nt)] = tk;
                     nt++;
                     it2++;
                     if (w_marker(tk)) {
@@ -823,8 +844,8 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
                     if (lb == 0xFFFFFFFFu) jb = jb - e + s1;
                 }
                 ok = (la != 0xFFFFFFFFu ? 1u : 0u) | (lb != 0xFFFFFFFFu ? 2u : 0u);
-                ta = gl[la != 0xFFFFFFFFu ? (u64)la * IW_TSTR + pa : 0ull];
-                tb = gl[lb != 0xFFFFFFFFu ? (u64)lb * IW_TSTR + pb : 0ull];
+                ta = gl[la != 0xFFFFFFFFu ? iw_ta(la, pa) : 0u];
+                tb = gl[lb != 0xFFFFFFFFu ? iw_ta(lb, pb) : 0u];
             };
             u32 tq0a, tq0b, tq1a, tq1b, tq2a, tq2b, ok0, ok1, ok2;
             auto refetch = [&]() {
@@ -1146,7 +1167,7 @@ static u32 iw_nslot(uint32_t n) {
 
 const char* cfg_inflate_wave() {
     return "inflate_wave:S=" ZCG_STR(ZIW_S) ",TCAP=" ZCG_STR(ZIW_TCAP) ",WPE=" ZCG_STR(ZIW_WPE)
-           ",EST_PCT=" ZCG_STR(ZIW_EST_PCT) ",MARKW=" ZCG_STR(ZIW_MARKW) ",DBG=" ZCG_STR(ZIW_DBG);
+           ",EST_PCT=" ZCG_STR(ZIW_EST_PCT) ",MARKW=" ZCG_STR(ZIW_MARKW) ",G=" ZCG_STR(ZIW_G) ",DBG=" ZCG_STR(ZIW_DBG);
 }
 
 uint64_t inflate_wave_ws_bytes(const zcg_array* a, uint32_t n) {
