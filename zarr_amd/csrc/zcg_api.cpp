@@ -182,7 +182,7 @@ int zcg_abi_version(void) { return ZCG_ABI_VERSION; }
 const char* zcg_build_config(void) {
     static const std::string cfg = std::string(zcg::cfg_inflate_wave()) + ";" + zcg::cfg_inflate_par() + ";" +
                                    zcg::cfg_deflate() + ";" + zcg::cfg_raw() + ";" + zcg::cfg_region() + ";" +
-                                   zcg::cfg_lz4_dec() + ";" + zcg::cfg_xz_opt();
+                                   zcg::cfg_lz4_dec() + ";" + zcg::cfg_xz_opt() + ";" + zcg::cfg_bz2();
     return cfg.c_str();
 }
 

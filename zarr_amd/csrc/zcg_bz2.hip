@@ -36,7 +36,12 @@ namespace zcg {
 
 constexpr u32 BZ_NMAX = 900000;
 constexpr u32 BZ_NSAMP = 1024;
-constexpr int BZ_WALKS = BZ_NSAMP / 256 + 1;  // interleaved walks per thread (+ the start)
+constexpr int BZ_WALKS = BZ_NSAMP / 256 + 1;
+#ifndef ZB_KMUL
+#define ZB_KMUL 4
+#endif
+constexpr u32 BZ_KMUL = ZB_KMUL;  // kept bytes per walk, in sample strides
+static_assert(BZ_KMUL >= 1 && (BZ_KMUL & (BZ_KMUL - 1)) == 0, "power of two");  // interleaved walks per thread (+ the start)
 constexpr u32 BZ_T = 256;
 constexpr u64 BZ_LBYTES = 900096;  // L / T capacity (BZ_NMAX rounded up to 256)
 
@@ -348,7 +353,7 @@ struct BzBcLds {
 // orig, stored_crc, randomised, out_pos}.  Out: X.sh.out_pos advanced,
 // X.tcrc[0] = the block CRC; returns a final chunk status (>= 0) or -1 when
 // the stream continues.
-__device__ __forceinline__ int bz_block_bc(BzBcLds& X, const gu8* L, gu8* LB, gu8* T, gu32* W, gu8* dst,
+__device__ __forceinline__ int bz_block_bc(BzBcLds& X, const gu8* L, gu8* KB, gu8* T, gu32* W, gu8* dst,
                                            u64 D, DType t, u32 vflags, u64& t_last) {
     const u32 tid = threadIdx.x, lane = tid & 63;
     const u32 wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -416,11 +421,13 @@ __device__ __forceinline__ int bz_block_bc(BzBcLds& X, const gu8* L, gu8* LB, gu
     // One walk per sample: step m from position p reads W[p] = next << 8 |
     // L[next], i.e. output byte soff + 1 + m.  The first CAP bytes of each
     // walk are kept (4 at a time in a register, then one u32 store) in the
-    // L column's space, free once W exists; a walk longer than CAP records
-    // where it was at step CAP and finishes after the ranking.
-    const u32 CAP = S < 16 ? 16u : S;
-    gu32* buf32 = (gu32*)LB;
-    const u32 Lp0 = L[p0];  // T[0] (the cycle's first byte), before LB is overwritten
+    // slot's kept-byte buffer KB; a walk longer than CAP records where it was
+    // at step CAP and finishes after the ranking.  Walk lengths are close to
+    // exponential with mean nblock / NR <= S, so CAP = BZ_KMUL * S leaves
+    // ~e^-BZ_KMUL of the bytes to the second walk (CAP = S: ~31 %).
+    const u32 CAP = S < 16 / BZ_KMUL ? 16u : BZ_KMUL * S;
+    gu32* buf32 = (gu32*)KB;
+    const u32 Lp0 = L[p0];  // T[0] (the cycle's first byte)
     __syncthreads();
     {
         u32 ps[BZ_WALKS], ln[BZ_WALKS], sidk[BZ_WALKS], acc[BZ_WALKS];
@@ -672,7 +679,8 @@ constexpr u64 BZ_A_OFF_SEL = BZ_LBYTES;
 constexpr u64 BZ_A_OFF_ST = BZ_LBYTES + 18176;
 constexpr u64 BZ_A_SLOT = BZ_A_OFF_ST + 256;              // L, SEL, state
 constexpr u64 BZ_BC_OFF_W = BZ_LBYTES;
-constexpr u64 BZ_BC_SLOT = BZ_BC_OFF_W + 4ull * BZ_NMAX + 128;  // T, W
+constexpr u64 BZ_BC_OFF_K = BZ_BC_OFF_W + 4ull * BZ_NMAX + 128;
+constexpr u64 BZ_BC_SLOT = BZ_BC_OFF_K + (u64)BZ_KMUL * 1024 * (BZ_NSAMP + 1);  // T, W, kept walk bytes (CAP <= BZ_KMUL * 1024)
 constexpr u32 BZ_NA = 4096;  // chunks in flight (stage A occupancy: 16 waves per CU)
 constexpr u32 BZ_NB = 1024;  // stage B/C workspace slots (>= resident B/C workgroups)
 static_assert(BZ_A_SLOT % 256 == 0 && BZ_BC_SLOT % 256 == 0, "slot alignment");
@@ -809,7 +817,7 @@ __global__ __launch_bounds__(256) void bz2_stage_bc_kernel(const zcg_chunk* __re
     u8* bslot = wsb + (u64)b * BZ_BC_SLOT;
     const zcg_chunk ch = chunks[c];
     u64 t_last = __builtin_readcyclecounter();
-    const int fs = bz_block_bc(S, (const gu8*)slot, (gu8*)slot, (gu8*)bslot, (gu32*)(bslot + BZ_BC_OFF_W), (gu8*)ch.dst, D, t,
+    const int fs = bz_block_bc(S, (const gu8*)slot, (gu8*)(bslot + BZ_BC_OFF_K), (gu8*)bslot, (gu32*)(bslot + BZ_BC_OFF_W), (gu8*)ch.dst, D, t,
                                vflags, t_last);
     __syncthreads();  // all B/C workspace accesses done
     if (tid == 0) {
@@ -882,7 +890,7 @@ __global__ __launch_bounds__(256) void bz2_decode_kernel(const zcg_chunk* __rest
             S.sh.randomised = sh_s.randomised;
         }
         __syncthreads();
-        const int fs = bz_block_bc(S, (const gu8*)slot, (gu8*)slot, (gu8*)bslot, (gu32*)(bslot + BZ_BC_OFF_W), (gu8*)ch.dst,
+        const int fs = bz_block_bc(S, (const gu8*)slot, (gu8*)(bslot + BZ_BC_OFF_K), (gu8*)bslot, (gu32*)(bslot + BZ_BC_OFF_W), (gu8*)ch.dst,
                                    D, t, vflags, t_last);
         __syncthreads();
         if (fs >= 0) { final_status = fs; break; }
@@ -902,6 +910,8 @@ u32 bz_na(uint32_t n) { return n < BZ_NA ? n : BZ_NA; }
 u32 bz_nb(uint32_t n) { return n < BZ_NB ? n : BZ_NB; }
 constexpr u64 BZ_OWNER_BYTES = 4ull * BZ_NB;
 }  // namespace
+
+const char* cfg_bz2() { return "bz2:KMUL=" ZCG_STR(ZB_KMUL); }
 
 uint64_t bzip2_decode_ws_bytes(const zcg_array* a, uint32_t n) {
     (void)a;

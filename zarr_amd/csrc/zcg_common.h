@@ -250,6 +250,7 @@ const char* cfg_raw();
 const char* cfg_region();
 const char* cfg_lz4_dec();
 const char* cfg_xz_opt();
+const char* cfg_bz2();
 // Per-device facts and settings, made once per device under a lock (the
 // zcg_multi_* calls launch from one host thread per device): the current
 // device's CU count, and a kernel's dynamic-LDS limit raised to `bytes`.
