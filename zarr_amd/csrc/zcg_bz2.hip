@@ -40,6 +40,9 @@ constexpr int BZ_WALKS = BZ_NSAMP / 256 + 1;
 #ifndef ZB_KMUL
 #define ZB_KMUL 4
 #endif
+#ifndef ZB_WCOPY
+#define ZB_WCOPY 0
+#endif
 constexpr u32 BZ_KMUL = ZB_KMUL;  // kept bytes per walk, in sample strides
 static_assert(BZ_KMUL >= 1 && (BZ_KMUL & (BZ_KMUL - 1)) == 0, "power of two");  // interleaved walks per thread (+ the start)
 constexpr u32 BZ_T = 256;
@@ -488,6 +491,27 @@ __device__ __forceinline__ int bz_block_bc(BzBcLds& X, const gu8* L, gu8* KB, gu
     __syncthreads();
     BZ_TSTAMP(3);
     if (sh.single) {
+#if ZB_WCOPY
+        // kept bytes -> T, a wave per sample (byte m of walk s is T[soff + 1 + m]):
+        // lane l moves bytes 4l..4l+3 of each 256-byte piece, so a load is one
+        // coalesced dword per lane and a store instruction covers two lines
+        for (u32 sd = wave; sd <= NR; sd += BZ_T / 64) {
+            if (sd == NR && !extra) break;
+            const u32 so = soff[sd];
+            if (so == 0xFFFFFFFFu) continue;
+            const u32 len = slen[sd], kept = len < CAP ? len : CAP;
+            const gu32* kb = buf32 + ((sd * CAP) >> 2);
+            for (u32 m = 4 * lane; m < kept; m += 256) {
+                const u32 v = kb[m >> 2];
+#pragma unroll
+                for (u32 j = 0; j < 4; j++)
+                    if (m + j < kept) {
+                        const u32 idx = so + 1 + m + j;
+                        T[idx < nblock ? idx : idx - nblock] = (u8)(v >> (8 * j));
+                    }
+            }
+        }
+#else
         // kept bytes -> T (thread per sample; byte m of walk s is T[soff + 1 + m])
 #pragma unroll
         for (int k = 0; k < BZ_WALKS; k++) {
@@ -507,6 +531,7 @@ __device__ __forceinline__ int bz_block_bc(BzBcLds& X, const gu8* L, gu8* KB, gu
                     }
             }
         }
+#endif
         // walks longer than CAP: the rest, interleaved per thread
         u32 q[BZ_WALKS], rem[BZ_WALKS], of[BZ_WALKS];
         u32 act = 0;
