@@ -40,9 +40,6 @@ constexpr int BZ_WALKS = BZ_NSAMP / 256 + 1;
 #ifndef ZB_KMUL
 #define ZB_KMUL 4
 #endif
-#ifndef ZB_WCOPY
-#define ZB_WCOPY 0
-#endif
 constexpr u32 BZ_KMUL = ZB_KMUL;  // kept bytes per walk, in sample strides
 static_assert(BZ_KMUL >= 1 && (BZ_KMUL & (BZ_KMUL - 1)) == 0, "power of two");  // interleaved walks per thread (+ the start)
 constexpr u32 BZ_T = 256;
@@ -491,7 +488,6 @@ __device__ __forceinline__ int bz_block_bc(BzBcLds& X, const gu8* L, gu8* KB, gu
     __syncthreads();
     BZ_TSTAMP(3);
     if (sh.single) {
-#if ZB_WCOPY
         // kept bytes -> T, a wave per sample (byte m of walk s is T[soff + 1 + m]):
         // lane l moves bytes 4l..4l+3 of each 256-byte piece, so a load is one
         // coalesced dword per lane and a store instruction covers two lines
@@ -511,27 +507,6 @@ __device__ __forceinline__ int bz_block_bc(BzBcLds& X, const gu8* L, gu8* KB, gu
                     }
             }
         }
-#else
-        // kept bytes -> T (thread per sample; byte m of walk s is T[soff + 1 + m])
-#pragma unroll
-        for (int k = 0; k < BZ_WALKS; k++) {
-            const bool last = k == BZ_WALKS - 1;
-            const u32 sd = !last ? tid + (u32)k * BZ_T : NR;
-            const bool on = !last ? sd < NR : (tid == 0 && extra);
-            if (!on || soff[sd] == 0xFFFFFFFFu) continue;
-            const u32 len = slen[sd], kept = len < CAP ? len : CAP;
-            u32 o = soff[sd] + 1;
-            for (u32 m = 0; m < kept; m += 4) {
-                const u32 v = buf32[(sd * CAP + m) >> 2];
-#pragma unroll
-                for (u32 j = 0; j < 4; j++)
-                    if (m + j < kept) {
-                        const u32 idx = o + m + j;
-                        T[idx < nblock ? idx : idx - nblock] = (u8)(v >> (8 * j));
-                    }
-            }
-        }
-#endif
         // walks longer than CAP: the rest, interleaved per thread
         u32 q[BZ_WALKS], rem[BZ_WALKS], of[BZ_WALKS];
         u32 act = 0;
