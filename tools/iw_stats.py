@@ -67,7 +67,7 @@ fn(out.ctypes.data, 1)
 names = {0: "rounds", 1: "blocks", 2: "stages", 3: "groups", 4: "p1_lane_it", 5: "p2_lane_it", 6: "chain",
          7: "jump_passes", 8: "caps", 9: "rounds_no_eob", 10: "cyc_hdr", 11: "cyc_p1", 12: "cyc_p2",
          13: "cyc_chain", 14: "cyc_heads", 15: "cyc_expand", 16: "cyc_gather", 17: "cyc_jump", 18: "cyc_commit",
-         19: "cyc_total"}
+         19: "cyc_total", 20: "far_iters", 21: "near_batches", 22: "near_passes", 23: "near_straddle_batches"}
 d = {v: int(out[k]) for k, v in names.items()}
 res["per_chunk"] = {k: round(v / packed.n, 1) for k, v in d.items()}
 cyc = {k: v for k, v in d.items() if k.startswith("cyc_") and k != "cyc_total"}

@@ -53,6 +53,9 @@
 #ifndef ZIW_EST_PCT
 #define ZIW_EST_PCT 108
 #endif
+#ifndef ZIW_TL
+#define ZIW_TL 1  // token-granular L phase (far tokens copied by 16-byte pieces, near bytes in ordered batches)
+#endif
 #ifndef ZIW_DBG
 #define ZIW_DBG 1  // 0: the debug-counter code is compiled out (the flag is ignored)
 #endif
@@ -123,12 +126,12 @@ constexpr u32 W_LCAP = 852;
 constexpr int W_DB = 8;
 constexpr u32 W_DCAP = 432;  // >= enough(30, 8, 15) = 402
 
-constexpr u32 IW_NDBG = 20;
+constexpr u32 IW_NDBG = 24;
 __device__ unsigned long long g_iw_dbg[32];
 enum { IWD_ROUNDS, IWD_BLOCKS, IWD_STAGES, IWD_GROUPS, IWD_P1_IT, IWD_P2_IT, IWD_CHAIN, IWD_MRR, IWD_CAPS,
        IWD_NOEOB, IWT_HDR, IWT_P1, IWT_P2, IWT_CHAIN, IWT_HEADS, IWT_EXPAND, IWT_GATHER, IWT_JUMP,
-       IWT_COMMIT, IWT_TOTAL };
-static_assert(IWT_TOTAL < IW_NDBG, "debug slots");
+       IWT_COMMIT, IWT_TOTAL, IWD_FARIT, IWD_NBATCH, IWD_NPASS, IWD_NSTRAD };
+static_assert(IWD_NSTRAD < IW_NDBG, "debug slots");
 
 struct IwLds {
     u32 ltab[W_LCAP];
@@ -144,9 +147,17 @@ struct IwLds {
             u32 tst[2 * IW_K][64];  // ring of two aligned list blocks (slot = token index % 8)
             u32 mwin[IW_MWIN][64];
         } hr;
-        struct {       // L phase: the stage ring, its token-start bits (one word per lane block), the chain
+        struct {       // L phase: the stage ring, near-token descriptors and batch markers
             u16 ptr[IW_S];
+#if ZIW_TL
+            union {
+                u32 desc[128];  // near token 2l + slot of the group: (offset - first near index) | dist << 16
+                u64 fd[64];     // far tokens of the group by rank: source of the first quad | (quad, r, L) << 32
+            };
+            u8 mk[64];      // near batch: token id + 1 at the lane of its first byte in the batch
+#else
             u32 head[IW_S / 32];
+#endif
         } st;
     } u;
     u32 dbgc[IW_NDBG];
@@ -862,9 +873,220 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
                 const u64 S = P;
                 const u32 sa = (u32)(S & 31);
                 const u64 room = D - P;
-                const u32 capS = IW_S - sa;
+                const u32 capS = ZIW_TL ? IW_S : IW_S - sa;
                 const u32 cap = room < capS ? (u32)room : capS;
                 const bool fin = (u64)cap == room;
+#if ZIW_TL
+                // Token-granular stage.  The ring is cleared, then every kept
+                // token writes its own entries: a literal its final byte; a FAR
+                // match (whole source before the stage) its final bytes, copied
+                // from the committed output by 16-byte pieces, one aligned quad
+                // of entries OR-ed in per source dword; a NEAR match one pointer
+                // per byte (to the byte d before it), resolved in ordered
+                // batches of 64 near bytes by pointer jumping.  Sources always
+                // lie before their byte, so a batch only waits on itself.
+                {
+                    u32x4* z = (u32x4*)L.u.st.ptr;
+#pragma unroll
+                    for (u32 i = 0; i < IW_S / 512; i++) z[lane + 64 * i] = u32x4{0u, 0u, 0u, 0u};
+                }
+                wsync();
+                u32 emitted = 0;
+                bool bad = false;  // a distance before the output start
+                u32 why = 0;       // 1 final cut, 2 marker / round end, 3 capacity
+                u32 mcode = 0;
+                const gu8* gd = (const gu8*)dst;
+                // 16-byte source pieces: native byte order, and every piece of
+                // a far token ends before S + 16 <= D
+                const bool wide_ok = !tw.swap && room >= 16;
+                const u32 S32 = (u32)S;  // (D < 2^32)
+                struct Tk {
+                    u32 kind, o, L, d;  // kind 0 none, 1 literal (d = byte), 2 far, 3 near; L clipped at cap
+                };
+                auto classify = [&](u32 tk, u32 o, u32 len, bool keep) -> Tk {
+                    Tk t{0u, o, 0u, 0u};
+                    if (!keep) return t;
+                    if (!(tk & W_MATCH)) {
+                        t.kind = 1u;
+                        t.L = 1u;
+                        t.d = tk & 0xFFu;
+                        return t;
+                    }
+                    const u32 d = (tk & 0x7FFFu) + 1u;
+                    if (d > S32 + o) {
+                        bad = true;
+                        return t;
+                    }
+                    t.L = (fin && o + len > cap) ? cap - o : len;
+                    t.d = d;
+                    // far: the whole source lies before the stage, and the first
+                    // piece (from the aligned quad before the token) is in the output
+                    t.kind = (wide_ok && o + len <= d && S32 + o - d >= 3u) ? 2u : 3u;
+                    return t;
+                };
+                auto group2 = [&](u32& tqa, u32& tqb, u32& okq) -> bool {
+                    IW_ADD(IWD_GROUPS, 1);
+                    const u32 ta = (okq & 1u) ? tqa : (W_MARK | M_END), tb = (okq & 2u) ? tqb : (W_MARK | M_END);
+                    {
+                        u32 cm1 = cm, cj1 = cj;
+                        advance(cm1, cj1, 128 * IW_GK);
+                        fetch2(cm1, cj1, tqa, tqb, okq);
+                    }
+                    const u64 ma = __ballot(w_marker(ta)), mb = __ballot(w_marker(tb));
+                    const u32 fa = ma ? 2 * (u32)__builtin_ctzll(ma) : 128u, fb = mb ? 2 * (u32)__builtin_ctzll(mb) + 1 : 128u;
+                    const u32 fm = fa < fb ? fa : fb;  // first marker, in token order
+                    const u32 ia = 2 * lane, ib = ia + 1;
+                    const u32 la = ia < fm ? w_len(ta) : 0u, lb = ib < fm ? w_len(tb) : 0u;
+                    const u32 ps = la + lb;
+                    const u32 incl = iw_incl_scan(ps);
+                    const u32 oa = emitted + incl - ps, ob = oa + la;
+                    const bool ka = ia < fm && (fin ? oa < cap : oa + la <= cap);
+                    const bool kb = ib < fm && (fin ? ob < cap : ob + lb <= cap);
+                    const u32 ntk = (u32)__popcll(__ballot(ka)) + (u32)__popcll(__ballot(kb));
+                    const Tk A = classify(ta, oa, la, ka), B = classify(tb, ob, lb, kb);
+                    if (A.kind == 1u) L.u.st.ptr[(S32 + A.o) & (IW_S - 1)] = (u16)(IE_VAL | A.d);
+                    if (B.kind == 1u) L.u.st.ptr[(S32 + B.o) & (IW_S - 1)] = (u16)(IE_VAL | B.d);
+                    IW_T(IWT_HEADS);
+                    // far tokens, compacted one per lane (rank in token order):
+                    // 16-byte source pieces from the aligned quad before the
+                    // token, one quad of entries OR-ed per source dword (entries
+                    // outside the token OR-ed as zero)
+                    {
+                        const bool fA = A.kind == 2u, fB = B.kind == 2u;
+                        const u64 bA = __ballot(fA), bB = __ballot(fB);
+                        const u64 below = (1ull << lane) - 1ull;
+                        const u32 rkA = (u32)__popcll(bA & below) + (u32)__popcll(bB & below), rkB = rkA + (fA ? 1u : 0u);
+                        const u32 NF = (u32)__popcll(bA) + (u32)__popcll(bB);
+                        auto fdesc = [&](const Tk& t) -> u64 {
+                            const u32 y = S32 + t.o, r = y & 3u;
+                            return (u64)(y - t.d - r) | ((u64)(((y - r) & (IW_S - 1)) | (r << 11) | (t.L << 16)) << 32);
+                        };
+                        for (u32 f0 = 0; f0 < NF; f0 += 64) {
+                            if (fA && rkA - f0 < 64u) L.u.st.fd[rkA - f0] = fdesc(A);
+                            if (fB && rkB - f0 < 64u) L.u.st.fd[rkB - f0] = fdesc(B);
+                            wsync();
+                            if (f0 + lane < NF) {
+                                const u64 fdw = L.u.st.fd[lane];
+                                const u32 src = (u32)fdw, hi = (u32)(fdw >> 32);
+                                const u32 qb = hi & (IW_S - 1), r = (hi >> 11) & 3u, e = r + (hi >> 16);
+                                const u32 np = (e + 15) >> 4;
+                                const u32x4 V0 = *(const gu32x4_ua*)(gd + src);
+                                u32x4 V1 = V0;
+                                if (np > 1) V1 = *(const gu32x4_ua*)(gd + src + 16);
+                                auto piece = [&](const u32x4& V, u32 p) {
+#pragma unroll
+                                    for (u32 q = 0; q < 4; q++) {
+                                        const u32 K = 4 * p + q;
+                                        const int bq = (int)e - 4 * (int)K;
+                                        if (bq > 0) {
+                                            const u32 w = q == 0 ? V.x : q == 1 ? V.y : q == 2 ? V.z : V.w;
+                                            u64 m = bq >= 4 ? ~0ull : ((1ull << (16 * bq)) - 1ull);
+                                            if (K == 0) m &= ~0ull << (16 * r);
+                                            const u64 val = ((u64)__builtin_amdgcn_perm(0xFFFFFFFFu, w, 0x04030402u) << 32) |
+                                                            (u64)__builtin_amdgcn_perm(0xFFFFFFFFu, w, 0x04010400u);
+                                            atomicOr((unsigned long long*)(L.u.st.ptr + ((qb + 4 * K) & (IW_S - 1))), val & m);
+                                        }
+                                    }
+                                };
+                                piece(V0, 0);
+                                if (np > 1) piece(V1, 1);
+                                for (u32 p = 2; p < np; p++) {
+                                    IW_ADD(IWD_FARIT, 1);
+                                    const u32x4 Vp = *(const gu32x4_ua*)(gd + src + 16 * p);
+                                    piece(Vp, p);
+                                }
+                            }
+                            wsync();
+                        }
+                    }
+                    IW_T(IWT_EXPAND);
+                    // near bytes: index in the group's ordered near list
+                    const u32 nla = A.kind == 3u ? A.L : 0u, nlb = B.kind == 3u ? B.L : 0u;
+                    const u32 nps = nla + nlb;
+                    const u32 nincl = iw_incl_scan(nps);
+                    const u32 na = nincl - nps, nb = na + nla;
+                    const u32 NB = (u32)__builtin_amdgcn_readlane((int)nincl, 63);
+                    if (nla) L.u.st.desc[ia] = (A.o - na) | (A.d << 16);
+                    if (nlb) L.u.st.desc[ib] = (B.o - nb) | (B.d << 16);
+                    // near batches of 64 bytes in output order: lane i takes near
+                    // byte n0 + i; its token is the last one whose first byte in
+                    // the batch is at or before it (marker + max scan)
+                    for (u32 n0 = 0; n0 < NB; n0 += 64) {
+                        L.u.st.mk[lane] = 0;
+                        wsync();
+                        if (nla && na < n0 + 64 && na + nla > n0) L.u.st.mk[na > n0 ? na - n0 : 0u] = (u8)(ia + 1);
+                        if (nlb && nb < n0 + 64 && nb + nlb > n0) L.u.st.mk[nb > n0 ? nb - n0 : 0u] = (u8)(ib + 1);
+                        wsync();
+                        const int tid = iw_incl_max((int)L.u.st.mk[lane]) - 1;
+                        const u32 i = n0 + lane;
+                        bool done = i >= NB, strad = false;
+                        u32 pos = 0, cur = 0;
+                        if (!done) {
+                            const u32 dsc = L.u.st.desc[tid];
+                            const u32 p = (dsc & 0xFFFFu) + i;
+                            const u32 d = dsc >> 16;
+                            pos = (S32 + p) & (IW_S - 1);
+                            if (p >= d) cur = (S32 + p - d) & (IW_S - 1);
+                            else cur = IE_VAL | (u32)gd[swap_pos32(S32 + p - d, tw)];  // before the stage
+                            strad = p < d;
+                            L.u.st.ptr[pos] = (u16)cur;
+                            done = cur >= IE_VAL;
+                        }
+                        wsync();
+                        IW_ADD(IWD_NBATCH, 1);
+                        if (dbg && __ballot(strad) != 0) IW_ADD(IWD_NSTRAD, 1);
+                        for (u32 pass = 0; __ballot(!done) != 0; pass++) {
+                            IW_ADD(IWD_NPASS, 1);
+                            if (pass >= 8) {  // a 64-byte batch resolves in <= 7 passes
+                                bad = true;
+                                break;
+                            }
+                            u32 v = 0;
+                            if (!done) v = L.u.st.ptr[cur];
+                            wsync();
+                            if (!done) {
+                                L.u.st.ptr[pos] = (u16)v;
+                                cur = v;
+                                done = v >= IE_VAL;
+                            }
+                            wsync();
+                        }
+                    }
+                    IW_T(IWT_GATHER);
+                    if (ntk) {
+                        const u32 t = ntk - 1;  // the last taken token: lane t / 2, slot t % 2
+                        const u32 ea = incl - ps + la;
+                        emitted += (u32)__builtin_amdgcn_readlane((int)((t & 1) ? incl : ea), (int)(t >> 1));
+                    }
+                    advance(cm, cj, ntk);
+                    if (fin && emitted >= cap) { why = 1; return true; }
+                    if (ntk < 128) {
+                        if (ntk == fm) {
+                            why = 2;
+                            mcode = (u32)__builtin_amdgcn_readlane((int)((fm & 1) ? tb : ta), (int)(fm >> 1)) & 3u;
+                        } else {
+                            why = 3;
+                        }
+                        return true;
+                    }
+                    return false;
+                };
+                for (;;) {
+                    if (group2(tq0a, tq0b, ok0)) break;
+                    if (group2(tq1a, tq1b, ok1)) break;
+                    if (group2(tq2a, tq2b, ok2)) break;
+                }
+                refetch();  // the next stage starts at the cursor
+                IW_ADD(IWD_STAGES, 1);
+                if (__ballot(bad) != 0) { r = R_INVALID; break; }
+                const u32 emit = emitted < cap ? emitted : cap;  // a token may cross N: clip
+                IW_T(IWT_HEADS);
+                if (emit) {
+                    iw_commit(L, dst, S, S + emit, tw);
+                    P = S + emit;
+                    IW_T(IWT_COMMIT);
+                }
+#else
                 L.u.st.head[lane] = 0;
                 wsync();
                 u32 emitted = 0;
@@ -1077,6 +1299,7 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
                     P = S + emit;
                     IW_T(IWT_COMMIT);
                 }
+#endif
                 if (why == 1) {
                     // output full: zlib's look-ahead continues at the first untaken token
                     boundary = emitted == cap;
