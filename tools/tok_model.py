@@ -122,3 +122,29 @@ while S < N:
 print(dict(stages=stages, groups=groups, far_iter_per_stage=far_it / stages, far_iter_balanced=far_it_split / stages,
            far_quads_per_stage=fq_tot / stages, near_iter_per_stage=near_it / stages,
            near_bytes_per_stage=nb_tot / stages, near_batches_per_stage=nbatches / stages))
+
+# ---- near tokens whose source lies before their group's first byte (settled) ----
+S = 0; ti = 0; settled = 0; nearc = 0; settled_b = 0; near_b = 0; st16 = 0
+while S < N:
+    cap = 2048
+    lim = S + cap
+    j = bisect.bisect_right(starts, lim) - 1
+    E = starts[j] if starts[j] > S else min(N, lim)
+    stoks = []
+    while ti < len(tk) and starts[ti] < E:
+        stoks.append((starts[ti], tk[ti])); ti += 1
+    for g0 in range(0, len(stoks), 128):
+        grp = stoks[g0:g0 + 128]
+        og = grp[0][0]
+        for (o, t) in grp:
+            if t[0] == 'L':
+                continue
+            L, d = t[1], t[2]
+            if o - d + min(L, d) <= S and d >= L:
+                continue
+            nearc += 1; near_b += L
+            if o - d + min(L, d) <= og and o - d >= S:
+                settled += 1; settled_b += L
+                if L <= 16: st16 += 1
+    S = E
+print(dict(near=nearc, settled=settled, near_bytes=near_b, settled_bytes=settled_b, settled_le16=st16))

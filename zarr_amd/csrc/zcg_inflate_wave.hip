@@ -22,12 +22,14 @@
 //    records it and keeps decoding after it (the record is real only if the
 //    lane's valid range reaches it), so a garbage path never ends a segment
 //    early.
-//  L (LZ77) phase: the valid tokens, in stream order, are resolved IW_S output
-//    bytes at a time in LDS: one 16-bit entry per output byte (final byte,
-//    pointer to an earlier byte of the stage, or a far code for a byte before
-//    the stage, read back from the chunk's committed output), pointer jumping
-//    until every entry is final, and one coalesced 16-B store pass with the
-//    byte-order transform fused.
+//  L (LZ77) phase: the valid tokens, in stream order, are resolved up to IW_S
+//    output bytes at a time in an LDS ring of 16-bit entries, TOKEN by token:
+//    a literal writes its byte; a far match (its whole source before the
+//    stage) is copied from the chunk's committed output by 16-byte pieces, one
+//    far token per lane after a ballot compaction; a near match writes one
+//    pointer per byte, and the near bytes are resolved in ordered batches of
+//    64 by pointer jumping.  One coalesced 16-B store pass per stage commits
+//    the ring with the byte-order transform fused.
 //
 // Everything is wave-synchronous: no s_barrier between phases, and the other
 // chunks' waves on the SIMD fill the dependent-LDS latency.  Block headers,
@@ -52,9 +54,6 @@
 #endif
 #ifndef ZIW_EST_PCT
 #define ZIW_EST_PCT 108
-#endif
-#ifndef ZIW_TL
-#define ZIW_TL 1  // token-granular L phase (far tokens copied by 16-byte pieces, near bytes in ordered batches)
 #endif
 #ifndef ZIW_DBG
 #define ZIW_DBG 1  // 0: the debug-counter code is compiled out (the flag is ignored)
@@ -112,11 +111,9 @@ constexpr u32 S_MARKER = 65;     // pass 2 ended on a marker (last token of the 
 constexpr u32 S_CAP = 66;        // token list full
 
 // stage entries (u16): IE_VAL|byte = a final byte; a value below IW_S = the
-// ring index of an earlier byte of the stage; IE_FAR + k - 1 = the byte k
-// (1..32768) positions before the stage, read back from the committed output
+// ring index of an earlier byte of the stage (a near byte not yet resolved)
 constexpr u32 IE_VAL = 0xFF00u;
-constexpr u32 IE_FAR = 0x4000u;
-static_assert(IW_S <= IE_FAR && IE_FAR + 32768 <= IE_VAL, "stage entry encoding");
+static_assert(IW_S <= IE_VAL, "stage entry encoding");
 
 // Table geometry: a 9-bit literal/length root (zlib's ENOUGH_LENS = 852
 // entries covers every complete code) and an 8-bit distance root, so the LDS
@@ -126,12 +123,12 @@ constexpr u32 W_LCAP = 852;
 constexpr int W_DB = 8;
 constexpr u32 W_DCAP = 432;  // >= enough(30, 8, 15) = 402
 
-constexpr u32 IW_NDBG = 24;
+constexpr u32 IW_NDBG = 26;
 __device__ unsigned long long g_iw_dbg[32];
-enum { IWD_ROUNDS, IWD_BLOCKS, IWD_STAGES, IWD_GROUPS, IWD_P1_IT, IWD_P2_IT, IWD_CHAIN, IWD_MRR, IWD_CAPS,
-       IWD_NOEOB, IWT_HDR, IWT_P1, IWT_P2, IWT_CHAIN, IWT_HEADS, IWT_EXPAND, IWT_GATHER, IWT_JUMP,
-       IWT_COMMIT, IWT_TOTAL, IWD_FARIT, IWD_NBATCH, IWD_NPASS, IWD_NSTRAD };
-static_assert(IWD_NSTRAD < IW_NDBG, "debug slots");
+enum { IWD_ROUNDS, IWD_BLOCKS, IWD_STAGES, IWD_GROUPS, IWD_P1_IT, IWD_P2_IT, IWD_CHAIN, IWD_SPARE7, IWD_CAPS,
+       IWD_NOEOB, IWT_HDR, IWT_P1, IWT_P2, IWT_CHAIN, IWT_CLASSIFY, IWT_FAR, IWT_NEAR, IWT_PLACE,
+       IWT_COMMIT, IWT_TOTAL, IWD_FARIT, IWD_NBATCH, IWD_NPASS, IWD_NSTRAD, IWT_HTAB };
+static_assert(IWT_HTAB < IW_NDBG, "debug slots");
 
 struct IwLds {
     u32 ltab[W_LCAP];
@@ -141,6 +138,7 @@ struct IwLds {
             HuffLds lh, dh;
             u8 lens[320];
             u32 bcache[BI_CACHE_WORDS];
+            u32 hwin[130];  // 512 stream bytes from the code-length codes on (dynamic header)
         } h;
         struct {       // H round: marked extent (bits) of each segment, staged tokens, mark windows
             u32 mlim[65];
@@ -149,15 +147,11 @@ struct IwLds {
         } hr;
         struct {       // L phase: the stage ring, near-token descriptors and batch markers
             u16 ptr[IW_S];
-#if ZIW_TL
             union {
                 u32 desc[128];  // near token 2l + slot of the group: (offset - first near index) | dist << 16
                 u64 fd[64];     // far tokens of the group by rank: source of the first quad | (quad, r, L) << 32
             };
             u8 mk[64];      // near batch: token id + 1 at the lane of its first byte in the batch
-#else
-            u32 head[IW_S / 32];
-#endif
         } st;
     } u;
     u32 dbgc[IW_NDBG];
@@ -183,16 +177,6 @@ __device__ __forceinline__ u32 iw_incl_scan(u32 v) {
     const u32 t2 = t1 + (u32)__builtin_amdgcn_readlane((int)v, 47);
     const u32 lane = (u32)lane_id();
     return v + (lane < 16 ? 0u : (lane < 32 ? t0 : (lane < 48 ? t1 : t2)));
-}
-
-// OR over the wave (DPP row shifts, then the four row results), wave-uniform
-__device__ __forceinline__ u32 iw_wave_or(u32 v) {
-    v |= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
-    v |= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
-    v |= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
-    v |= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
-    return (u32)(__builtin_amdgcn_readlane((int)v, 15) | __builtin_amdgcn_readlane((int)v, 31) |
-                 __builtin_amdgcn_readlane((int)v, 47) | __builtin_amdgcn_readlane((int)v, 63));
 }
 
 __device__ __forceinline__ u32 iw_wave_sum(u32 v) {
@@ -404,25 +388,6 @@ __device__ __forceinline__ u32 swap_pos32(u32 p, const DType& t) {
     return (p & ~m) | (m - (p & m));
 }
 
-// entry k of a lane block held as 16 u32 (two u16 entries each)
-__device__ __forceinline__ u32 e16(const u32* w, u32 k) { return (k & 1) ? (w[k >> 1] >> 16) : (w[k >> 1] & 0xFFFFu); }
-__device__ __forceinline__ void e16_set(u32* w, u32 k, u32 v) {
-    w[k >> 1] = (k & 1) ? ((w[k >> 1] & 0xFFFFu) | (v << 16)) : ((w[k >> 1] & 0xFFFF0000u) | (v & 0xFFFFu));
-}
-__device__ __forceinline__ void blk_load(u32* w, const u16* p) {
-    const u32x4* q = (const u32x4*)p;
-#pragma unroll
-    for (u32 i = 0; i < 4; i++) {
-        const u32x4 x = q[i];
-        w[4 * i] = x.x; w[4 * i + 1] = x.y; w[4 * i + 2] = x.z; w[4 * i + 3] = x.w;
-    }
-}
-__device__ __forceinline__ void blk_store(u16* p, const u32* w) {
-    u32x4* q = (u32x4*)p;
-#pragma unroll
-    for (u32 i = 0; i < 4; i++) q[i] = u32x4{w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]};
-}
-
 // ---- dynamic block header, wave-parallel ------------------------------------
 // Same results, validity rules and order as read_dynamic
 // (zcg_inflate_common.h).  The code-length symbols are decoded at 64 bit
@@ -432,7 +397,7 @@ __device__ __forceinline__ void blk_store(u16* p, const u32* w) {
 // instructions instead of two dependent LDS round trips.
 template <int LB, u32 LCAP, int DB, u32 DCAP>
 __device__ __attribute__((always_inline)) int read_dynamic_wave(BitIn& b, u8* lens, HuffLds* lh, u32* ltab,
-                                                                HuffLds* dh, u32* dtab) {
+                                                                HuffLds* dh, u32* dtab, u32* hwin, u32* tcyc) {
     const u32 lane = (u32)lane_id();
     if (!bi_has(b, 14)) return R_EXHAUSTED;
     const u32 nlen = bi_bits(b, 5) + 257, ndist = bi_bits(b, 5) + 1, ncode = bi_bits(b, 4) + 4;
@@ -440,9 +405,12 @@ __device__ __attribute__((always_inline)) int read_dynamic_wave(BitIn& b, u8* le
     if (!bi_has(b, 3 * ncode)) return R_EXHAUSTED;
     const gu8* src = (const gu8*)b.src;
     const u64 nbytes = b.n;
-    // 32 stream bits from absolute bit q (bytes past the input read as 0)
-    auto bits32 = [&](u64 q) -> u32 {
-        const u64 by = q >> 3;
+    // The code lengths take < 300 bytes (<= 316 symbols of <= 7 + 7 bits):
+    // one coalesced load puts the 512 bytes from here in LDS, so the window
+    // walk below waits on LDS, not on a global round trip per window.
+    const u64 wb = (b.consumed >> 3) & ~7ull;  // window base byte
+    {
+        const u64 by = wb + 8ull * lane;
         u64 w = 0;
         if (by + 8 <= nbytes) {
             w = *(const __attribute__((address_space(1))) u64 __attribute__((aligned(1)))*)(src + by);
@@ -450,6 +418,23 @@ __device__ __attribute__((always_inline)) int read_dynamic_wave(BitIn& b, u8* le
             for (u32 k = 0; k < 8; k++)
                 if (by + k < nbytes) w |= (u64)src[by + k] << (8 * k);
         }
+        hwin[2 * lane] = (u32)w;
+        hwin[2 * lane + 1] = (u32)(w >> 32);
+        if (lane < 2) hwin[128 + lane] = 0;
+    }
+    __syncthreads();
+    // 32 stream bits from absolute bit q (bytes past the input read as 0)
+    auto bits32 = [&](u64 q) -> u32 {
+        const u32 r = (u32)(q - 8 * wb);
+        const u32 wi = r >> 5;
+        if (wi + 1 < 130) {
+            const u64 x = ((u64)hwin[wi + 1] << 32) | hwin[wi];
+            return (u32)(x >> (r & 31));
+        }
+        const u64 by = q >> 3;
+        u64 w = 0;
+        for (u32 k = 0; k < 8; k++)
+            if (by + k < nbytes) w |= (u64)src[by + k] << (8 * k);
         return (u32)(w >> (q & 7));
     };
     // the 3-bit code-length code lengths: lane i < ncode reads its own field
@@ -507,6 +492,7 @@ __device__ __attribute__((always_inline)) int read_dynamic_wave(BitIn& b, u8* le
     }
     b.cbase = ~0ull;
     bi_seek(b, pos);
+    const u64 t_tab = tcyc ? __builtin_readcyclecounter() : 0ull;
     __syncthreads();
     u8 dl = 0;
     if (lane < ndist) dl = lens[nlen + lane];
@@ -517,13 +503,14 @@ __device__ __attribute__((always_inline)) int read_dynamic_wave(BitIn& b, u8* le
     if (lens[256] == 0) return R_INVALID;  // "invalid code -- missing end-of-block"
     if (build_table(lens, 288, lh, ltab, LB, false, LCAP) != 0) return R_INVALID;
     if (build_table(lens + 288, 30, dh, dtab, DB, true, DCAP) != 0) return R_INVALID;
+    if (tcyc && lane == 0) *tcyc += (u32)(__builtin_readcyclecounter() - t_tab);
     return R_OK;
 }
 
 template <int LB, u32 LCAP, int DB, u32 DCAP>
 __device__ __attribute__((always_inline)) int read_block_header_wave(BitIn& b, bool* last, u32* type, u32* slen,
                                                                      u8* lens, HuffLds* lh, u32* ltab, HuffLds* dh,
-                                                                     u32* dtab) {
+                                                                     u32* dtab, u32* hwin, u32* tcyc) {
     if (!bi_has(b, 3)) return R_EXHAUSTED;
     const u32 hdr = bi_bits(b, 3);
     *last = hdr & 1;
@@ -533,7 +520,7 @@ __device__ __attribute__((always_inline)) int read_block_header_wave(BitIn& b, b
         bi_seek(b, b.consumed - 3);
         return read_block_header<LB, LCAP, DB, DCAP>(b, last, type, slen, lens, lh, ltab, dh, dtab);
     }
-    return read_dynamic_wave<LB, LCAP, DB, DCAP>(b, lens, lh, ltab, dh, dtab);
+    return read_dynamic_wave<LB, LCAP, DB, DCAP>(b, lens, lh, ltab, dh, dtab, hwin, tcyc);
 }
 
 constexpr u32 IW_NSLOT_MAX = 8192;
@@ -605,7 +592,8 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
         b.cbase = ~0ull;  // the reader's LDS cache shares storage with the stage
         wsync();
         r = read_block_header_wave<W_LB, W_LCAP, W_DB, W_DCAP>(b, &last, &type, &slen, L.u.h.lens, &L.u.h.lh, L.ltab,
-                                                               &L.u.h.dh, L.dtab);
+                                                               &L.u.h.dh, L.dtab, L.u.h.hwin,
+                                                               dbg ? &L.dbgc[IWT_HTAB] : nullptr);
         const u32 hdr_end = (u32)b.consumed;
         IW_T(IWT_HDR);
         if (r != R_OK) break;
@@ -859,6 +847,7 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
                 tb = gl[lb != 0xFFFFFFFFu ? iw_ta(lb, pb) : 0u];
             };
             u32 tq0a, tq0b, tq1a, tq1b, tq2a, tq2b, ok0, ok1, ok2;
+            u32 pcm = 0, pcj = 0;  // prefetch cursor: IW_GK groups past the cursor (groups inside a stage are whole)
             auto refetch = [&]() {
                 u32 cm1 = cm, cj1 = cj;
                 fetch2(cm1, cj1, tq0a, tq0b, ok0);
@@ -866,17 +855,18 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
                 fetch2(cm1, cj1, tq1a, tq1b, ok1);
                 advance(cm1, cj1, 128);
                 fetch2(cm1, cj1, tq2a, tq2b, ok2);
+                advance(cm1, cj1, 128);
+                pcm = cm1;
+                pcj = cj1;
             };
             refetch();
             bool round_done = false;
             while (!round_done && r == R_OK) {
                 const u64 S = P;
-                const u32 sa = (u32)(S & 31);
                 const u64 room = D - P;
-                const u32 capS = ZIW_TL ? IW_S : IW_S - sa;
+                const u32 capS = IW_S;
                 const u32 cap = room < capS ? (u32)room : capS;
                 const bool fin = (u64)cap == room;
-#if ZIW_TL
                 // Token-granular stage.  The ring is cleared, then every kept
                 // token writes its own entries: a literal its final byte; a FAR
                 // match (whole source before the stage) its final bytes, copied
@@ -927,11 +917,8 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
                 auto group2 = [&](u32& tqa, u32& tqb, u32& okq) -> bool {
                     IW_ADD(IWD_GROUPS, 1);
                     const u32 ta = (okq & 1u) ? tqa : (W_MARK | M_END), tb = (okq & 2u) ? tqb : (W_MARK | M_END);
-                    {
-                        u32 cm1 = cm, cj1 = cj;
-                        advance(cm1, cj1, 128 * IW_GK);
-                        fetch2(cm1, cj1, tqa, tqb, okq);
-                    }
+                    fetch2(pcm, pcj, tqa, tqb, okq);
+                    advance(pcm, pcj, 128);
                     const u64 ma = __ballot(w_marker(ta)), mb = __ballot(w_marker(tb));
                     const u32 fa = ma ? 2 * (u32)__builtin_ctzll(ma) : 128u, fb = mb ? 2 * (u32)__builtin_ctzll(mb) + 1 : 128u;
                     const u32 fm = fa < fb ? fa : fb;  // first marker, in token order
@@ -943,10 +930,11 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
                     const bool ka = ia < fm && (fin ? oa < cap : oa + la <= cap);
                     const bool kb = ib < fm && (fin ? ob < cap : ob + lb <= cap);
                     const u32 ntk = (u32)__popcll(__ballot(ka)) + (u32)__popcll(__ballot(kb));
+                    IW_T(IWT_PLACE);
                     const Tk A = classify(ta, oa, la, ka), B = classify(tb, ob, lb, kb);
                     if (A.kind == 1u) L.u.st.ptr[(S32 + A.o) & (IW_S - 1)] = (u16)(IE_VAL | A.d);
                     if (B.kind == 1u) L.u.st.ptr[(S32 + B.o) & (IW_S - 1)] = (u16)(IE_VAL | B.d);
-                    IW_T(IWT_HEADS);
+                    IW_T(IWT_CLASSIFY);
                     // far tokens, compacted one per lane (rank in token order):
                     // 16-byte source pieces from the aligned quad before the
                     // token, one quad of entries OR-ed per source dword (entries
@@ -999,7 +987,7 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
                             wsync();
                         }
                     }
-                    IW_T(IWT_EXPAND);
+                    IW_T(IWT_FAR);
                     // near bytes: index in the group's ordered near list
                     const u32 nla = A.kind == 3u ? A.L : 0u, nlb = B.kind == 3u ? B.L : 0u;
                     const u32 nps = nla + nlb;
@@ -1052,7 +1040,7 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
                             wsync();
                         }
                     }
-                    IW_T(IWT_GATHER);
+                    IW_T(IWT_NEAR);
                     if (ntk) {
                         const u32 t = ntk - 1;  // the last taken token: lane t / 2, slot t % 2
                         const u32 ea = incl - ps + la;
@@ -1080,226 +1068,12 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
                 IW_ADD(IWD_STAGES, 1);
                 if (__ballot(bad) != 0) { r = R_INVALID; break; }
                 const u32 emit = emitted < cap ? emitted : cap;  // a token may cross N: clip
-                IW_T(IWT_HEADS);
+                IW_T(IWT_CLASSIFY);
                 if (emit) {
                     iw_commit(L, dst, S, S + emit, tw);
                     P = S + emit;
                     IW_T(IWT_COMMIT);
                 }
-#else
-                L.u.st.head[lane] = 0;
-                wsync();
-                u32 emitted = 0;
-                bool far = false;
-                u32 why = 0;  // 1 final cut, 2 marker / round end, 3 capacity
-                u32 mcode = 0;
-                auto place = [&](u32 tk, u32 o) {
-                    u16 v;
-                    if (tk & W_MATCH) {
-                        const u32 d = (tk & 0x7FFF) + 1;
-                        if ((u64)d > S + o) far = true;  // before the stream start
-                        v = (u16)(d - 1);
-                    } else {
-                        v = (u16)(IE_VAL | (tk & 0xFF));
-                    }
-                    const u32 ri = (u32)((S + o) & (IW_S - 1));
-                    L.u.st.ptr[ri] = v;
-                    atomicOr(&L.u.st.head[ri >> 5], 1u << (ri & 31));
-                };
-                auto group2 = [&](u32& tqa, u32& tqb, u32& okq) -> bool {
-                    IW_ADD(IWD_GROUPS, 1);
-                    const u32 ta = (okq & 1u) ? tqa : (W_MARK | M_END), tb = (okq & 2u) ? tqb : (W_MARK | M_END);
-                    {
-                        u32 cm1 = cm, cj1 = cj;
-                        advance(cm1, cj1, 128 * IW_GK);
-                        fetch2(cm1, cj1, tqa, tqb, okq);
-                    }
-                    const u64 ma = __ballot(w_marker(ta)), mb = __ballot(w_marker(tb));
-                    const u32 fa = ma ? 2 * (u32)__builtin_ctzll(ma) : 128u, fb = mb ? 2 * (u32)__builtin_ctzll(mb) + 1 : 128u;
-                    const u32 fm = fa < fb ? fa : fb;  // first marker, in token order
-                    const u32 ia = 2 * lane, ib = ia + 1;
-                    const u32 la = ia < fm ? w_len(ta) : 0u, lb = ib < fm ? w_len(tb) : 0u;
-                    const u32 ps = la + lb;
-                    const u32 incl = iw_incl_scan(ps);
-                    const u32 oa = emitted + incl - ps, ob = oa + la;
-                    const bool ka = ia < fm && (fin ? oa < cap : oa + la <= cap);
-                    const bool kb = ib < fm && (fin ? ob < cap : ob + lb <= cap);
-                    const u32 ntk = (u32)__popcll(__ballot(ka)) + (u32)__popcll(__ballot(kb));
-                    if (ka) place(ta, oa);
-                    if (kb) place(tb, ob);
-                    if (ntk) {
-                        const u32 t = ntk - 1;  // the last taken token: lane t / 2, slot t % 2
-                        const u32 ea = incl - ps + la;
-                        emitted += (u32)__builtin_amdgcn_readlane((int)((t & 1) ? incl : ea), (int)(t >> 1));
-                    }
-                    advance(cm, cj, ntk);
-                    if (fin && emitted >= cap) { why = 1; return true; }
-                    if (ntk < 128) {
-                        if (ntk == fm) {
-                            why = 2;
-                            mcode = (u32)__builtin_amdgcn_readlane((int)((fm & 1) ? tb : ta), (int)(fm >> 1)) & 3u;
-                        } else {
-                            why = 3;
-                        }
-                        return true;
-                    }
-                    return false;
-                };
-                for (;;) {
-                    if (group2(tq0a, tq0b, ok0)) break;
-                    if (group2(tq1a, tq1b, ok1)) break;
-                    if (group2(tq2a, tq2b, ok2)) break;
-                }
-                refetch();  // the next stage starts at the cursor
-                IW_ADD(IWD_STAGES, 1);
-                if (__ballot(far) != 0) { r = R_INVALID; break; }
-                const u32 emit = emitted < cap ? emitted : cap;  // a token may cross N: clip
-                wsync();
-                IW_T(IWT_HEADS);
-                if (emit) {
-                    // ---- LZ77 resolution, my 32-entry block in registers -----------------
-                    const u64 B0 = S & ~31ull;
-                    const u32 rb = (u32)((B0 + 32ull * lane) & (IW_S - 1));  // my block's ring index
-                    const int xr0 = 32 * (int)lane - (int)sa;                 // my block's first entry, stage-relative
-                    const u32 hw = L.u.st.head[rb >> 5];
-                    // the token covering my first entry: the last token start below it
-                    const int lastpos = hw ? xr0 + 31 - (int)__builtin_clz(hw) : INT_MIN;
-                    int carry = iw_incl_max(lastpos);
-                    carry = __shfl_up(carry, 1, 64);
-                    if (lane == 0) carry = INT_MIN;
-                    u32 ev[16];
-                    blk_load(ev, L.u.st.ptr + rb);
-                    int mo = 0;
-                    u32 md = 0, mj = 0;
-                    bool in_match = false;
-                    if (!(hw & 1u) && carry != INT_MIN && xr0 >= 0 && xr0 < (int)emit) {
-                        mo = carry;
-                        md = (u32)L.u.st.ptr[(u32)((S + (u32)carry) & (IW_S - 1))] + 1;
-                        const u32 k0 = (u32)(xr0 - carry - 1);  // the loop steps mj before use
-                        mj = k0 < md ? k0 : k0 % md;
-                        in_match = md < IE_VAL;  // (a literal cannot cover a later byte)
-                    }
-                    u32 nfar = 0;
-#pragma unroll
-                    // branch-free per entry (the lanes' token layouts differ, so
-                    // branches would only juggle exec masks): a token start sets
-                    // the match state (a literal clears it), a continuation steps
-                    // mj; entries outside [0, emit) keep their value (before the
-                    // stage no head bit is set, so the state stays clear there)
-                    for (u32 k = 0; k < 32; k++) {
-                        const int xr = xr0 + (int)k;
-                        const bool valid = xr >= 0 && xr < (int)emit;
-                        const u32 v = e16(ev, k);
-                        const bool head = (hw >> k) & 1u;
-                        const bool start = head && v < IE_VAL;
-                        in_match = start || (!head && in_match);
-                        mo = start ? xr : mo;
-                        md = start ? v + 1 : md;
-                        mj = start ? 0u : ((mj + 1 == md) ? 0u : mj + 1);
-                        const bool act = valid && in_match;
-                        const int sp = mo - (int)md + (int)mj;
-                        const u32 nv = sp < 0 ? IE_FAR - 1 + (u32)(-sp) : (u32)((S + (u32)sp) & (IW_S - 1));
-                        e16_set(ev, k, act ? nv : v);
-                        nfar += (act && sp < 0) ? 1u : 0u;
-                    }
-                    IW_T(IWT_EXPAND);
-                    // far codes: bytes before the stage, from the committed output
-                    if (__ballot(nfar != 0)) {
-                        const gu8* gd = (const gu8*)dst;
-                        const u32 S32 = (u32)S;
-                        // The loads are scattered over 64 lanes' sources, so the
-                        // vector L1's address path (one line per lane request), not
-                        // latency, bounds this phase: four far entries of one match
-                        // (consecutive sources) come as one unaligned dword, the rest
-                        // byte by byte.  16 entries per round.
-                        typedef __attribute__((address_space(1))) u32 gu32_ua __attribute__((aligned(1)));
-#pragma unroll
-                        for (u32 qt = 0; qt < 2; qt++) {
-                            u32 qw[4], bv[16], pv[16];
-                            bool run[4];
-#pragma unroll
-                            for (u32 qd = 0; qd < 4; qd++) {
-                                bool all = !tw.swap;
-#pragma unroll
-                                for (u32 j = 0; j < 4; j++) {
-                                    const u32 k = qt * 16 + qd * 4 + j;
-                                    const u32 v = e16(ev, k);
-                                    const int xr = xr0 + (int)k;
-                                    const bool f = xr >= 0 && xr < (int)emit && v >= IE_FAR && v < IE_VAL;
-                                    pv[qd * 4 + j] = f ? S32 - (v - IE_FAR + 1) : 0xFFFFFFFFu;
-                                    all = all && f && (j == 0 || pv[qd * 4 + j] == pv[qd * 4] + j);
-                                }
-                                run[qd] = all;
-                                qw[qd] = all ? *(const gu32_ua*)(gd + pv[qd * 4]) : 0u;
-#pragma unroll
-                                for (u32 j = 0; j < 4; j++) {
-                                    const u32 pj = pv[qd * 4 + j];
-                                    bv[qd * 4 + j] = (!all && pj != 0xFFFFFFFFu) ? (u32)gd[swap_pos32(pj, tw)] : 0u;
-                                }
-                            }
-#pragma unroll
-                            for (u32 qd = 0; qd < 4; qd++)
-#pragma unroll
-                                for (u32 j = 0; j < 4; j++) {
-                                    const u32 k = qt * 16 + qd * 4 + j;
-                                    const u32 byte = run[qd] ? (qw[qd] >> (8 * j)) & 0xFF : bv[qd * 4 + j];
-                                    if (pv[qd * 4 + j] != 0xFFFFFFFFu) e16_set(ev, k, IE_VAL | byte);
-                                }
-                        }
-                    }
-                    blk_store(L.u.st.ptr + rb, ev);
-                    wsync();
-                    IW_T(IWT_GATHER);
-                    // pointer jumping: every pointer points strictly backwards, so
-                    // log2(IW_S) passes resolve any stage (the cap guards the invariant).
-                    // pm = my entries that are still pointers; a pass touches only
-                    // the entry positions some lane still needs (wave OR of pm,
-                    // scalar branches), so later passes cost what is left.
-                    u32 pm = 0;
-#pragma unroll
-                    for (u32 k = 0; k < 32; k++) {
-                        const int xr = xr0 + (int)k;
-                        if (xr >= 0 && xr < (int)emit && e16(ev, k) < IW_S) pm |= 1u << k;
-                    }
-                    for (u32 pass = 0;; pass++) {
-                        const u32 wm = iw_wave_or(pm);
-                        if (wm == 0) break;
-                        if (pass >= 13) { r = R_INVALID; break; }
-#pragma unroll
-                        for (u32 half = 0; half < 2; half++) {
-                            if (((wm >> (16 * half)) & 0xFFFFu) == 0) continue;
-                            // per position: a wave-uniform skip, then branch-free
-                            // lanes (every lane reads; the index is masked into the
-                            // ring, and lanes whose entry is final keep it)
-                            u32 nw[16];
-#pragma unroll
-                            for (u32 u = 0; u < 16; u++) {
-                                const u32 k = half * 16 + u;
-                                nw[u] = 0;
-                                if ((wm >> k) & 1u) nw[u] = (u32)L.u.st.ptr[e16(ev, k) & (IW_S - 1)];
-                            }
-#pragma unroll
-                            for (u32 u = 0; u < 16; u++) {
-                                const u32 k = half * 16 + u;
-                                if ((wm >> k) & 1u) {
-                                    const bool pk = (pm >> k) & 1u;
-                                    const u32 v = pk ? nw[u] : e16(ev, k);
-                                    e16_set(ev, k, v);
-                                    pm &= (pk && v >= IW_S) ? ~(1u << k) : ~0u;
-                                }
-                            }
-                        }
-                        blk_store(L.u.st.ptr + rb, ev);
-                        IW_ADD(IWD_MRR, 1);
-                        wsync();
-                    }
-                    IW_T(IWT_JUMP);
-                    if (r != R_OK) break;
-                    iw_commit(L, dst, S, S + emit, tw);
-                    P = S + emit;
-                    IW_T(IWT_COMMIT);
-                }
-#endif
                 if (why == 1) {
                     // output full: zlib's look-ahead continues at the first untaken token
                     boundary = emitted == cap;
