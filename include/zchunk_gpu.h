@@ -97,6 +97,12 @@ enum zcg_status {
  * kernel (coarse segments, 16 chunks per CU).  These flags force one. */
 #define ZCG_FLAG_INFLATE_BLOCK_PAR 0x2000u
 #define ZCG_FLAG_INFLATE_WAVE 0x4000u
+/* Gzip encode at levels 4-9 is byte-identical to zlib 1.2.11 / flate2
+ * (gzip.rs:54-56) by default.  This flag selects the faster segmented coder
+ * instead (16 KiB blocks, each ended by an empty stored block; the stream
+ * inflates to the same data, but its bytes differ from zlib's).  Levels 1-3
+ * always use the segmented coder. */
+#define ZCG_FLAG_GZIP_SEGMENTED 0x8000u
 
 /* CompressionType + its configuration (camelCase JSON keys in the reference). */
 typedef struct zcg_compression {
@@ -342,8 +348,10 @@ uint64_t zcg_chunk_key(const char* path, const char* separator, const uint64_t* 
  * stays in the path, and the key is refused with ZCG_ERR_NOT_FOUND when its
  * NET nesting (+1 per normal component, -1 per "..") is negative — the
  * reference's rule, so "a/../b" and even "../x" (net 0) are accepted, "../../x"
- * is not.  The path is
- * root + '/' + the normalised key.  *path_len (optional) receives its length;
+ * is not.  That rule lets "../x" resolve OUTSIDE the root: a reference flaw
+ * restated on purpose (parity); callers writing untrusted keys should refuse
+ * ".." components themselves.  The path is root + '/' + the normalised key
+ * (just the key when root is empty, as PathBuf::join does).  *path_len (optional) receives its length;
  * `out` (cap bytes, NUL-terminated) may be NULL to query the length, and a cap
  * below path_len + 1 gives ZCG_ERR_OUTPUT_TOO_SMALL.  Returns ZCG_OK. */
 int zcg_store_path(const char* root, const char* key, char* out, uint64_t cap, uint64_t* path_len);

@@ -196,7 +196,13 @@ import zlib  # noqa: E402
 from zarr_amd import Gzip  # noqa: E402
 
 
-def check_gzip_member(stream: bytes, content: bytes, level: int):
+def zlib_raw(content: bytes, level: int) -> bytes:
+    """flate2's deflate body: zlib raw deflate, windowBits -15, memLevel 8, default strategy."""
+    c = zlib.compressobj(level, zlib.DEFLATED, -15, 8, zlib.Z_DEFAULT_STRATEGY)
+    return c.compress(content) + c.flush()
+
+
+def check_gzip_member(stream: bytes, content: bytes, level: int, exact=None):
     eff = 6 if (level < 0 or level > 9) else level
     xfl = 2 if eff >= 9 else (4 if eff <= 1 else 0)
     assert stream[:10] == bytes([0x1F, 0x8B, 8, 0, 0, 0, 0, 0, xfl, 255])
@@ -204,6 +210,14 @@ def check_gzip_member(stream: bytes, content: bytes, level: int):
     assert crc == zlib.crc32(content) and isize == len(content) & 0xFFFFFFFF
     d = zlib.decompressobj(-15)
     assert d.decompress(stream[10:-8]) == content and d.eof and not d.unused_data
+    if exact if exact is not None else eff >= 4:
+        # levels 4-9: byte-identical to zlib (gzip.rs:54-56 -> flate2 -> zlib deflate_slow)
+        ref = zlib_raw(content, eff)
+        body = stream[10:-8]
+        if body != ref:
+            k = next((i for i in range(min(len(body), len(ref))) if body[i] != ref[i]), min(len(body), len(ref)))
+            raise AssertionError(f"gzip level {eff}: deflate body differs from zlib's at byte {k} "
+                                 f"(len {len(body)} vs {len(ref)})")
 
 
 def test_gzip_encode_doc_spec_exact():
@@ -276,6 +290,35 @@ def test_gzip_encode_quant_ratio():
     for a, s in zip(arrays, outs):
         check_gzip_member(s, a.tobytes(), 6)
     assert ours <= 1.4 * ref, (ours, ref)
+
+
+@pytest.mark.parametrize("level", [4, 5, 6, 7, 8, 9])
+def test_gzip_encode_matches_zlib_levels(level):
+    """write_chunk bytes = flate2/zlib's at every deflate_slow level, on a mixed
+    batch: the five DATASETS kinds, the C5 'quant' f32 chunk, and sizes that
+    end blocks / windows at their edges."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from bench import quant_chunk
+    D = 1 << 19
+    arrays = [_data(k, D, seed=3) for k in ("zeros", "uniform", "randwalk", "text", "ramp", "mixed")]
+    arrays.append(quant_chunk(7).view(np.uint8)[:D].copy())
+    meta = ArrayMetadata.new([D * len(arrays)], [D], "u1", Gzip(level))
+    st, outs = encode_batch(meta, arrays)
+    assert (st == 0).all()
+    for a, s in zip(arrays, outs):
+        check_gzip_member(s, a.tobytes(), level, exact=True)
+
+
+@pytest.mark.parametrize("nbytes", [1, 2, 3, 258, 259, 16383, 32506, 32768, 65274, 65275, 65536, 98304 + 7])
+def test_gzip_encode_matches_zlib_edges(nbytes):
+    """Window-slide and block-flush edges: zlib's bytes exactly (level 6)."""
+    arrays = [_data("text", nbytes, 4), _data("uniform", nbytes, 5), _data("zeros", nbytes), _data("ramp", nbytes)]
+    meta = ArrayMetadata.new([nbytes * 4], [nbytes], "u1", Gzip(6))
+    st, outs = encode_batch(meta, arrays)
+    assert (st == 0).all()
+    for a, s in zip(arrays, outs):
+        check_gzip_member(s, a.tobytes(), 6, exact=True)
 
 
 # ---- Xz (xz.rs:34-43: xz2 XzEncoder = lzma_easy_encoder(preset, CRC64)) ----

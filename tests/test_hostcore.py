@@ -384,3 +384,48 @@ def test_xz_opt_restatement_quant_ratio():
         ours += len(s)
         ref += len(lzma.compress(v, format=lzma.FORMAT_XZ, check=lzma.CHECK_CRC64, preset=6))
     assert tot / ours >= 0.97 * tot / ref, (tot / ours, tot / ref)
+
+
+# ---- gzip encode: the zlib deflate_slow restatement (zcg_zlib_core.h) ------------
+import zlib  # noqa: E402
+
+
+def host_deflate(b: bytes, level: int) -> bytes:
+    h = host()
+    h.zz_host_deflate.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64]
+    h.zz_host_deflate.restype = ctypes.c_int64
+    cap = len(b) + len(b) // 8 + 1024
+    out = ctypes.create_string_buffer(cap)
+    n = h.zz_host_deflate(b, len(b), level, out, cap)
+    assert n >= 0
+    return out.raw[:n]
+
+
+def zlib_raw(b: bytes, level: int) -> bytes:
+    c = zlib.compressobj(level, zlib.DEFLATED, -15, 8, zlib.Z_DEFAULT_STRATEGY)
+    return c.compress(b) + c.flush()
+
+
+@pytest.mark.parametrize("level", [4, 5, 6, 7, 8, 9])
+def test_zlib_core_matches_zlib(level):
+    """The GPU gzip encoder's core (match search per position, lazy parse,
+    trees) driven serially: byte-identical to the system zlib 1.2.11 (the
+    library flate2 wraps, gzip.rs:54-56) on mixed inputs, incl. window-slide
+    and block-flush edges."""
+    rng = np.random.default_rng(level)
+    cases = [b"", b"a", b"abcabcabcabc", bytes(70000), rng.integers(0, 256, 20000, dtype=np.uint8).tobytes(),
+             rng.integers(0, 4, 100000, dtype=np.uint8).tobytes(),
+             (b"the quick brown fox jumps over the lazy dog " * 2000)[:65275],
+             np.cumsum(rng.integers(-3, 4, 70000)).astype("<i2").tobytes(),
+             (np.arange(60000) % 4096).astype("<i2").tobytes()]
+    for b in cases:
+        assert host_deflate(b, level) == zlib_raw(b, level), (level, len(b))
+
+
+def test_zlib_core_matches_zlib_quant():
+    """C5's 'quant' f32 chunk (1 MiB) at level 6: zlib's bytes."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from bench import quant_chunk
+    b = quant_chunk(2).tobytes()
+    assert host_deflate(b, 6) == zlib_raw(b, 6)

@@ -234,6 +234,10 @@ def test_store_path_net_nesting_rule(tmp_path):
     for key in ("..", "/../", "../../x", "a/../../x/..", "./../", "a/b/../../.."):
         st, p = _native.store_path(root, key)
         assert st == _native.NOT_FOUND, (key, st, p)
+    # an empty root: PathBuf::from("").join(rel) is the relative path itself
+    for key, want in {"a/b": "a/b", "/c0/0": "c0/0", "": "", "./x": "x"}.items():
+        st, p = _native.store_path("", key)
+        assert st == _native.OK and p == want, (key, st, p)
     # the Python store goes through the same rule
     from zarr_amd.storage import FilesystemHierarchy
     from zarr_amd.chunk import ZarrIOError

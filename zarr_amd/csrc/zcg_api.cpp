@@ -32,6 +32,10 @@ struct zcg_ctx {
         void* p;
         size_t bytes;
         uint64_t used;
+        // the LZ4 decoder's side stream and its fork/join events, owned by
+        // this (ctx, stream) pair: created on first use, never shared
+        hipStream_t side = nullptr;
+        hipEvent_t fork = nullptr, join = nullptr;
     };
     static constexpr size_t WS_MAX = 4;
     std::vector<Ws> ws;
@@ -99,6 +103,35 @@ int ensure_pin(zcg_ctx* ctx, size_t need) {
 
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
+void ws_release(zcg_ctx::Ws& w) {
+    if (w.p) (void)hipFree(w.p);
+    if (w.fork) (void)hipEventDestroy(w.fork);
+    if (w.join) (void)hipEventDestroy(w.join);
+    if (w.side) (void)hipStreamDestroy(w.side);
+    w.p = nullptr;
+    w.fork = w.join = nullptr;
+    w.side = nullptr;
+}
+
+// the side stream + events of a workspace (nullptr side on failure: the
+// caller then runs single-stream)
+void ws_side(zcg_ctx::Ws* w) {
+    if (w->side) return;
+    hipStream_t st = nullptr;
+    hipEvent_t f = nullptr, j = nullptr;
+    if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess &&
+        hipEventCreateWithFlags(&f, hipEventDisableTiming) == hipSuccess &&
+        hipEventCreateWithFlags(&j, hipEventDisableTiming) == hipSuccess) {
+        w->side = st;
+        w->fork = f;
+        w->join = j;
+        return;
+    }
+    if (j) (void)hipEventDestroy(j);
+    if (f) (void)hipEventDestroy(f);
+    if (st) (void)hipStreamDestroy(st);
+}
+
 // the workspace of batches enqueued on `stream`, grown to at least `need` bytes
 int stream_ws(zcg_ctx* ctx, void* stream, size_t need, zcg_ctx::Ws** out) {
     zcg_ctx::Ws* w = nullptr;
@@ -112,7 +145,7 @@ int stream_ws(zcg_ctx* ctx, void* stream, size_t need, zcg_ctx::Ws** out) {
             for (size_t i = 1; i < ctx->ws.size(); i++)
                 if (ctx->ws[i].used < ctx->ws[v].used) v = i;
             (void)hipDeviceSynchronize();
-            if (ctx->ws[v].p) (void)hipFree(ctx->ws[v].p);
+            ws_release(ctx->ws[v]);
             ctx->ws.erase(ctx->ws.begin() + (long)v);
         }
         ctx->ws.push_back({stream, nullptr, 0, 0});
@@ -132,20 +165,7 @@ namespace {
 std::mutex g_dev_mu;
 std::map<int, uint32_t> g_dev_cus;
 std::map<std::pair<const void*, int>, hipError_t> g_lds_attr;
-std::map<int, hipStream_t> g_side;
 }  // namespace
-
-hipStream_t side_stream() {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    std::lock_guard<std::mutex> lk(g_dev_mu);
-    auto it = g_side.find(dev);
-    if (it != g_side.end()) return it->second;
-    hipStream_t st = nullptr;
-    if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) st = nullptr;
-    g_side[dev] = st;
-    return st;
-}
 
 uint32_t device_cu_count() {
     int dev = 0;
@@ -204,8 +224,7 @@ void zcg_destroy(zcg_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->store) store_slots_free(ctx->store);
-    for (auto& w : ctx->ws)
-        if (w.p) (void)hipFree(w.p);
+    for (auto& w : ctx->ws) ws_release(w);
     if (ctx->d_buf) (void)hipFree(ctx->d_buf);
     if (ctx->h_pin) (void)hipHostFree(ctx->h_pin);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -288,7 +307,8 @@ int zcg_decode_batch(zcg_ctx* ctx, const zcg_array* a, const zcg_chunk* d_chunks
         zcg_ctx::Ws* w = nullptr;
         const int r = stream_ws(ctx, stream, lz4_decode_ws_bytes(a, n), &w);
         if (r != ZCG_OK) return r;
-        e = launch_lz4_decode(a, d_chunks, n, d_status, w->p, w->bytes, s);
+        ws_side(w);
+        e = launch_lz4_decode(a, d_chunks, n, d_status, w->p, w->bytes, s, w->side, w->fork, w->join);
         break;
     }
     case ZCG_CODEC_GZIP: {

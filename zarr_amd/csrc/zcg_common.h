@@ -258,11 +258,13 @@ uint32_t device_cu_count();
 hipError_t lds_attr_once(const void* kernel, int bytes);
 // a second stream of the current device (created once; nullptr if that failed):
 // kernels of one call that may run side by side are forked onto it
-hipStream_t side_stream();
 hipError_t launch_raw(const zcg_array* a, const zcg_chunk* d_chunks, uint32_t n, int32_t* d_status,
                       uint64_t* d_out_len, int encode, hipStream_t s);
+// side / fork / join: the caller's side stream and events for the
+// side-by-side lane+wave run (nullptr side: single stream)
 hipError_t launch_lz4_decode(const zcg_array* a, const zcg_chunk* d_chunks, uint32_t n,
-                             int32_t* d_status, void* ws, uint64_t ws_bytes, hipStream_t s);
+                             int32_t* d_status, void* ws, uint64_t ws_bytes, hipStream_t s,
+                             hipStream_t side, hipEvent_t fork, hipEvent_t join);
 uint64_t lz4_decode_ws_bytes(const zcg_array* a, uint32_t n);
 hipError_t launch_lz4_encode(const zcg_array* a, const zcg_chunk* d_chunks, uint32_t n,
                              uint64_t* d_out_len, int32_t* d_status, void* ws, uint64_t ws_bytes,

@@ -34,6 +34,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include "zcg_common.h"
+#include "zcg_zlib_core.h"
 
 namespace zcg {
 
@@ -753,10 +754,684 @@ __global__ void df_best(const zcg_chunk* __restrict__ chunks, u32 c0, u64 D, u64
 
 }  // namespace
 
+// ===================== zlib-exact deflate (levels 4-9) ==========================
+// gzip.rs:54-56 writes flate2's GzEncoder, i.e. zlib deflate_slow at levels
+// 4-9.  zcg_zlib_core.h restates it as (1) a per-position match search,
+// (2) a short sequential lazy parse and (3) per-block trees; the kernels
+// below run (1) over every position (data-parallel), (2) one wave per chunk
+// (wave-uniform, scalar), (3) one wave per block, then place the blocks'
+// bits at their prefix-summed offsets.  Output bytes are identical to zlib's
+// (tests/test_hostcore.py pins the core on the CPU, tests/test_gpu_encode.py
+// the kernels).
+namespace {
+
+constexpr u64 DZ_SUPER_BYTES = 512ull << 20;  // input bytes per super-batch (match results kept for all)
+constexpr u32 DZ_TAILCAP = 2048;               // symbols a segment's parse may run past its end before syncing
+constexpr u32 DZ_HDRW = 96;                 // header bit-string words per block (<= 14 + 57 + 316 * 14 bits)
+
+struct DzBlock {     // one flushed block (zz::BlockRec) + its plan
+    u32 s0, s1, b0, b1;
+    u32 in_win, last, type, hbits;
+    u32 dbits, pad;
+    u64 bitoff;      // bit offset in the chunk's deflate stream
+    u32 lcode[zz::L_CODES];  // code | len << 16 (dynamic)
+    u32 dcode[zz::D_CODES];
+    u32 hdr[DZ_HDRW];        // the block-type bits and (dynamic) send_all_trees, LSB first
+};
+
+struct DzChunk {
+    u32 nblocks, status;
+    u64 bytes;       // deflate stream bytes
+    u64 fsym, fpos;  // the final symbol stream and its positions (u32 offsets from the workspace base)
+    u32 nsym, nloop;
+};
+
+struct DzLayout {
+    u32 m, sb, nbmax;
+    u64 tot, cub_bytes, outcap;
+    u64 off_ka, off_kb, off_va, off_vb, off_prev, off_cub, off_m2, off_sym, off_pos, off_bm, off_tail, off_ch, off_blk,
+        off_out, total;
+};
+
+DzLayout dz_layout(u64 D, u32 n) {
+    DzLayout y{};
+    u64 m = D ? DF_SUB_BYTES / D : n;
+    if (m < 1) m = 1;
+    if (m > n) m = n;
+    if (m > 65536) m = 65536;  // chunk id + 16 key bits fit 32
+    y.m = (u32)m;
+    y.tot = m * D;
+    u64 sb = D ? DZ_SUPER_BYTES / D : n;
+    sb = sb / m * m;
+    if (sb < m) sb = m;
+    if (sb > n) sb = n;
+    y.sb = (u32)sb;
+    y.nbmax = (u32)((D + zz::BLOCK_SYMS - 1) / zz::BLOCK_SYMS + 1);
+    y.outcap = (D + D / 8 + 4096 + 255) & ~255ull;
+    size_t cb = 0;
+    hipcub::DoubleBuffer<u32> k(nullptr, nullptr), v(nullptr, nullptr);
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, cb, k, v, (int)(y.tot ? y.tot : 1), 0, 32);
+    y.cub_bytes = (cb + 511) & ~255ull;
+    u64 p = 0;
+    auto take = [&](u64 bytes) { const u64 o = p; p = (p + bytes + 255) & ~255ull; return o; };
+    y.off_ka = take(4 * y.tot);
+    y.off_kb = take(4 * y.tot);
+    y.off_va = take(4 * y.tot);
+    y.off_vb = take(4 * y.tot);
+    y.off_prev = take(4 * y.tot);
+    y.off_cub = take(y.cub_bytes);
+    y.off_m2 = take(8 * (u64)y.sb * D + 4096);   // match results; then the final symbols + positions
+    y.off_sym = take(4 * (u64)y.sb * D + 4096);  // per-segment symbols (pass 1)
+    y.off_pos = take(4 * (u64)y.sb * D + 4096);  // their positions
+    y.off_bm = take(4 * (u64)y.sb * (D / 32 + 2));
+    y.off_tail = take(8ull * 64 * DZ_TAILCAP * y.sb);
+    y.off_ch = take(sizeof(DzChunk) * (u64)y.sb);
+    y.off_blk = take(sizeof(DzBlock) * (u64)y.sb * y.nbmax);
+    y.off_out = take(y.outcap * y.sb);
+    y.total = p;
+    return y;
+}
+
+// keys: chunk id << 16 | zlib's 15-bit hash of the serialised bytes p..p+2
+// (positions past D-3 are never inserted: a group of their own)
+__global__ void dz_keys(const zcg_chunk* __restrict__ chunks, u32 c0, u64 D, u64 tot, DType t,
+                        u32* __restrict__ keys, u32* __restrict__ vals) {
+    const u64 g = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= tot) return;
+    const u32 cl = (u32)(g / D);
+    const u64 p = g - (u64)cl * D;
+    const zcg_chunk ch = chunks[c0 + cl];
+    u32 h = 0x8000u;
+    if (p + 3 <= D && ch.src_len >= D) {
+        const u8* src = (const u8*)ch.src;
+        h = zz::hash3(df_ser1(src, p, t), df_ser1(src, p + 1, t), df_ser1(src, p + 2, t));
+    }
+    keys[g] = (cl << 16) | h;
+    vals[g] = (u32)g;
+}
+
+__global__ void dz_chain(u64 tot, const u32* __restrict__ keys, const u32* __restrict__ vals,
+                         u32* __restrict__ prev) {
+    const u64 j = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= tot) return;
+    prev[vals[j]] = (j > 0 && keys[j] == keys[j - 1]) ? vals[j - 1] : 0xFFFFFFFFu;
+}
+
+// zz::search at every position of the sub-batch: m2[g] = {full, red}.
+// (An LDS-staged variant -- each workgroup's 40 KB search window of bytes and
+// u16 chain links in LDS -- measured slower: 48.9 vs 45.2 ms per 128 C5
+// chunks, one 122 KB workgroup per CU could not hide its fill.)
+__global__ void dz_best(const zcg_chunk* __restrict__ chunks, u32 c0, u64 D, u64 tot, DType t, zz::Config cfg,
+                        const u32* __restrict__ prev, uint2* __restrict__ m2) {
+    const u64 g = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= tot) return;
+    const u32 cl = (u32)(g / D);
+    const u32 p = (u32)(g - (u64)cl * D);
+    zz::Match2 r{0u, 0u};
+    const zcg_chunk ch = chunks[c0 + cl];
+    if (ch.src_len >= D) {
+        const u8* src = (const u8*)ch.src;
+        const u64 cbase = (u64)cl * D;
+        auto b1 = [&](u32 i) -> u32 { return df_ser1(src, i, t); };
+        auto b4 = [&](u32 i) -> u32 { return df_ser4(src, i, t); };
+        auto pv = [&](u32 i) -> u32 {
+            const u32 q = prev[cbase + i];
+            return q == 0xFFFFFFFFu ? zz::NONE : (u32)(q - cbase);
+        };
+        r = zz::search(p, (u32)D, cfg, b4, b1, pv);
+    }
+    m2[g] = make_uint2(r.full, r.red);
+}
+
+// The lazy parse of one chunk, SEGMENT-PARALLEL: lane k parses positions
+// [k seg, (k+1) seg) from a canonical state (zz::PState: prev_len 2, not
+// pending -- the state after any match), marking the positions of its
+// canonical loop tops in a bitmap (pass 1).  Then each lane continues its
+// parse past its segment until it reaches a canonical loop top that a later
+// segment's parse also reached (pass 2): from there the two agree, so the
+// true parse is lane 0's path, its tail, the next segment's path from the
+// sync symbol, and so on (stitched into one stream).  A tail that does not
+// sync within DZ_TAILCAP symbols sends the chunk to a serial parse.  The
+// stitched stream and block records equal deflate_slow's
+// (tests/hostcore/zlib_ref.cpp zz_host_deflate_seg restates this exactly).
+__global__ __launch_bounds__(64) void dz_parse(const zcg_chunk* __restrict__ chunks, u32 c0, u32 nc, u64 D, DType t,
+                                              zz::Config cfg, u32* __restrict__ wbase, u64 off_m2, u64 off_sym,
+                                              u64 off_pos, u64 off_bm, u64 off_tail, DzChunk* __restrict__ cst,
+                                              DzBlock* __restrict__ blks, u32 nbmax) {
+    const u32 c = blockIdx.x;
+    if (c >= nc) return;
+    const u32 lane = threadIdx.x;
+    const zcg_chunk ch = chunks[c0 + c];
+    DzChunk* cs = cst + c;
+    if (ch.src_len < D) {
+        if (lane == 0) { cs->nblocks = 0; cs->status = ZCG_ERR_INVALID_DATA; }
+        return;
+    }
+    const u8* src = (const u8*)ch.src;
+    const u32 D32 = (u32)D;
+    const uint2* mc = (const uint2*)(wbase + off_m2) + (u64)c * D;  // match results (8 B / position)
+    u32* fsy = wbase + off_m2 + (u64)c * 2 * D;                      // final stream (reuses them)
+    u32* fps = fsy + D;
+    u32* psy = wbase + off_sym + (u64)c * D;                         // pass-1 symbols / positions
+    u32* pps = wbase + off_pos + (u64)c * D;
+    u32* bm = wbase + off_bm + (u64)c * (D / 32 + 2);
+    u32* tsy = wbase + off_tail + (u64)c * 2 * 64 * DZ_TAILCAP + (u64)lane * 2 * DZ_TAILCAP;
+    u32* tps = tsy + DZ_TAILCAP;
+    const u32 seg = D32 ? (((D32 + 63) / 64 + 31) & ~31u) : 32u;
+    const u32 nseg = D32 ? (D32 + seg - 1) / seg : 1u;
+    const bool act = lane < nseg;
+    const u32 S0 = lane * seg, S1 = (lane + 1 == nseg) ? D32 : (lane + 1) * seg;
+    auto get = [&](u32 p) -> zz::Match2 {
+        const uint2 v = mc[p];
+        return zz::Match2{v.x, v.y};
+    };
+    auto byte = [&](u32 i) -> u32 { return df_ser1(src, i, t); };
+    // ---- pass 1 ----
+    zz::PState st = zz::fresh_state(S0);
+    u32 n1 = 0, fin1 = 0;
+    if (act) {
+        for (u32 w = S0 / 32; w < (S1 + 31) / 32; w++) bm[w] = 0;
+        u32 cwi = S0 / 32, cwv = 0;
+        auto em = [&](u32 sym, u32 at) {
+            psy[S0 + n1] = sym;
+            pps[S0 + n1] = at;
+            n1++;
+        };
+        while (st.p < S1) {
+            if (zz::canonical(st)) {
+                const u32 wi = st.p >> 5;
+                if (wi != cwi) {
+                    if (cwv) bm[cwi] = cwv;
+                    cwi = wi;
+                    cwv = 0;
+                }
+                cwv |= 1u << (st.p & 31);
+            }
+            zz::step(st, D32, cfg, get, byte, em);
+        }
+        if (cwv) bm[cwi] = cwv;
+        if (lane + 1 == nseg && st.avail) {  // Z_FINISH: the pending literal
+            em(byte(st.p - 1), st.p - 1);
+            st.avail = 0;
+            fin1 = 1;
+        }
+    }
+    __syncthreads();  // every segment's bitmap is in place
+    // ---- pass 2 ----
+    u32 nt = 0, syncq = 0xFFFFFFFFu, tfin = 0, ovf = 0;
+    if (act && lane + 1 < nseg) {
+        auto em = [&](u32 sym, u32 at) {
+            tsy[nt] = sym;
+            tps[nt] = at;
+            nt++;
+        };
+        while (true) {
+            if (st.p >= D32) {
+                if (st.avail) {
+                    em(byte(st.p - 1), st.p - 1);
+                    tfin = 1;
+                }
+                break;
+            }
+            if (st.p >= S1 && zz::canonical(st) && ((bm[st.p >> 5] >> (st.p & 31)) & 1u)) {
+                syncq = st.p;
+                break;
+            }
+            if (nt + 1 >= DZ_TAILCAP) {
+                ovf = 1;
+                break;
+            }
+            zz::step(st, D32, cfg, get, byte, em);
+        }
+    }
+    __syncthreads();  // tails written
+    const bool any_ovf = __ballot(ovf != 0) != 0;
+    u32 nsym = 0, finlit = 0;
+    u64 fsel_sy = (u64)(fsy - wbase), fsel_ps = (u64)(fps - wbase);
+    if (!any_ovf) {
+        // ---- stitch (wave-uniform chain walk, cooperative copies) ----
+        auto copy = [&](const u32* ssy, const u32* sps, u32 n) {
+            for (u32 i = lane; i < n; i += 64) {
+                fsy[nsym + i] = ssy[i];
+                fps[nsym + i] = sps[i];
+            }
+            nsym += n;
+        };
+        u32 cur = 0, idx = 0;
+        while (true) {
+            const u32 cS0 = cur * seg;
+            const u32 cn1 = (u32)__builtin_amdgcn_readlane((int)n1, (int)cur);
+            copy(psy + cS0 + idx, pps + cS0 + idx, cn1 - idx);
+            if (cur + 1 == nseg) {
+                finlit = (u32)__builtin_amdgcn_readlane((int)fin1, (int)cur);
+                break;
+            }
+            const u32 cnt = (u32)__builtin_amdgcn_readlane((int)nt, (int)cur);
+            const u32* csy = wbase + off_tail + (u64)c * 2 * 64 * DZ_TAILCAP + (u64)cur * 2 * DZ_TAILCAP;
+            copy(csy, csy + DZ_TAILCAP, cnt);
+            const u32 q = (u32)__builtin_amdgcn_readlane((int)syncq, (int)cur);
+            if (q == 0xFFFFFFFFu) {
+                finlit = (u32)__builtin_amdgcn_readlane((int)tfin, (int)cur);
+                break;
+            }
+            const u32 nx = q / seg;
+            const u32 xS0 = nx * seg;
+            const u32 xn1 = (u32)__builtin_amdgcn_readlane((int)n1, (int)nx);
+            // the first symbol of segment nx at or after q (there is one: q is
+            // one of its canonical loop tops)
+            u32 j = 0;
+            for (u32 j0 = 0; j0 < xn1; j0 += 64) {
+                const u32 jj = j0 + lane;
+                const u64 m = __ballot(jj < xn1 && pps[xS0 + jj] >= q);
+                if (m) {
+                    j = j0 + (u32)__builtin_ctzll(m);
+                    break;
+                }
+                j = xn1;
+            }
+            cur = nx;
+            idx = j;
+        }
+    } else {
+        // ---- a tail did not sync: the serial parse into the pass-1 arrays ----
+        __syncthreads();
+        fsel_sy = (u64)(psy - wbase);
+        fsel_ps = (u64)(pps - wbase);
+        zz::PState s2 = zz::fresh_state(0);
+        u32 k = 0;
+        auto em = [&](u32 sym, u32 at) {
+            if (lane == 0) {
+                psy[k] = sym;
+                pps[k] = at;
+            }
+            k++;
+        };
+        auto gu = [&](u32 p) -> zz::Match2 {
+            const uint2 v = mc[p];
+            return zz::Match2{(u32)__builtin_amdgcn_readfirstlane(v.x), (u32)__builtin_amdgcn_readfirstlane(v.y)};
+        };
+        auto bu = [&](u32 i) -> u32 { return (u32)__builtin_amdgcn_readfirstlane(df_ser1(src, i, t)); };
+        while (s2.p < D32) zz::step(s2, D32, cfg, gu, bu, em);
+        if (s2.avail) {
+            em(bu(s2.p - 1), s2.p - 1);
+            finlit = 1;
+        }
+        nsym = k;
+    }
+    __syncthreads();  // the final stream is in place
+    const u32* Fs = wbase + fsel_sy;
+    const u32* Fp = wbase + fsel_ps;
+    const u32 nloop = nsym - finlit;
+    const u32 nb = zz::num_blocks(nloop);
+    auto P = [&](u32 i) -> u32 { return Fp[i]; };
+    auto Y = [&](u32 i) -> u32 { return Fs[i]; };
+    for (u32 k = lane; k < nb && k < nbmax; k += 64) {
+        const zz::BlockRec r = zz::block_rec(k, nsym, nloop, D32, P, Y);
+        DzBlock* o = blks + (u64)c * nbmax + k;
+        o->s0 = r.s0; o->s1 = r.s1; o->b0 = r.b0; o->b1 = r.b1; o->in_win = r.in_win; o->last = r.last;
+    }
+    if (lane == 0) {
+        cs->fsym = fsel_sy;
+        cs->fpos = fsel_ps;
+        cs->nsym = nsym;
+        cs->nloop = nloop;
+        cs->nblocks = nb <= nbmax ? nb : 0u;
+        cs->status = nb <= nbmax ? ZCG_OK : ZCG_ERR_INVALID_DATA;
+    }
+}
+
+struct DzPlanLds {
+    zz::BlockWork bw;
+    u32 lf[zz::L_CODES], df[zz::D_CODES];
+    u32 hbits;
+};
+
+// One wave per block: histogram, zlib's trees and block-type decision, the
+// header bit-string and the block's exact bit count.
+__global__ __launch_bounds__(64) void dz_plan(u32 nc, DzChunk* __restrict__ cst, DzBlock* __restrict__ blks,
+                                             u32 nbmax, const u32* __restrict__ wbase, u64 D) {
+    __shared__ DzPlanLds L;
+    const u32 c = blockIdx.x / nbmax, k = blockIdx.x % nbmax;
+    if (c >= nc) return;
+    const DzChunk cs = cst[c];
+    if (cs.status != ZCG_OK || k >= cs.nblocks) return;
+    DzBlock* B = blks + (u64)c * nbmax + k;
+    const u32* sy = wbase + cs.fsym;
+    const u32 lane = threadIdx.x;
+    const u32 s0 = B->s0, s1 = B->s1;
+    for (u32 i = lane; i < (u32)zz::L_CODES; i += 64) L.lf[i] = 0;
+    if (lane < (u32)zz::D_CODES) L.df[lane] = 0;
+    __syncthreads();
+    for (u32 i = s0 + lane; i < s1; i += 64) {
+        const u32 s = sy[i];
+        if (!(s & 0x80000000u)) {
+            atomicAdd(&L.lf[s & 0xFF], 1u);
+        } else {
+            atomicAdd(&L.lf[zz::len_code(((s >> 16) & 0xFF) + 3) + zz::LITERALS + 1], 1u);
+            atomicAdd(&L.df[zz::dist_code((s & 0xFFFF) + 1)], 1u);
+        }
+    }
+    __syncthreads();
+    if (lane == 0) L.lf[zz::END_BLOCK] = 1;
+    __syncthreads();
+    for (u32 i = lane; i < (u32)zz::HEAP_SIZE; i += 64) L.bw.lt.freq[i] = i < (u32)zz::L_CODES ? L.lf[i] : 0u;
+    for (u32 i = lane; i < (u32)(2 * zz::D_CODES + 1); i += 64) L.bw.dt.freq[i] = i < (u32)zz::D_CODES ? L.df[i] : 0u;
+    for (u32 i = lane; i < DZ_HDRW; i += 64) B->hdr[i] = 0;
+    __syncthreads();
+    if (lane == 0) {
+        const zz::BlockPlan pl = zz::plan_block(L.bw, B->b1 - B->b0, B->in_win != 0);
+        u32 hb = 0;
+        u32 acc = 0;  // header bit-string, LSB first, flushed word by word
+        auto put = [&](u32 v, u32 n) {
+            if (!n) return;
+            v &= n >= 32 ? 0xFFFFFFFFu : ((1u << n) - 1);
+            const u32 sh = hb & 31;
+            acc |= v << sh;
+            if (sh + n >= 32) {
+                B->hdr[hb >> 5] = acc;
+                acc = sh ? (v >> (32 - sh)) : 0u;
+            }
+            hb += n;
+        };
+        zz::send_header(L.bw, pl, B->last != 0, put);
+        if (hb & 31) B->hdr[hb >> 5] = acc;
+        B->type = pl.type;
+        B->hbits = hb;
+        L.hbits = hb;
+        u64 db = 0;
+        if (pl.type == zz::BT_DYN) {
+            for (int i = 0; i < zz::L_CODES; i++) {
+                const u32 x = i > zz::END_BLOCK ? zz::extra_lbits(i - 257) : 0u;
+                db += (u64)L.lf[i] * (L.bw.lt.len[i] + x);
+            }
+            for (int i = 0; i < zz::D_CODES; i++) db += (u64)L.df[i] * (L.bw.dt.len[i] + zz::extra_dbits(i));
+        } else if (pl.type == zz::BT_STATIC) {
+            for (int i = 0; i < zz::L_CODES; i++) {
+                const u32 x = i > zz::END_BLOCK ? zz::extra_lbits(i - 257) : 0u;
+                db += (u64)L.lf[i] * (zz::static_llen(i) + x);
+            }
+            for (int i = 0; i < zz::D_CODES; i++) db += (u64)L.df[i] * (5 + zz::extra_dbits(i));
+        }
+        B->dbits = (u32)db;
+    }
+    __syncthreads();
+    for (u32 i = lane; i < (u32)zz::L_CODES; i += 64) B->lcode[i] = L.bw.lt.code[i] | ((u32)L.bw.lt.len[i] << 16);
+    if (lane < (u32)zz::D_CODES) B->dcode[lane] = L.bw.dt.code[lane] | ((u32)L.bw.dt.len[lane] << 16);
+}
+
+// Per chunk: block bit offsets (a stored block pads to a byte after its 3
+// header bits), the stream length, and the boundary words cleared (blocks
+// OR their first and last words in; every other word has one writer).
+__global__ void dz_offsets(u32 nc, DzChunk* __restrict__ cst, DzBlock* __restrict__ blks, u32 nbmax, u8* out,
+                           u64 outcap) {
+    const u32 c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= nc) return;
+    DzChunk* cs = cst + c;
+    if (cs->status != ZCG_OK) return;
+    u32* ow = (u32*)(out + (u64)c * outcap);
+    u64 acc = 0;
+    for (u32 k = 0; k < cs->nblocks; k++) {
+        DzBlock* B = blks + (u64)c * nbmax + k;
+        B->bitoff = acc;
+        ow[acc >> 5] = 0;
+        if (B->type == zz::BT_STORED) {
+            acc += 3;
+            acc = (acc + 7) & ~7ull;
+            acc += 32 + 8ull * (B->b1 - B->b0);
+        } else {
+            acc += (u64)B->hbits + B->dbits;
+        }
+        if (acc) ow[(acc - 1) >> 5] = 0;
+    }
+    ow[acc >> 5] = 0;
+    cs->bytes = (acc + 7) >> 3;
+    if (cs->bytes + 64 > outcap) cs->status = ZCG_ERR_OUTPUT_TOO_SMALL;
+}
+
+// One wave per block: its bits at its offset.  Symbols 64 at a time: each
+// lane its symbol's bit count, a wave scan places them, and the bits are
+// OR-ed into an LDS ring of words flushed in order (the block's first and
+// last words with global atomics, the rest with plain stores).
+struct DzEmitLds {
+    u32 lc[zz::L_CODES], dc[zz::D_CODES];
+    u32 ring[1024];
+};
+
+__global__ __launch_bounds__(64) void dz_emit(const zcg_chunk* __restrict__ chunks, u32 c0, u32 nc, u64 D, DType t,
+                                             const DzChunk* __restrict__ cst, const DzBlock* __restrict__ blks,
+                                             u32 nbmax, const u32* __restrict__ wbase, u8* out, u64 outcap) {
+    __shared__ DzEmitLds L;
+    const u32 c = blockIdx.x / nbmax, k = blockIdx.x % nbmax;
+    if (c >= nc) return;
+    const DzChunk cs = cst[c];
+    if (cs.status != ZCG_OK || k >= cs.nblocks) return;
+    const DzBlock* B = blks + (u64)c * nbmax + k;
+    const u32 lane = threadIdx.x;
+    const u32* sy = wbase + cs.fsym;
+    u32* ow = (u32*)(out + (u64)c * outcap);
+    const u64 b0 = B->bitoff;
+    const u32 type = B->type;
+    const bool stat = type == zz::BT_STATIC;
+    for (u32 i = lane; i < (u32)zz::L_CODES; i += 64) L.lc[i] = B->lcode[i];
+    if (lane < (u32)zz::D_CODES) L.dc[lane] = B->dcode[lane];
+    for (u32 i = lane; i < 1024; i += 64) L.ring[i] = 0;
+    __syncthreads();
+    // bit position relative to the aligned word holding bit b0
+    const u64 w0 = b0 >> 5;
+    u32 pos = (u32)(b0 & 31);  // next bit, relative to 32 * w0
+    u32 fw = 0;                // ring words flushed (relative to w0)
+    u64 bend = 0;              // the block's end bit, relative to 32 * w0
+    {
+        u64 len = (u64)B->hbits + B->dbits;
+        if (type == zz::BT_STORED) len = 0;  // (computed below)
+        bend = pos + len;
+    }
+    auto put_lane = [&](u32 at, u32 v, u32 n) {  // at: relative bit; n <= 32
+        if (!n) return;
+        v &= n >= 32 ? 0xFFFFFFFFu : ((1u << n) - 1);
+        const u32 w = at >> 5, sh = at & 31;
+        atomicOr(&L.ring[w & 1023], v << sh);
+        if (sh + n > 32) atomicOr(&L.ring[(w + 1) & 1023], v >> (32 - sh));
+    };
+    auto flush_to = [&](u32 upto, bool fin) {  // words [fw, upto) are complete (fin: and the partial last one)
+        __syncthreads();
+        const u32 lastw = fin ? (u32)((bend + 31) >> 5) : upto;
+        for (u32 w = fw + lane; w < lastw; w += 64) {
+            const u32 v = L.ring[w & 1023];
+            const bool edge = (w == 0) || (fin && w == lastw - 1);
+            if (edge) atomicOr(&ow[w0 + w], v);
+            else ow[w0 + w] = v;
+            L.ring[w & 1023] = 0;
+        }
+        fw = lastw;
+        __syncthreads();
+    };
+    // header bit-string
+    {
+        const u32 hb = B->hbits;
+        for (u32 i = lane; i < (hb + 31) / 32; i += 64) {
+            const u32 n = (i + 1) * 32 <= hb ? 32u : hb - i * 32;
+            put_lane(pos + i * 32, B->hdr[i], n);
+        }
+        pos += hb;
+    }
+    if (type == zz::BT_STORED) {
+        pos = (pos + 7) & ~7u;
+        const u32 len = B->b1 - B->b0;
+        if (lane == 0) {
+            put_lane(pos, len & 0xFFFF, 16);
+            put_lane(pos + 16, ~len & 0xFFFF, 16);
+        }
+        pos += 32;
+        bend = pos + 8ull * len;
+        const u8* src = (const u8*)chunks[c0 + c].src;
+        for (u32 i0 = 0; i0 < len; i0 += 256) {
+            __syncthreads();
+            for (u32 i = i0 + lane; i < i0 + 256 && i < len; i += 64)
+                put_lane(pos + 8 * i, df_ser1(src, (u64)B->b0 + i, t), 8);
+            flush_to((pos + 8 * (i0 + 256 < len ? i0 + 256 : len)) >> 5, false);
+        }
+        flush_to(0, true);
+        return;
+    }
+    const u32 s0 = B->s0, s1 = B->s1;
+    for (u32 i0 = s0; i0 < s1; i0 += 64) {
+        const u32 i = i0 + lane;
+        zz::SymBits sb{{0, 0, 0, 0}, {0, 0, 0, 0}};
+        if (i < s1) {
+            const u32 s = sy[i];
+            if (stat) {
+                sb = zz::sym_bits(s, true, nullptr, nullptr, nullptr, nullptr);
+            } else if (!(s & 0x80000000u)) {
+                const u32 e = L.lc[s & 0xFF];
+                sb.v[0] = e & 0xFFFF;
+                sb.n[0] = e >> 16;
+            } else {
+                const u32 lc = (s >> 16) & 0xFF, dist = (s & 0xFFFF) + 1;
+                const int code = (int)zz::len_code(lc + 3);
+                const u32 e = L.lc[code + zz::LITERALS + 1];
+                sb.v[0] = e & 0xFFFF;
+                sb.n[0] = e >> 16;
+                sb.n[1] = zz::extra_lbits(code);
+                sb.v[1] = lc - zz::base_length(code);
+                const int dcd = (int)zz::dist_code(dist);
+                const u32 f = L.dc[dcd];
+                sb.v[2] = f & 0xFFFF;
+                sb.n[2] = f >> 16;
+                sb.n[3] = zz::extra_dbits(dcd);
+                sb.v[3] = (dist - 1) - zz::base_dist(dcd);
+            }
+        }
+        const u32 nbits = sb.n[0] + sb.n[1] + sb.n[2] + sb.n[3];
+        u32 x = nbits;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const u32 y = __shfl_up(x, d, 64);
+            if ((int)lane >= d) x += y;
+        }
+        u32 at = pos + x - nbits;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            // a part is <= 15 bits, so two parts always fit one 32-bit put
+            put_lane(at, sb.v[j], sb.n[j]);
+            at += sb.n[j];
+        }
+        pos += __shfl(x, 63, 64);
+        if (((pos >> 5) - fw) >= 512) flush_to(pos >> 5, false);
+    }
+    if (lane == 0) {
+        const u32 e = stat ? (zz::static_lcode(zz::END_BLOCK) | (7u << 16)) : L.lc[zz::END_BLOCK];
+        put_lane(pos, e & 0xFFFF, e >> 16);
+    }
+    flush_to(0, true);
+}
+
+// Per chunk: gzip header, the stream, CRC32/ISIZE (gzip_crc32 after it).
+__global__ __launch_bounds__(256) void dz_final(const zcg_chunk* __restrict__ chunks, u32 c0, u32 nc, u64 D,
+                                               u64 bound, u32 xfl, const DzChunk* __restrict__ cst, const u8* out,
+                                               u64 outcap, u64* __restrict__ out_len, i32* __restrict__ status) {
+    const u32 c = blockIdx.x, tid = threadIdx.x;
+    if (c >= nc) return;
+    const zcg_chunk ch = chunks[c0 + c];
+    const DzChunk cs = cst[c];
+    if (ch.src_len < D) { if (tid == 0) { status[c0 + c] = ZCG_ERR_INVALID_DATA; out_len[c0 + c] = 0; } return; }
+    if (cs.status != ZCG_OK) { if (tid == 0) { status[c0 + c] = (i32)cs.status; out_len[c0 + c] = 0; } return; }
+    if (ch.dst_cap < bound || ch.dst_cap < DF_HDR + cs.bytes + 8) {
+        if (tid == 0) { status[c0 + c] = ZCG_ERR_OUTPUT_TOO_SMALL; out_len[c0 + c] = 0; }
+        return;
+    }
+    u8* dst = (u8*)ch.dst;
+    const u8* o = out + (u64)c * outcap;
+    if (tid == 0) {
+        const u8 h[10] = {0x1F, 0x8B, 8, 0, 0, 0, 0, 0, (u8)xfl, 255};
+        for (u32 i = 0; i < 10; i++) dst[i] = h[i];
+    }
+    const u64 n = cs.bytes;
+    for (u64 i = (u64)tid * 16; i < n; i += 256 * 16) {
+        if (i + 16 <= n) st16(dst + DF_HDR + i, *(const u32x4*)(o + i));
+        else for (u64 j = i; j < n; j++) dst[DF_HDR + j] = o[j];
+    }
+    if (tid == 0) {
+        out_len[c0 + c] = DF_HDR + n + 8;
+        status[c0 + c] = ZCG_OK;
+    }
+}
+
+}  // namespace
+
+uint64_t deflate_exact_ws_bytes(const zcg_array* a, uint32_t n) {
+    const DType t = make_dtype(a->dtype);
+    const u64 D = a->chunk_num_elements * (u64)t.es;
+    if (n == 0) return 0;
+    return dz_layout(D, n).total;
+}
+
+static hipError_t launch_deflate_exact(const zcg_array* a, const zcg_chunk* d_chunks, uint32_t n, u32 level,
+                                       uint64_t* d_out_len, int32_t* d_status, void* ws, uint64_t ws_bytes,
+                                       hipStream_t s) {
+    const DType t = make_dtype(a->dtype);
+    const u64 D = a->chunk_num_elements * (u64)t.es;
+    const u32 xfl = level >= 9 ? 2u : (level <= 1 ? 4u : 0u);
+    const u64 bound = zcg_encode_bound(&a->compression, D);
+    const DzLayout y = dz_layout(D, n);
+    if (ws_bytes < y.total || y.tot >= (1ull << 31) || D >= (1ull << 31)) return hipErrorInvalidValue;
+    const zz::Config cfg = zz::level_config((int)level);
+    u8* w = (u8*)ws;
+    uint2* m2 = (uint2*)(w + y.off_m2);
+    DzChunk* cst = (DzChunk*)(w + y.off_ch);
+    DzBlock* blks = (DzBlock*)(w + y.off_blk);
+    u8* out = w + y.off_out;
+    for (u32 s0 = 0; s0 < n; s0 += y.sb) {
+        const u32 scnt = (n - s0) < y.sb ? (n - s0) : y.sb;
+        for (u32 c0 = s0; c0 < s0 + scnt && D > 0; c0 += y.m) {
+            const u32 cnt = (s0 + scnt - c0) < y.m ? (s0 + scnt - c0) : y.m;
+            const u64 tot = (u64)cnt * D;
+            u32 *ka = (u32*)(w + y.off_ka), *kb = (u32*)(w + y.off_kb);
+            u32 *va = (u32*)(w + y.off_va), *vb = (u32*)(w + y.off_vb);
+            const u32 G = (u32)((tot + 255) / 256);
+            u32 cbits = 0;
+            while ((1u << cbits) < cnt) cbits++;
+            hipLaunchKernelGGL(dz_keys, dim3(G), dim3(256), 0, s, d_chunks, c0, D, tot, t, ka, va);
+            hipcub::DoubleBuffer<u32> dk(ka, kb), dv(va, vb);
+            size_t cb = y.cub_bytes;
+            hipError_t e = hipcub::DeviceRadixSort::SortPairs(w + y.off_cub, cb, dk, dv, (int)tot, 0,
+                                                              (int)(16 + cbits), s);
+            if (e != hipSuccess) return e;
+            hipLaunchKernelGGL(dz_chain, dim3(G), dim3(256), 0, s, tot, dk.Current(), dv.Current(),
+                               (u32*)(w + y.off_prev));
+            hipLaunchKernelGGL(dz_best, dim3(G), dim3(256), 0, s, d_chunks, c0, D, tot, t, cfg,
+                               (const u32*)(w + y.off_prev), m2 + (u64)(c0 - s0) * D);
+        }
+        hipLaunchKernelGGL(dz_parse, dim3(scnt), dim3(64), 0, s, d_chunks, s0, scnt, D, t, cfg, (u32*)w,
+                           y.off_m2 / 4, y.off_sym / 4, y.off_pos / 4, y.off_bm / 4, y.off_tail / 4, cst, blks,
+                           y.nbmax);
+        const u64 nbk = (u64)scnt * y.nbmax;
+        hipLaunchKernelGGL(dz_plan, dim3((u32)nbk), dim3(64), 0, s, scnt, cst, blks, y.nbmax, (const u32*)w, D);
+        hipLaunchKernelGGL(dz_offsets, dim3((scnt + 63) / 64), dim3(64), 0, s, scnt, cst, blks, y.nbmax, out,
+                           y.outcap);
+        hipLaunchKernelGGL(dz_emit, dim3((u32)nbk), dim3(64), 0, s, d_chunks, s0, scnt, D, t, (const DzChunk*)cst,
+                           (const DzBlock*)blks, y.nbmax, (const u32*)w, out, y.outcap);
+        hipLaunchKernelGGL(dz_final, dim3(scnt), dim3(256), 0, s, d_chunks, s0, scnt, D, bound, xfl,
+                           (const DzChunk*)cst, (const u8*)out, y.outcap, (u64*)d_out_len, (i32*)d_status);
+    }
+    const u64 Lsl = D / 64;
+    CrcShift op;
+    crc_shift_op(Lsl, op.m);
+    hipLaunchKernelGGL(gzip_crc32, dim3(n), dim3(64), 0, s, d_chunks, n, D, Lsl, op, (const u64*)d_out_len,
+                       (const i32*)d_status, t);
+    return hipGetLastError();
+}
+
+static bool deflate_exact_level(const zcg_array* a) {
+    const int level = zcg_effective_gzip_level(a->compression.gzip_level);
+    return level >= 4 && (a->compression.flags & ZCG_FLAG_GZIP_SEGMENTED) == 0;
+}
+
 uint64_t deflate_ws_bytes(const zcg_array* a, uint32_t n) {
     const DType t = make_dtype(a->dtype);
     const u64 D = a->chunk_num_elements * (u64)t.es;
     if (n == 0) return 0;
+    if (deflate_exact_level(a)) return deflate_exact_ws_bytes(a, n);
     return df_layout(D, n).total;
 }
 
@@ -772,6 +1447,7 @@ hipError_t launch_deflate(const zcg_array* a, const zcg_chunk* d_chunks, uint32_
     const DType t = make_dtype(a->dtype);
     const u64 D = a->chunk_num_elements * (u64)t.es;
     const u32 level = (u32)zcg_effective_gzip_level(a->compression.gzip_level);
+    if (deflate_exact_level(a)) return launch_deflate_exact(a, d_chunks, n, level, d_out_len, d_status, ws, ws_bytes, s);
     const u32 xfl = level >= 9 ? 2u : (level <= 1 ? 4u : 0u);
     const u32 nseg = (u32)((D + DF_SEG - 1) / DF_SEG);
     const u64 bound = zcg_encode_bound(&a->compression, D);

@@ -1099,7 +1099,8 @@ uint64_t lz4_decode_ws_bytes(const zcg_array* a, uint32_t n) {
 }
 
 hipError_t launch_lz4_decode(const zcg_array* a, const zcg_chunk* d_chunks, uint32_t n, int32_t* d_status,
-                             void* ws, uint64_t ws_bytes, hipStream_t s) {
+                             void* ws, uint64_t ws_bytes, hipStream_t s, hipStream_t side, hipEvent_t fork,
+                             hipEvent_t join) {
     if (n == 0) return hipSuccess;
     const DType t = make_dtype(a->dtype);
     const u64 D = a->chunk_num_elements * (u64)t.es;
@@ -1120,7 +1121,7 @@ hipError_t launch_lz4_decode(const zcg_array* a, const zcg_chunk* d_chunks, uint
         const bool corun = !forced && waves >= LZ_CORUN_LO && waves < LZ_CORUN_HI;
         const bool wave = (fl & ZCG_FLAG_LZ4_WAVE_PER_BLOCK) ||
                           (!(fl & ZCG_FLAG_LZ4_LANE_PER_BLOCK) && !corun && waves < LZ_LANE_MIN_BLOCKS);
-        hipStream_t s2 = corun ? side_stream() : nullptr;
+        hipStream_t s2 = corun && fork && join ? side : nullptr;
         if (wave) {
             hipLaunchKernelGGL(lz4_blocks_kernel, dim3((u32)((waves + 3) / 4)), dim3(256), 0, s, d_chunks, n, D,
                                (u32)S, a->compression.flags, (const Lz4ChunkInfo*)info, slots);
@@ -1129,10 +1130,7 @@ hipError_t launch_lz4_decode(const zcg_array* a, const zcg_chunk* d_chunks, uint
             // stream at the same time: the lane kernel is latency-bound and the
             // wave kernel VALU-bound, so they share the CUs
             const u32 n1 = (u32)((u64)n * LZ_CORUN_PCT / 100);
-            hipEvent_t fork = nullptr, join = nullptr;
-            hipError_t e = hipEventCreateWithFlags(&fork, hipEventDisableTiming);
-            if (e == hipSuccess) e = hipEventCreateWithFlags(&join, hipEventDisableTiming);
-            if (e == hipSuccess) e = hipEventRecord(fork, s);
+            hipError_t e = hipEventRecord(fork, s);
             if (e == hipSuccess) e = hipStreamWaitEvent(s2, fork, 0);
             if (e != hipSuccess) return e;
             const u64 w2 = (u64)(n - n1) * S;
@@ -1144,8 +1142,6 @@ hipError_t launch_lz4_decode(const zcg_array* a, const zcg_chunk* d_chunks, uint
                                    d_chunks, n1, D, (u32)S, a->compression.flags, (const Lz4ChunkInfo*)info, slots);
             e = hipEventRecord(join, s2);
             if (e == hipSuccess) e = hipStreamWaitEvent(s, join, 0);
-            (void)hipEventDestroy(fork);
-            (void)hipEventDestroy(join);
             if (e != hipSuccess) return e;
         } else {
             hipLaunchKernelGGL(lz4_lanes_kernel, dim3((u32)((waves + LZ_LWG - 1) / LZ_LWG)), dim3(LZ_LWG), 0, s,

@@ -520,10 +520,14 @@ extern "C" int zcg_store_path(const char* root, const char* key, char* out, uint
         p = *e ? e + 1 : e;
     }
     if (nest < 0) return ZCG_ERR_NOT_FOUND;
+    // PathBuf::from(root).join(rel): an empty root joins to the relative path
     std::string path = root;
     if (!rel.empty()) {
-        if (path.empty() || path.back() != '/') path += '/';
-        path += rel;
+        if (path.empty()) path = rel;
+        else {
+            if (path.back() != '/') path += '/';
+            path += rel;
+        }
     }
     if (path_len) *path_len = path.size();
     if (!out || cap < path.size() + 1) {

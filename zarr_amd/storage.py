@@ -73,7 +73,9 @@ class FilesystemHierarchy:
     def _path(self, key: str) -> str:
         """FilesystemHierarchy::get_path (filesystem.rs:151-190) through the
         C ABI (zcg_store_path): the key relative to the root, refused with
-        NotFound when its net nesting is negative."""
+        NotFound when its net nesting is negative.  Like the reference this
+        checks only the NET nesting, so '../x' and 'a/../../b' resolve outside
+        the root (a reference flaw kept for parity)."""
         st, p = _native.store_path(self.base_path, key)
         if st == _native.NOT_FOUND:
             raise ZarrIOError("NotFound", "Path name is outside this Zarr filesystem")
