@@ -54,6 +54,18 @@ struct XzHostIO {
         Buf buf{dst + a};
         zx::bcj_serial(buf, b - a, id, start);
     }
+    void sha256(uint64_t a, uint64_t b, uint32_t* h) const {
+        zx::sha256_init(h);
+        uint64_t q = a;
+        for (; q + 64 <= b; q += 64) {
+            uint32_t m[16];
+            for (int i = 0; i < 16; i++)
+                m[i] = ((uint32_t)dst[q + 4 * i] << 24) | ((uint32_t)dst[q + 4 * i + 1] << 16) |
+                       ((uint32_t)dst[q + 4 * i + 2] << 8) | dst[q + 4 * i + 3];
+            zx::sha256_compress(h, m);
+        }
+        zx::sha256_tail(h, dst + q, (uint32_t)(b - q), b - a);
+    }
     uint64_t check(uint32_t id, uint64_t a, uint64_t b) const {
         if (id == 4) {
             uint64_t c = ~0ull;

@@ -9,7 +9,30 @@
  * hash5 of 5 bytes, candidates more than 65 535 back skipped.
  * tests/test_hostcore.py checks it byte for byte against liblz4's own
  * LZ4_compress_fast; the GPU encoder (zcg_lz4_enc.hip) restates the same
- * steps with a wave-parallel search.  Never linked into the product. */
+ * steps with a wave-parallel search.  Never linked into the product.
+ *
+ * It follows liblz4's LZ4_compress_generic closely (its search order and
+ * hash-table updates decide the bytes), so it carries liblz4's notice:
+ *   LZ4 - Fast LZ compression algorithm.  Copyright (C) 2011-present, Yann
+ *   Collet.  BSD 2-Clause License: Redistribution and use in source and
+ *   binary forms, with or without modification, are permitted provided that
+ *   the following conditions are met: * Redistributions of source code must
+ *   retain the above copyright notice, this list of conditions and the
+ *   following disclaimer.  * Redistributions in binary form must reproduce the
+ *   above copyright notice, this list of conditions and the following
+ *   disclaimer in the documentation and/or other materials provided with the
+ *   distribution.  THIS SOFTWARE IS PROVIDED BY THE COPYRIGHT HOLDERS AND
+ *   CONTRIBUTORS "AS IS" AND ANY EXPRESS OR IMPLIED WARRANTIES, INCLUDING, BUT
+ *   NOT LIMITED TO, THE IMPLIED WARRANTIES OF MERCHANTABILITY AND FITNESS FOR
+ *   A PARTICULAR PURPOSE ARE DISCLAIMED.  IN NO EVENT SHALL THE COPYRIGHT
+ *   OWNER OR CONTRIBUTORS BE LIABLE FOR ANY DIRECT, INDIRECT, INCIDENTAL,
+ *   SPECIAL, EXEMPLARY, OR CONSEQUENTIAL DAMAGES (INCLUDING, BUT NOT LIMITED
+ *   TO, PROCUREMENT OF SUBSTITUTE GOODS OR SERVICES; LOSS OF USE, DATA, OR
+ *   PROFITS; OR BUSINESS INTERRUPTION) HOWEVER CAUSED AND ON ANY THEORY OF
+ *   LIABILITY, WHETHER IN CONTRACT, STRICT LIABILITY, OR TORT (INCLUDING
+ *   NEGLIGENCE OR OTHERWISE) ARISING IN ANY WAY OUT OF THE USE OF THIS
+ *   SOFTWARE, EVEN IF ADVISED OF THE POSSIBILITY OF SUCH DAMAGE.
+ * (Altered: a restatement, not liblz4's source.) */
 #include <stdint.h>
 #include <string.h>
 

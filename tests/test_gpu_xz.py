@@ -41,7 +41,7 @@ def test_xz_transform(dt):
     check("xz", s, dt, n)
 
 
-@pytest.mark.parametrize("check_id", [lzma.CHECK_NONE, lzma.CHECK_CRC32, lzma.CHECK_CRC64])
+@pytest.mark.parametrize("check_id", [lzma.CHECK_NONE, lzma.CHECK_CRC32, lzma.CHECK_CRC64, lzma.CHECK_SHA256])
 @pytest.mark.parametrize("lclppb", [(3, 0, 2), (0, 4, 0), (4, 0, 4), (1, 3, 1), (2, 2, 3)])
 def test_xz_liblzma_variants(check_id, lclppb):
     lc, lp, pb = lclppb
@@ -161,7 +161,70 @@ def test_xz_filter_chains(chain):
             check("xz", s, "u1", D)
 
 
-def test_xz_unsupported_fails_loudly():
+def test_xz_sha256_check_parity():
+    """Check ID 10: liblzma verifies the SHA-256 of each block; whole and
+    partial reads, a corrupted digest byte, corrupted data, two blocks."""
+    rng = np.random.default_rng(11)
+    payload = rw(150000, seed=2).tobytes()
+    s = lzma.compress(payload, format=lzma.FORMAT_XZ, check=lzma.CHECK_SHA256, preset=6)
+    streams, Ds = [s], [len(payload), 70001]
+    isz = (int.from_bytes(s[-8:-4], "little") + 1) * 4  # backward size: the index
+    dend = len(s) - 12 - isz                            # the block's digest ends here
+    for k in (0, 5, 31):
+        b = bytearray(s)
+        b[dend - 32 + k] ^= 0x10
+        streams.append(bytes(b))
+    for _ in range(6):
+        b = bytearray(s)
+        b[int(rng.integers(24, dend - 32))] ^= 1 << int(rng.integers(0, 8))
+        streams.append(bytes(b))
+    small = lzma.compress(payload[:333], format=lzma.FORMAT_XZ, check=lzma.CHECK_SHA256)
+    streams.append(small)
+    Ds.append(333)
+    for st_ in streams:
+        for D in Ds:
+            check("xz", st_, "u1", D)
+
+
+def test_xz_lzma1_block_is_invalid_like_liblzma():
+    """An LZMA1 block (filter 0x4000000000000001 as the last filter, raw LZMA1
+    data with its end marker) in an .xz container: liblzma 5.2 answers
+    LZMA_DATA_ERROR, so the reference's read_chunk is InvalidData, and so is ours."""
+    import struct
+    import zlib
+
+    def vli(x):
+        out = b""
+        while True:
+            b, x = x & 0x7F, x >> 7
+            out += bytes([b | (0x80 if x else 0)])
+            if not x:
+                return out
+
+    def crc(b):
+        return struct.pack("<I", zlib.crc32(b) & 0xFFFFFFFF)
+
+    payload = rw(20000, seed=3).tobytes()
+    for lc, lp, pb, ds in [(3, 0, 2, 1 << 16), (0, 0, 0, 4096), (1, 3, 1, 1 << 20)]:
+        raw = lzma.compress(payload, format=lzma.FORMAT_RAW,
+                            filters=[{"id": lzma.FILTER_LZMA1, "lc": lc, "lp": lp, "pb": pb, "dict_size": ds}])
+        hb = bytes([0]) + vli(0x4000000000000001) + vli(5) + bytes([(pb * 5 + lp) * 9 + lc]) + struct.pack("<I", ds)
+        hsize = (len(hb) + 5 + 3) // 4 * 4
+        hdr = bytes([hsize // 4 - 1]) + hb
+        hdr += b"\0" * (hsize - 4 - len(hdr))
+        hdr += crc(hdr)
+        body = hdr + raw + b"\0" * ((4 - len(raw) % 4) % 4) + crc(payload)
+        idx = b"\0" + vli(1) + vli(len(hdr) + len(raw) + 4) + vli(len(payload))
+        idx += b"\0" * ((4 - len(idx) % 4) % 4)
+        idx += crc(idx)
+        ft = struct.pack("<I", len(idx) // 4 - 1) + bytes([0, 1])
+        s = b"\xfd7zXZ\0\x00\x01" + crc(b"\x00\x01") + body + idx + crc(ft) + ft + b"YZ"
+        for D in (len(payload), 100, 1):
+            assert zref.decode(zref.XZ, s, D)[0] == zref.INVALID_DATA
+            check("xz", s, "u1", D)
+
+
+def test_xz_bcj_open_tail_fails_loudly():
     """A read that stops inside an x86 BCJ block whose last decoded bytes
     could start a cut-off instruction (liblzma decodes past the end to finish
     it) raises instead of returning bytes that might differ."""

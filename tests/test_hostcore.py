@@ -429,3 +429,25 @@ def test_zlib_core_matches_zlib_quant():
     from bench import quant_chunk
     b = quant_chunk(2).tobytes()
     assert host_deflate(b, 6) == zlib_raw(b, 6)
+
+
+def test_xz_sha256_core_matches_liblzma():
+    """Check ID 10 (SHA-256) in the device core, host build: whole and partial
+    reads, every byte of the digest corrupted, random corruptions."""
+    rng = np.random.default_rng(23)
+    for n in (0, 1, 55, 56, 63, 64, 65, 119, 120, 5000, 70000):
+        payload = rng.integers(0, 4, n, dtype=np.uint8).tobytes()
+        s = lzma.compress(payload, format=lzma.FORMAT_XZ, check=lzma.CHECK_SHA256, preset=1)
+        same(s, n)
+        if n:
+            same(s, n // 2 + 1)
+        isz = (int.from_bytes(s[-8:-4], "little") + 1) * 4
+        dend = len(s) - 12 - isz
+        for k in range(32):
+            b = bytearray(s)
+            b[dend - 32 + k] ^= 1 << (k % 8)
+            same(bytes(b), n)
+        for _ in range(20):
+            b = bytearray(s)
+            b[int(rng.integers(0, len(s)))] ^= 1 << int(rng.integers(0, 8))
+            same(bytes(b), n)

@@ -694,6 +694,27 @@ struct BzeBlkShared {
 
 // libbz2 huffman.c BZ2_hbMakeCodeLengths (restated): weights carry the depth
 // in the low 8 bits; lengths over maxLen -> halve the frequencies and retry.
+// This function follows libbz2's statement by statement (its heap order
+// decides the code lengths, and so the bytes), so it carries libbz2's notice:
+//   bzip2/libbzip2 version 1.0.8 of 13 July 2019, Copyright (C) 1996-2019
+//   Julian Seward <jseward@acm.org>.  Redistribution and use in source and
+//   binary forms, with or without modification, are permitted provided that
+//   the following conditions are met: 1. Redistributions of source code must
+//   retain the above copyright notice, this list of conditions and the
+//   following disclaimer.  2. The origin of this software must not be
+//   misrepresented; you must not claim that you wrote the original software.
+//   If you use this software in a product, an acknowledgment in the product
+//   documentation would be appreciated but is not required.  3. Altered
+//   source versions must be plainly marked as such, and must not be
+//   misrepresented as being the original software.  4. The name of the author
+//   may not be used to endorse or promote products derived from this software
+//   without specific prior written permission.  THIS SOFTWARE IS PROVIDED BY
+//   THE AUTHOR "AS IS" AND ANY EXPRESS OR IMPLIED WARRANTIES, INCLUDING, BUT
+//   NOT LIMITED TO, THE IMPLIED WARRANTIES OF MERCHANTABILITY AND FITNESS FOR
+//   A PARTICULAR PURPOSE ARE DISCLAIMED.  IN NO EVENT SHALL THE AUTHOR BE
+//   LIABLE FOR ANY DIRECT, INDIRECT, INCIDENTAL, SPECIAL, EXEMPLARY, OR
+//   CONSEQUENTIAL DAMAGES ARISING IN ANY WAY OUT OF THE USE OF THIS SOFTWARE.
+// (Altered: a device restatement on LDS arrays, not libbz2's source.)
 __device__ void bze_make_lengths(u8* len, const u32* freq, i32 alpha, i32 maxlen, i32* heap, i32* weight,
                                  i32* parent) {
     for (i32 i = 0; i < alpha; i++) weight[i + 1] = (freq[i] == 0 ? 1 : (i32)freq[i]) << 8;

@@ -255,6 +255,34 @@ struct XzDevIO {
         }
         __threadfence_block();
     }
+    // SHA-256 of out[a, b) (check ID 10): 256 bytes per round come in as one
+    // dword per lane (big-endian words), the four blocks are compressed on
+    // the scalar path from v_readlane words
+    __device__ __attribute__((noinline)) void sha256(u64 a, u64 b, u32* h) {
+        zx::sha256_init(h);
+        u64 q = a;
+        while (q + 64 <= b) {
+            const u64 rem = (b - q) / 64;
+            const u32 nblk = rem < 4 ? (u32)rem : 4u;
+            u32 wv = 0;
+            if ((u32)lane < 16 * nblk) {
+                const u64 o = q + 4ull * lane;
+                wv = ((u32)dst[o] << 24) | ((u32)dst[o + 1] << 16) | ((u32)dst[o + 2] << 8) | (u32)dst[o + 3];
+            }
+            for (u32 k = 0; k < nblk; k++) {
+                u32 m[16];
+#pragma unroll
+                for (u32 i = 0; i < 16; i++) m[i] = __builtin_amdgcn_readlane(wv, (int)(16 * k + i));
+                zx::sha256_compress(h, m);
+            }
+            q += 64ull * nblk;
+        }
+        u8 last[64];
+        const u32 r = (u32)(b - q);
+        for (u32 i = 0; i < r; i++) last[i] = __builtin_amdgcn_readfirstlane((u32)dst[q + i]);
+        zx::sha256_tail(h, last, r, b - a);
+        for (u32 i = 0; i < 8; i++) h[i] = __builtin_amdgcn_readfirstlane(h[i]);
+    }
     __device__ __forceinline__ u64 check(u32 id, u64 a, u64 b) {
         if (id == 4) return wave_crc<u64, CRC64_POLY>((const u8*)dst, a, b);
         return (u64)wave_crc<u32, CRC32_POLY>((const u8*)dst, a, b);

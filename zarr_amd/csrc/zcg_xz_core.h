@@ -26,11 +26,14 @@
 // validating headers/sizes/checks up to that window's end and stops there
 // with OK.  Truncation before D bytes is UNEXPECTED_EOF.
 //
-// Not restated: LZMA1 (liblzma accepts it as the last filter, the kernel
-// reports UNSUPPORTED; delta and BCJ x86 / PowerPC / IA-64 / ARM / ARM-Thumb
-// / SPARC filters before LZMA2 are decoded), and the SHA-256
-// check (the block check is skipped for check ID 10, as for the IDs liblzma
-// does not know).  xz2's XzEncoder writes a single LZMA2 filter with CRC64.
+// Filters: LZMA2 with up to three delta / BCJ x86 / PowerPC / IA-64 / ARM /
+// ARM-Thumb / SPARC filters before it.  An LZMA1 block is InvalidData, as in
+// liblzma 5.2 (its .xz decoder rejects LZMA1 blocks with LZMA_DATA_ERROR).
+// Checks: CRC32, CRC64 and SHA-256 are verified; the IDs liblzma does not
+// know are skipped, as it does.  xz2's XzEncoder writes a single LZMA2 filter
+// with CRC64.  One difference stays: a read that stops inside a BCJ block
+// whose last bytes could start a cut-off instruction is UNSUPPORTED
+// (liblzma decodes past the caller's end to finish that instruction).
 #pragma once
 
 #include <stdint.h>
@@ -112,6 +115,66 @@ ZX_INL u32 crc32_byte(u32 c, u32 b) {
     c ^= b;
     for (int k = 0; k < 8; k++) c = (c >> 1) ^ (0xEDB88320u & (0u - (c & 1u)));
     return c;
+}
+
+// SHA-256 (FIPS 180-4) for the block check with ID 10 (liblzma verifies
+// it: a mismatch is LZMA_DATA_ERROR).  The IO streams the block's output
+// through sha256_compress (16 big-endian words per 64-byte block);
+// sha256_tail pads the last partial block.
+ZX_INL u32 sha_rotr(u32 x, u32 n) { return (x >> n) | (x << (32 - n)); }
+ZX_INL void sha256_init(u32* h) {
+    h[0] = 0x6a09e667u; h[1] = 0xbb67ae85u; h[2] = 0x3c6ef372u; h[3] = 0xa54ff53au;
+    h[4] = 0x510e527fu; h[5] = 0x9b05688cu; h[6] = 0x1f83d9abu; h[7] = 0x5be0cd19u;
+}
+ZX_INL void sha256_compress(u32* h, const u32* m) {
+    const u32 K[64] = {
+        0x428a2f98u, 0x71374491u, 0xb5c0fbcfu, 0xe9b5dba5u, 0x3956c25bu, 0x59f111f1u, 0x923f82a4u, 0xab1c5ed5u,
+        0xd807aa98u, 0x12835b01u, 0x243185beu, 0x550c7dc3u, 0x72be5d74u, 0x80deb1feu, 0x9bdc06a7u, 0xc19bf174u,
+        0xe49b69c1u, 0xefbe4786u, 0x0fc19dc6u, 0x240ca1ccu, 0x2de92c6fu, 0x4a7484aau, 0x5cb0a9dcu, 0x76f988dau,
+        0x983e5152u, 0xa831c66du, 0xb00327c8u, 0xbf597fc7u, 0xc6e00bf3u, 0xd5a79147u, 0x06ca6351u, 0x14292967u,
+        0x27b70a85u, 0x2e1b2138u, 0x4d2c6dfcu, 0x53380d13u, 0x650a7354u, 0x766a0abbu, 0x81c2c92eu, 0x92722c85u,
+        0xa2bfe8a1u, 0xa81a664bu, 0xc24b8b70u, 0xc76c51a3u, 0xd192e819u, 0xd6990624u, 0xf40e3585u, 0x106aa070u,
+        0x19a4c116u, 0x1e376c08u, 0x2748774cu, 0x34b0bcb5u, 0x391c0cb3u, 0x4ed8aa4au, 0x5b9cca4fu, 0x682e6ff3u,
+        0x748f82eeu, 0x78a5636fu, 0x84c87814u, 0x8cc70208u, 0x90befffau, 0xa4506cebu, 0xbef9a3f7u, 0xc67178f2u};
+    u32 w[16];
+    for (int i = 0; i < 16; i++) w[i] = m[i];
+    u32 a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
+    for (int i = 0; i < 64; i++) {
+        u32 wi;
+        if (i < 16) {
+            wi = w[i];
+        } else {
+            const u32 w15 = w[(i + 1) & 15], w2 = w[(i + 14) & 15];
+            const u32 s0 = sha_rotr(w15, 7) ^ sha_rotr(w15, 18) ^ (w15 >> 3);
+            const u32 s1 = sha_rotr(w2, 17) ^ sha_rotr(w2, 19) ^ (w2 >> 10);
+            wi = w[i & 15] = w[i & 15] + s0 + w[(i + 9) & 15] + s1;
+        }
+        const u32 S1 = sha_rotr(e, 6) ^ sha_rotr(e, 11) ^ sha_rotr(e, 25);
+        const u32 ch = (e & f) ^ (~e & g);
+        const u32 t1 = hh + S1 + ch + K[i] + wi;
+        const u32 S0 = sha_rotr(a, 2) ^ sha_rotr(a, 13) ^ sha_rotr(a, 22);
+        const u32 mj = (a & b) ^ (a & c) ^ (b & c);
+        const u32 t2 = S0 + mj;
+        hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+    }
+    h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
+}
+// last[0, r) = the message's final r < 64 bytes; total = message length
+ZX_INL void sha256_tail(u32* h, const u8* last, u32 r, u64 total) {
+    u8 blk[128];
+    for (u32 i = 0; i < 128; i++) blk[i] = 0;
+    for (u32 i = 0; i < r; i++) blk[i] = last[i];
+    blk[r] = 0x80;
+    const u32 nb = r + 9 <= 64 ? 1u : 2u;
+    const u64 bits = total * 8;
+    for (u32 k = 0; k < 8; k++) blk[64 * nb - 1 - k] = (u8)(bits >> (8 * k));
+    for (u32 q = 0; q < nb; q++) {
+        u32 m[16];
+        for (u32 i = 0; i < 16; i++)
+            m[i] = ((u32)blk[64 * q + 4 * i] << 24) | ((u32)blk[64 * q + 4 * i + 1] << 16) |
+                   ((u32)blk[64 * q + 4 * i + 2] << 8) | blk[64 * q + 4 * i + 3];
+        sha256_compress(h, m);
+    }
 }
 
 // 64-bit mixing hash of the (unpadded, uncompressed) size pairs; stands in
@@ -431,6 +494,7 @@ out:
 //   void copy(u64 d, u32 len);           append len bytes from d bytes back
 //   void copy_in(u64 ip, u32 len);       append input bytes [ip, ip+len)
 //   u64 check(u32 id, u64 a, u64 b);     CRC32 (id 1) / CRC64 (id 4) of out[a,b)
+//   void sha256(u64 a, u64 b, u32* h);   SHA-256 state words of out[a,b)
 //   void finish();                       make all output visible in dst
 //   void apply_delta(u64 a, u64 b, u32 dist);  delta filter decode of out[a,b) in place
 //   void apply_bcj(u64 a, u64 b, u32 id, u32 start);  BCJ filter decode of out[a,b) (bcj_* below)
@@ -743,7 +807,10 @@ ZX_INL int xz_decode_blocks(IO& io, FilterPending& fp) {
             const bool lz = fid[f] == 0x21 || fid[f] == 0x4000000000000001ull;
             if (lz != (f + 1 == nfilt)) return ST_INVALID;
         }
-        if (unsupported_chain) return full ? ST_OK : ST_UNSUPPORTED;
+        // liblzma 5.2's .xz decoder rejects an LZMA1 block with LZMA_DATA_ERROR
+        // (measured with the oracle over lc/lp/pb, dictionary sizes, checks and
+        // size fields), so it is InvalidData here too
+        if (unsupported_chain) return ST_INVALID;
 
         ip = h0 + hsize;
         const u64 cstart = ip;             // block compressed data start
@@ -890,6 +957,12 @@ ZX_INL int xz_decode_blocks(IO& io, FilterPending& fp) {
                 const u64 c = io.check(check_id, ustart, io.pos);
                 for (u32 k = 0; k < csz_check; k++)
                     if (io.in(ip + k) != (u32)((c >> (8 * k)) & 0xFF)) return ST_INVALID;
+            } else if (check_id == 10) {  // SHA-256 (the digest's bytes in order)
+                io.finish();
+                u32 hsh[8];
+                io.sha256(ustart, io.pos, hsh);
+                for (u32 k = 0; k < 32; k++)
+                    if (io.in(ip + k) != ((hsh[k >> 2] >> (24 - 8 * (k & 3))) & 0xFFu)) return ST_INVALID;
             }
             ip += csz_check;
         }
