@@ -30,8 +30,11 @@ value = decoded bytes of ALL ranks / max rank time.
 roofline: algorithmic bytes per launch = sum(C + D) over the batch (C =
 compressed stream bytes read once, D = decoded bytes written once) / the
 decode launch's average duration measured with HIP events on the stream the
-kernel runs on.  traffic: HBM bytes per launch from rocprofv3 --pmc passes
-over the same bench leg (tools/pmc_traffic.sh -> profiles/<round>_pmc_traffic.json).
+kernel runs on.  traffic: memory-side bytes per launch from rocprofv3 --pmc
+passes over the same bench leg (tools/pmc_traffic.sh ->
+profiles/<round>_pmc_traffic.json): reads = the L2's sized read requests
+(every miss is one 128 B request, profiles/r05_pmc_calibration.json), writes =
+WRITE_SIZE; Infinity-Cache hits are included, so it bounds HBM bytes above.
 cpu_baseline: the oracle (the reference's C codec libraries via
 oracle/zref.c) on host threads over a bounded sample, rank 0, N=1 only, at
 T = every CPU this process may run on and at T = 1.
@@ -69,7 +72,8 @@ LEG = {"gzip": {"pool": 64, "batch": 4096, "strong": False},
 ENCODE_LEG = {"gzip": (512, 2), "lz4": (1024, 3), "xz": (1024, 2), "bzip2": (512, 2)}
 # committed PMC traffic passes, newest first: a leg takes the first file that
 # measured it at the bench's own batch (kernels change between rounds)
-TRAFFIC_FILES = [os.path.join(ROOT, "profiles", f) for f in ("r04_pmc_traffic.json", "r03_pmc_traffic.json", "r02_pmc_traffic.json")]
+TRAFFIC_FILES = [os.path.join(ROOT, "profiles", f) for f in ("r05_pmc_traffic.json", "r04_pmc_traffic.json", "r03_pmc_traffic.json",
+                                                              "r02_pmc_traffic.json")]
 
 
 # ---------------------------------------------------------------- inputs ----
@@ -375,7 +379,8 @@ def decode_leg(codec, batch, strong, steps, warmup, pool, rank, world, dev, thre
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                      "traffic": pmc_traffic(codec, n),
                      "traffic_source": os.path.relpath(traffic_file(codec) or TRAFFIC_FILES[-1], ROOT) +
-                                       " (2*FETCH_SIZE + WRITE_SIZE per launch, same leg and batch)",
+                                       " (sized read requests + WRITE_SIZE per launch, same leg and batch; "
+                                       "multipliers profiles/r05_pmc_calibration.json)",
                      "kernel": KERNEL[codec], "kernel_ms": round(kern_ms, 4),
                      "algorithmic_bytes_per_launch": algo_bytes},
     }

@@ -30,6 +30,18 @@ def test_bzip2_large(data, level):
             check("bzip2", s, "u1", D, param=level)
 
 
+@pytest.mark.parametrize("meta_level", [1, 4])
+def test_bzip2_blocks_larger_than_metadata_level(meta_level):
+    """The stage-B kept-byte region is sized from the array's level; a stream
+    written at level 9 under level-1/4 metadata keeps fewer bytes per walk
+    and must decode the same (the reference ignores the level on read)."""
+    payload = b"".join(rw(450000, seed=s).tobytes() for s in range(2)) + bytes(300000)
+    s = bz2.compress(payload, 9)
+    for D in (len(payload), 900001, 123457):
+        check("bzip2", s, "u1", D, param=meta_level)
+    check_many("bzip2", [s, bz2.compress(payload[:500000], 9)], "u1", 500000, param=meta_level)
+
+
 @pytest.mark.parametrize("dt", ["<i2", ">i2", ">f4", ">u8", "bool", "i1"])
 def test_bzip2_transform(dt):
     from golden_util import dtype_info

@@ -475,7 +475,7 @@ def test_decode_never_writes_past_n(codec):
                 assert (out[i, D:] == 0xAB).all(), (D, i, flags)
 
 
-def check_many(codec, streams, dt, n, flags=0):
+def check_many(codec, streams, dt, n, flags=0, param=None):
     """Batch decode of many streams; each result must classify and decode like
     the oracle (one launch, so sweeps of corruptions stay fast)."""
     import torch
@@ -484,7 +484,7 @@ def check_many(codec, streams, dt, n, flags=0):
     st_ref, out_ref = zref.decode_batch(CODEC_IDS[codec], [np.frombuffer(s, np.uint8) for s in streams],
                                         n * es, elem_size=es, big_endian=be, is_bool=isb)
     packed = PackedStreams(streams, n * es, "cuda:0")
-    BatchCodec(0).decode(meta_for(codec, dt, n), packed, flags=flags)
+    BatchCodec(0).decode(meta_for(codec, dt, n, param), packed, flags=flags)
     torch.cuda.synchronize()
     st = packed.status.cpu().numpy()
     out = packed.dst.cpu().numpy().reshape(len(streams), n * es)

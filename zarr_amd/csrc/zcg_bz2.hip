@@ -353,7 +353,7 @@ struct BzBcLds {
 // orig, stored_crc, randomised, out_pos}.  Out: X.sh.out_pos advanced,
 // X.tcrc[0] = the block CRC; returns a final chunk status (>= 0) or -1 when
 // the stream continues.
-__device__ __forceinline__ int bz_block_bc(BzBcLds& X, const gu8* L, gu8* KB, gu8* T, gu32* W, gu8* dst,
+__device__ __forceinline__ int bz_block_bc(BzBcLds& X, const gu8* L, gu8* KB, u32 kcap, gu8* T, gu32* W, gu8* dst,
                                            u64 D, DType t, u32 vflags, u64& t_last) {
     const u32 tid = threadIdx.x, lane = tid & 63;
     const u32 wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -424,8 +424,13 @@ __device__ __forceinline__ int bz_block_bc(BzBcLds& X, const gu8* L, gu8* KB, gu
     // slot's kept-byte buffer KB; a walk longer than CAP records where it was
     // at step CAP and finishes after the ranking.  Walk lengths are close to
     // exponential with mean nblock / NR <= S, so CAP = BZ_KMUL * S leaves
-    // ~e^-BZ_KMUL of the bytes to the second walk (CAP = S: ~31 %).
-    const u32 CAP = S < 16 / BZ_KMUL ? 16u : BZ_KMUL * S;
+    // ~e^-BZ_KMUL of the bytes to the second walk (CAP = S: ~31 %).  The
+    // kept-byte region is sized from the array's block-size level (kcap per
+    // walk, a power of two >= 16); a stream whose blocks are larger than the
+    // level says keeps fewer bytes per walk and leaves more to the second
+    // walk, with the same output.
+    const u32 CAP0 = S < 16 / BZ_KMUL ? 16u : BZ_KMUL * S;
+    const u32 CAP = CAP0 < kcap ? CAP0 : kcap;
     gu32* buf32 = (gu32*)KB;
     const u32 Lp0 = L[p0];  // T[0] (the cycle's first byte)
     __syncthreads();
@@ -680,10 +685,21 @@ constexpr u64 BZ_A_OFF_ST = BZ_LBYTES + 18176;
 constexpr u64 BZ_A_SLOT = BZ_A_OFF_ST + 256;              // L, SEL, state
 constexpr u64 BZ_BC_OFF_W = BZ_LBYTES;
 constexpr u64 BZ_BC_OFF_K = BZ_BC_OFF_W + 4ull * BZ_NMAX + 128;
-constexpr u64 BZ_BC_SLOT = BZ_BC_OFF_K + (u64)BZ_KMUL * 1024 * (BZ_NSAMP + 1);  // T, W, kept walk bytes (CAP <= BZ_KMUL * 1024)
+// B/C slot: T, W, then the kept walk bytes, (NSAMP + 1) walks of kcap bytes
+// each; kcap follows the array's block-size level (bz_kcap), so a level-1
+// array's slot is 3.6 MB smaller than a level-9 one's
+__host__ __device__ constexpr u32 bz_kcap(int lvl) {
+    u32 S = 1;
+    while ((u64)BZ_NSAMP * S < 100000ull * (u64)lvl) S <<= 1;
+    return S < 16 / BZ_KMUL ? 16u : BZ_KMUL * S;
+}
+__host__ __device__ constexpr u64 bz_bc_slot(u32 kcap) {
+    return (BZ_BC_OFF_K + (u64)kcap * (BZ_NSAMP + 1) + 255) & ~255ull;
+}
+static_assert(bz_kcap(9) == BZ_KMUL * 1024 && bz_kcap(1) == BZ_KMUL * 128, "kept-byte caps");
 constexpr u32 BZ_NA = 4096;  // chunks in flight (stage A occupancy: 16 waves per CU)
 constexpr u32 BZ_NB = 1024;  // stage B/C workspace slots (>= resident B/C workgroups)
-static_assert(BZ_A_SLOT % 256 == 0 && BZ_BC_SLOT % 256 == 0, "slot alignment");
+static_assert(BZ_A_SLOT % 256 == 0 && BZ_BC_OFF_K % 16 == 0, "slot alignment");
 
 __device__ __forceinline__ void bz_io_init(BzDevIO& io, const zcg_chunk& ch, zb::Group* groups, u8* lensb, u8* seq,
                                            gu8* sel, gu8* L, int lane) {
@@ -791,8 +807,8 @@ __global__ __launch_bounds__(64) void bz2_stage_a_kernel(const zcg_chunk* __rest
 
 __global__ __launch_bounds__(256) void bz2_stage_bc_kernel(const zcg_chunk* __restrict__ chunks, u32 n, u64 D,
                                                            DType t, u8* __restrict__ wsa, u8* __restrict__ wsb,
-                                                           u32* __restrict__ owner, u32 nb, u32 c_base, u32 vflags,
-                                                           i32* __restrict__ status) {
+                                                           u32* __restrict__ owner, u32 nb, u32 kcap, u32 c_base,
+                                                           u32 vflags, i32* __restrict__ status) {
     __shared__ BzBcLds S;
     const u32 k = blockIdx.x;
     const u32 c = c_base + k;
@@ -814,10 +830,10 @@ __global__ __launch_bounds__(256) void bz2_stage_bc_kernel(const zcg_chunk* __re
     }
     __syncthreads();
     const u32 b = S.sh.p0;
-    u8* bslot = wsb + (u64)b * BZ_BC_SLOT;
+    u8* bslot = wsb + (u64)b * bz_bc_slot(kcap);
     const zcg_chunk ch = chunks[c];
     u64 t_last = __builtin_readcyclecounter();
-    const int fs = bz_block_bc(S, (const gu8*)slot, (gu8*)(bslot + BZ_BC_OFF_K), (gu8*)bslot, (gu32*)(bslot + BZ_BC_OFF_W), (gu8*)ch.dst, D, t,
+    const int fs = bz_block_bc(S, (const gu8*)slot, (gu8*)(bslot + BZ_BC_OFF_K), kcap, (gu8*)bslot, (gu32*)(bslot + BZ_BC_OFF_W), (gu8*)ch.dst, D, t,
                                vflags, t_last);
     __syncthreads();  // all B/C workspace accesses done
     if (tid == 0) {
@@ -835,8 +851,8 @@ __global__ __launch_bounds__(256) void bz2_stage_bc_kernel(const zcg_chunk* __re
 // The whole stream in one workgroup, for chunks the rounds did not finish.
 __global__ __launch_bounds__(256) void bz2_decode_kernel(const zcg_chunk* __restrict__ chunks, u32 n,
                                                          u64 D, DType t, u8* __restrict__ wsa, u8* __restrict__ wsb,
-                                                         u32* __restrict__ owner, u32 nb, u32 c_base, u32 vflags,
-                                                         i32* __restrict__ status) {
+                                                         u32* __restrict__ owner, u32 nb, u32 kcap, u32 c_base,
+                                                         u32 vflags, i32* __restrict__ status) {
     __shared__ zb::Group groups[6];
     __shared__ __attribute__((aligned(16))) u8 lensb[6 * 260];
     __shared__ __attribute__((aligned(16))) u8 seq[256];
@@ -861,7 +877,7 @@ __global__ __launch_bounds__(256) void bz2_decode_kernel(const zcg_chunk* __rest
     }
     __syncthreads();
     const u32 b = S.sh.p0;
-    u8* bslot = wsb + (u64)b * BZ_BC_SLOT;
+    u8* bslot = wsb + (u64)b * bz_bc_slot(kcap);
     BzDevIO io;
     zb::BzState s;
     if (wave == 0) {
@@ -890,7 +906,7 @@ __global__ __launch_bounds__(256) void bz2_decode_kernel(const zcg_chunk* __rest
             S.sh.randomised = sh_s.randomised;
         }
         __syncthreads();
-        const int fs = bz_block_bc(S, (const gu8*)slot, (gu8*)(bslot + BZ_BC_OFF_K), (gu8*)bslot, (gu32*)(bslot + BZ_BC_OFF_W), (gu8*)ch.dst,
+        const int fs = bz_block_bc(S, (const gu8*)slot, (gu8*)(bslot + BZ_BC_OFF_K), kcap, (gu8*)bslot, (gu32*)(bslot + BZ_BC_OFF_W), (gu8*)ch.dst,
                                    D, t, vflags, t_last);
         __syncthreads();
         if (fs >= 0) { final_status = fs; break; }
@@ -913,10 +929,15 @@ constexpr u64 BZ_OWNER_BYTES = 4ull * BZ_NB;
 
 const char* cfg_bz2() { return "bz2:KMUL=" ZCG_STR(ZB_KMUL); }
 
+// the array's block-size level (9 when the metadata does not say)
+static int bz_level(const zcg_array* a) {
+    const int l = a->compression.bzip2_block_size;
+    return l >= 1 && l <= 9 ? l : 9;
+}
+
 uint64_t bzip2_decode_ws_bytes(const zcg_array* a, uint32_t n) {
-    (void)a;
     if (n == 0) return 0;
-    return BZ_OWNER_BYTES + (u64)bz_na(n) * BZ_A_SLOT + (u64)bz_nb(n) * BZ_BC_SLOT;
+    return BZ_OWNER_BYTES + (u64)bz_na(n) * BZ_A_SLOT + (u64)bz_nb(n) * bz_bc_slot(bz_kcap(bz_level(a)));
 }
 
 hipError_t launch_bzip2_decode(const zcg_array* a, const zcg_chunk* d_chunks, uint32_t n,
@@ -934,8 +955,8 @@ hipError_t launch_bzip2_decode(const zcg_array* a, const zcg_chunk* d_chunks, ui
     // (each block emits >= 4/5 of its 100 000 * level bytes), + the block
     // after N and the end-of-stream record; anything longer finishes in the
     // whole-stream kernel
-    const int lvl = a->compression.bzip2_block_size >= 1 && a->compression.bzip2_block_size <= 9
-                        ? a->compression.bzip2_block_size : 9;
+    const int lvl = bz_level(a);
+    const u32 kcap = bz_kcap(lvl);
     const u64 per = 80000ull * (u64)lvl;
     const u32 rounds = (u32)((D + per - 1) / per) + 2;
     hipError_t e = hipMemsetAsync(owner, 0, BZ_OWNER_BYTES, s);
@@ -947,10 +968,10 @@ hipError_t launch_bzip2_decode(const zcg_array* a, const zcg_chunk* d_chunks, ui
         for (u32 r = 0; r < rounds; r++) {
             hipLaunchKernelGGL(bz2_stage_a_kernel, dim3(cnt), dim3(64), 0, s, d_chunks, n, wsa, c0, vflags, d_status);
             hipLaunchKernelGGL(bz2_stage_bc_kernel, dim3(cnt), dim3(BZ_T), 0, s, d_chunks, n, D, t, wsa, wsb, owner,
-                               nb, c0, vflags, d_status);
+                               nb, kcap, c0, vflags, d_status);
         }
         hipLaunchKernelGGL(bz2_decode_kernel, dim3(cnt), dim3(BZ_T), 0, s, d_chunks, n, D, t, wsa, wsb, owner, nb,
-                           c0, vflags, d_status);
+                           kcap, c0, vflags, d_status);
         e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
