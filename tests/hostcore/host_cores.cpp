@@ -23,23 +23,28 @@ struct XzHostIO {
     const uint8_t* src;
     uint8_t* dst;
     uint16_t probs[1846 + (0x300 << 4)];
+    uint8_t tail[64];  // output bytes from D on (a BCJ block's look-past, zx::xz_decode)
+    uint8_t& at(uint64_t i) { return i < D ? dst[i] : tail[i - D]; }
     void make_uniform() {}
     uint32_t in(uint64_t i) const { return src[i]; }
     uint32_t pget(uint32_t i) const { return probs[i]; }
     void pset(uint32_t i, uint32_t v) { probs[i] = (uint16_t)v; }
     void init_probs(uint32_t count) { for (uint32_t i = 0; i < count; i++) probs[i] = 1024; }
     bool lclp_ok(uint32_t) const { return true; }
-    void put(uint32_t b) { dst[pos++] = (uint8_t)b; }
-    uint32_t back(uint64_t dist) const { return dst[pos - 1 - dist]; }
+    void put(uint32_t b) { at(pos++) = (uint8_t)b; }
+    uint32_t back(uint64_t dist) { return at(pos - 1 - dist); }
     void copy(uint64_t d, uint32_t len) {
-        for (uint32_t k = 0; k < len; k++) dst[pos + k] = dst[pos + k - d];
+        for (uint32_t k = 0; k < len; k++) at(pos + k) = at(pos + k - d);
         pos += len;
     }
     void copy_in(uint64_t ip, uint32_t len) {
-        memcpy(dst + pos, src + ip, len);
+        for (uint32_t k = 0; k < len; k++) at(pos + k) = src[ip + k];
         pos += len;
     }
     void finish() {}
+    void reset() { pos = 0; }
+    uint32_t tail_byte(uint64_t i) { return at(i); }
+    void set_byte(uint64_t i, uint32_t v) { dst[i] = (uint8_t)v; }
     void apply_delta(uint64_t a, uint64_t b, uint32_t dist) {
         for (uint64_t i = a; i < b; i++)
             if (i >= a + dist) dst[i] = (uint8_t)(dst[i] + dst[i - dist]);
@@ -50,9 +55,9 @@ struct XzHostIO {
         void set(uint64_t i, uint32_t v) { p[i] = (uint8_t)v; }
     };
     uint32_t out_byte(uint64_t i) const { return dst[i]; }
-    void apply_bcj(uint64_t a, uint64_t b, uint32_t id, uint32_t start) {
+    zx::BcjState apply_bcj(uint64_t a, uint64_t b, uint32_t id, uint32_t start) {
         Buf buf{dst + a};
-        zx::bcj_serial(buf, b - a, id, start);
+        return zx::bcj_serial(buf, b - a, id, start);
     }
     void sha256(uint64_t a, uint64_t b, uint32_t* h) const {
         zx::sha256_init(h);

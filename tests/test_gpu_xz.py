@@ -121,10 +121,9 @@ def test_xz_delta_filter_dtypes():
 @pytest.mark.parametrize("name", ["X86", "ARM", "ARMTHUMB", "POWERPC", "SPARC", "IA64"])
 def test_xz_bcj_filters(name):
     """BCJ + LZMA2 chains (liblzma simple/*.c) against the oracle's liblzma:
-    whole reads, reads past the end, reads that stop inside the block (at
-    the sizes the host core decodes exactly rather than UNSUPPORTED,
-    tests/test_hostcore.py), start offsets, and a corruption sweep."""
-    from test_hostcore import bcj_payload, host_xz
+    whole reads, reads past the end, reads that stop inside the block (the
+    simple coder's look-past decode), start offsets, and a corruption sweep."""
+    from test_hostcore import bcj_payload
     fid = getattr(lzma, "FILTER_" + name)
     rng = np.random.default_rng(len(name) + 7)
     for n in (5, 4097, 200001):
@@ -132,8 +131,7 @@ def test_xz_bcj_filters(name):
             raw = bcj_payload(rng, n, fid)
             f0 = {"id": fid} if so == 0 else {"id": fid, "start_offset": so}
             s = lzma.compress(raw, format=lzma.FORMAT_XZ, filters=[f0, {"id": lzma.FILTER_LZMA2}])
-            part = [D for D in range(max(1, n // 3), max(1, n // 3) + 4) if host_xz(s, D)[0] != 4]
-            for D in sorted({n, n + 5, *part}):
+            for D in sorted({n, n + 5, *range(max(1, n // 3), max(1, n // 3) + 6)}):
                 check("xz", s, "u1", D)
     raw = bcj_payload(rng, 40000, fid)
     s = lzma.compress(raw, format=lzma.FORMAT_XZ, filters=[{"id": fid}, {"id": lzma.FILTER_LZMA2}])
@@ -156,7 +154,7 @@ def test_xz_filter_chains(chain):
     for n in (4097, 200001):
         raw = bcj_payload(rng, n, getattr(lzma, "FILTER_" + bcj[0]))
         s = lzma.compress(raw, format=lzma.FORMAT_XZ, filters=filters)
-        part = [D for D in range(n // 3, n // 3 + 4) if host_xz(s, D)[0] != 4]
+        part = [D for D in range(n // 3, n // 3 + 6) if host_xz(s, D)[0] != 4]
         for D in sorted({n, n + 5, *part}):
             check("xz", s, "u1", D)
 
@@ -224,15 +222,43 @@ def test_xz_lzma1_block_is_invalid_like_liblzma():
             check("xz", s, "u1", D)
 
 
-def test_xz_bcj_open_tail_fails_loudly():
-    """A read that stops inside an x86 BCJ block whose last decoded bytes
-    could start a cut-off instruction (liblzma decodes past the end to finish
-    it) raises instead of returning bytes that might differ."""
+@pytest.mark.parametrize("name", ["X86", "ARMTHUMB", "IA64", "SPARC"])
+def test_xz_bcj_look_past_parity(name):
+    """A read that stops inside a BCJ block: liblzma's simple coder decodes
+    past the caller's end to release the bytes its loop held back.  Every
+    stop offset over a range, and truncations / corruptions of the stream
+    around the compressed position of the stop (EOF when the input cannot
+    supply the look-past bytes, InvalidData when they are corrupt), with and
+    without an outer delta stage, one batch per case list, against the oracle."""
+    from test_hostcore import _min_input, bcj_payload
+    fid = getattr(lzma, "FILTER_" + name)
+    rng = np.random.default_rng(len(name) + 200)
+    raw = bcj_payload(rng, 30001, fid)
+    for chain in ([{"id": fid}], [{"id": lzma.FILTER_DELTA, "dist": 3}, {"id": fid}]):
+        s = lzma.compress(raw, format=lzma.FORMAT_XZ, filters=chain + [{"id": lzma.FILTER_LZMA2}])
+        for D in range(10000, 10024):
+            check("xz", s, "u1", D)
+        for D in (12345, 20002):
+            lo = _min_input(s, D)
+            cases = [s[:t] for t in range(lo - 24, min(len(s), lo + 24))]
+            for p in range(lo - 24, min(len(s), lo + 12)):
+                b = bytearray(s)
+                b[p] ^= 0x55
+                cases.append(bytes(b))
+            check_many("xz", cases, "u1", D)
+
+
+def test_xz_bcj_unmodelled_look_past_fails_loudly():
+    """The look-past decode is modelled for one BCJ stage fed by LZMA2 (outer
+    delta stages allowed).  A partial read of an x86-over-delta block whose
+    last bytes could start a cut-off instruction raises instead of returning
+    bytes that might differ."""
     from test_hostcore import bcj_payload, host_xz
     from zarr_amd import ArrayMetadata, DefaultChunk, NativeUnavailable
     from zarr_amd.compression import Xz
     payload = bcj_payload(np.random.default_rng(5), 5000, lzma.FILTER_X86)
-    s = lzma.compress(payload, format=lzma.FORMAT_XZ, filters=[{"id": lzma.FILTER_X86}, {"id": lzma.FILTER_LZMA2}])
+    s = lzma.compress(payload, format=lzma.FORMAT_XZ,
+                      filters=[{"id": lzma.FILTER_X86}, {"id": lzma.FILTER_DELTA, "dist": 1}, {"id": lzma.FILTER_LZMA2}])
     D = next(d for d in range(1000, 5000) if host_xz(s, d)[0] == 4)
     assert zref.decode(zref.XZ, s, D)[0] == zref.OK
     meta = ArrayMetadata.new([D], [D], "u1", Xz(6))

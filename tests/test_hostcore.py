@@ -140,12 +140,10 @@ BCJ_FILTERS = ["X86", "ARM", "ARMTHUMB", "POWERPC", "SPARC", "IA64"]
 @pytest.mark.parametrize("name", BCJ_FILTERS)
 def test_xz_core_bcj_filters_vs_liblzma(name):
     """BCJ + LZMA2 chains (liblzma simple/*.c): the core's block-end BCJ decode
-    against liblzma for whole reads, reads that stop inside the block (exact,
-    or UNSUPPORTED when the block's last bytes could start an instruction
-    the stop cut off), start offsets, and corruptions."""
+    against liblzma for whole reads, reads that stop inside the block (the
+    simple coder's look-past decode, exact), start offsets, and corruptions."""
     fid = getattr(lzma, "FILTER_" + name)
     rng = np.random.default_rng(len(name))
-    unsupported = 0
     for n in (1, 3, 4, 5, 7, 100, 4097, 70001):
         for so in (0, 16 if name == "IA64" else 4, 1024):
             raw = bcj_payload(rng, n, fid)
@@ -153,13 +151,9 @@ def test_xz_core_bcj_filters_vs_liblzma(name):
             s = lzma.compress(raw, format=lzma.FORMAT_XZ, filters=[f0, {"id": lzma.FILTER_LZMA2}])
             st, out = host_xz(s, n)
             assert st == 0 and out == raw
-            for D in (max(1, n // 3), n + 1):
+            for D in sorted({max(1, n // 3), max(1, n // 3) + 1, max(1, n - 2), n + 1}):
                 r1 = zref.decode(zref.XZ, s, D)
                 r2 = host_xz(s, D)
-                if r2[0] == 4 and r1[0] == zref.OK:  # UNSUPPORTED: only for a stop inside the block
-                    assert D < n
-                    unsupported += 1
-                    continue
                 assert r1[0] == r2[0], (n, so, D, r1[0], r2[0])
                 if r1[0] == zref.OK:
                     assert r1[1] == r2[1], (n, so, D)
@@ -174,12 +168,59 @@ def test_xz_core_bcj_filters_vs_liblzma(name):
             assert r1[1] == r2[1]
 
 
+def _min_input(s, D):
+    """The shortest prefix of s from which liblzma's read_exact of D succeeds."""
+    lo, hi = 0, len(s)
+    while lo < hi:
+        m = (lo + hi) // 2
+        if zref.decode(zref.XZ, s[:m], D)[0] == zref.OK:
+            hi = m
+        else:
+            lo = m + 1
+    return lo
+
+
+@pytest.mark.parametrize("name", BCJ_FILTERS)
+def test_xz_core_bcj_look_past_vs_liblzma(name):
+    """A read that stops inside a BCJ block: liblzma's simple coder holds back
+    the bytes its loop has not processed and decodes up to 2 x unfiltered_max
+    bytes past the end to release them (EOF if the input cannot supply them,
+    InvalidData if that data is corrupt).  Every stop offset over a range,
+    and truncations / corruptions of the stream around the compressed
+    position of the stop, against liblzma; outer delta stages too."""
+    fid = getattr(lzma, "FILTER_" + name)
+    rng = np.random.default_rng(len(name) + 100)
+    raw = bcj_payload(rng, 30001, fid)
+    for chain in ([{"id": fid}], [{"id": lzma.FILTER_DELTA, "dist": 3}, {"id": fid}]):
+        s = lzma.compress(raw, format=lzma.FORMAT_XZ, filters=chain + [{"id": lzma.FILTER_LZMA2}])
+        for D in range(10000, 10040):
+            r1, r2 = zref.decode(zref.XZ, s, D), host_xz(s, D)
+            assert r1[0] == r2[0] == zref.OK and r1[1] == r2[1], (D, r1[0], r2[0])
+        kinds = set()
+        for D in (12345, 20002):
+            lo = _min_input(s, D)
+            cases = [s[:t] for t in range(lo - 24, min(len(s), lo + 24))]
+            for p in range(lo - 24, min(len(s), lo + 12)):
+                b = bytearray(s)
+                b[p] ^= 0x55
+                cases.append(bytes(b))
+            for c in cases:
+                r1, r2 = zref.decode(zref.XZ, c, D), host_xz(c, D)
+                kinds.add(r1[0])
+                assert r1[0] == r2[0], (D, len(c), r1[0], r2[0])
+                if r1[0] == zref.OK:
+                    assert r1[1] == r2[1]
+        assert zref.OK in kinds and zref.EOF in kinds
+
+
 @pytest.mark.parametrize("chain", [("DELTA", "X86"), ("X86", "DELTA"), ("ARM", "DELTA", "SPARC"),
                                    ("DELTA", "DELTA"), ("ARMTHUMB", "IA64")])
 def test_xz_core_filter_chains_vs_liblzma(chain):
     """Chains of two or three delta / BCJ filters before LZMA2 (decoded in
     reverse chain order, each over the previous one's output) against
-    liblzma, whole and partial reads."""
+    liblzma, whole and partial reads.  A partial read may be UNSUPPORTED
+    only where the look-past decode is not modelled: a second BCJ stage, or
+    a delta stage under the BCJ."""
     rng = np.random.default_rng(len(chain) * 7 + len(chain[0]))
     filters = [{"id": lzma.FILTER_DELTA, "dist": 4} if c == "DELTA" else {"id": getattr(lzma, "FILTER_" + c)}
                for c in chain] + [{"id": lzma.FILTER_LZMA2}]
@@ -192,7 +233,7 @@ def test_xz_core_filter_chains_vs_liblzma(chain):
         for D in (max(1, n // 3), n + 1):
             r1, r2 = zref.decode(zref.XZ, s, D), host_xz(s, D)
             if r2[0] == 4 and r1[0] == zref.OK:
-                assert D < n
+                assert D < n and (len(bcj) > 1 or chain[-1] == "DELTA")
                 continue
             assert r1[0] == r2[0] and (r1[0] != zref.OK or r1[1] == r2[1]), (n, D)
 

@@ -68,8 +68,10 @@ struct XzDevIO {
     }
     __device__ __forceinline__ bool lclp_ok(u32 lclp) { return zx::probs_count(lclp) <= nprob_cap; }
 
-    // store ring bytes [gfl, e) to HBM, then fence
+    // store ring bytes [gfl, e) to HBM, then fence; bytes from D on (a BCJ
+    // block decoded past the caller's end, zx::xz_decode) stay in the ring
     __device__ __forceinline__ void flush(u64 e) {
+        if (e > D) e = D;
         const u64 a = gfl;
         u64 a16 = (a + 15) & ~15ull;
         if (a16 > e) a16 = e;
@@ -122,6 +124,16 @@ struct XzDevIO {
     __device__ __forceinline__ void finish() {
         if (gfl != pos) flush(pos);
     }
+    __device__ __forceinline__ void reset() {
+        pos = 0;
+        gfl = 0;
+    }
+    // output byte i >= D: in the ring (at most 32 past D, XZ_RING back)
+    __device__ __forceinline__ u32 tail_byte(u64 i) const {
+        return __builtin_amdgcn_readfirstlane((u32)ring[i & (XZ_RING - 1)]);
+    }
+    // output byte i < D in HBM (wave-uniform value; read back after finish())
+    __device__ __forceinline__ void set_byte(u64 i, u32 v) { dst[i] = (u8)v; }
     // delta filter decode of dst[a, b) in place (out[i] += out[i - dist]),
     // wave-parallel: rows of `dist` bytes, 64 rows per step, one wave scan
     // per column with the column's running sum carried in LDS (the model's
@@ -170,13 +182,17 @@ struct XzDevIO {
     };
     // an output byte already in HBM (after finish()), wave-uniform
     __device__ __forceinline__ u32 out_byte(u64 i) const { return __builtin_amdgcn_readfirstlane((u32)dst[i]); }
-    __device__ void apply_bcj(u64 a, u64 b, u32 id, u32 start) {
+    // returns where the serial loop would have stopped, and the x86 state there
+    __device__ zx::BcjState apply_bcj(u64 a, u64 b, u32 id, u32 start) {
         const u64 len = b > a ? b - a : 0;
         gu8* d = dst + a;
+        zx::BcjState st{0, 0u, start - 5};
         if (id == 7 || id == 5 || id == 9) {
+            st.stop = len & ~3ull;
             LaneBuf lb{d};
             for (u64 i = 4 * (u64)lane; i + 4 <= len; i += 4 * 64) zx::bcj_word(lb, i, id, start + (u32)i);
         } else if (id == 6) {
+            st.stop = len & ~15ull;
             LaneBuf lb{d};
             for (u64 i = 16 * (u64)lane; i + 16 <= len; i += 16 * 64) zx::bcj_ia64_bundle(lb, i, start + (u32)i);
         } else if (id == 4 && len >= 5) {
@@ -226,6 +242,9 @@ struct XzDevIO {
                     }
                 }
             }
+            st.stop = len - 4 > next ? len - 4 : next;
+            st.prev_mask = prev_mask;
+            st.prev_pos = prev_pos;
         } else if (id == 8) {
             GBuf g{d};
             u64 next = 0;
@@ -252,8 +271,13 @@ struct XzDevIO {
                     next = c + 4;
                 }
             }
+            if (len >= 4) {
+                const u64 e = (len - 3 + 1) & ~1ull;  // the first even position the loop cannot process
+                st.stop = e > next ? e : next;
+            }
         }
         __threadfence_block();
+        return st;
     }
     // SHA-256 of out[a, b) (check ID 10): 256 bytes per round come in as one
     // dword per lane (big-endian words), the four blocks are compressed on

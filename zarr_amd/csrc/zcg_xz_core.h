@@ -31,9 +31,11 @@
 // liblzma 5.2 (its .xz decoder rejects LZMA1 blocks with LZMA_DATA_ERROR).
 // Checks: CRC32, CRC64 and SHA-256 are verified; the IDs liblzma does not
 // know are skipped, as it does.  xz2's XzEncoder writes a single LZMA2 filter
-// with CRC64.  One difference stays: a read that stops inside a BCJ block
-// whose last bytes could start a cut-off instruction is UNSUPPORTED
-// (liblzma decodes past the caller's end to finish that instruction).
+// with CRC64.  A read that stops inside a BCJ block follows liblzma's simple
+// coder, which decodes past the caller's end to release the bytes its filter
+// loop held back (xz_decode below); only chains it does not model (two BCJ
+// stages, or a delta under the BCJ) keep UNSUPPORTED for a stop whose last
+// bytes could start a cut-off instruction.
 #pragma once
 
 #include <stdint.h>
@@ -248,7 +250,7 @@ ZX_INL u32 rc_bit(u32& range, u32& code, u32& p) {
 // all 32-bit (the kernel restricts streams and chunks to < 4 GiB).  Returns
 // ST_CONT when the chunk ended cleanly, otherwise the final status.
 struct LzJob {
-    u32 ip, lim, rlim, n, D, chunk_end, dict_start, dsz, u_end, kstart, csz, full;
+    u32 ip, lim, rlim, n, D, Dfull, chunk_end, dict_start, dsz, u_end, kstart, csz, full;
     u32 rc_range, rc_code, lc, lp, pb, state, rep0, rep1, rep2, rep3;
 };
 constexpr int ST_CONT = -1;
@@ -258,13 +260,13 @@ ZX_HOT int lzma_symbols(IO& io_r, LzJob& j) {
     IO io = io_r;
     io.make_uniform();  // device: function arguments arrive as per-lane values
     u32 ip = j.ip, lim = j.lim;
-    u32 rlim = j.rlim, n = j.n, D = j.D, chunk_end = j.chunk_end, dict_start = j.dict_start;
+    u32 rlim = j.rlim, n = j.n, D = j.D, Dfull = j.Dfull, chunk_end = j.chunk_end, dict_start = j.dict_start;
     u32 dsz = j.dsz, u_end = j.u_end, kstart = j.kstart, csz = j.csz;
     u32 fullw = j.full;
     u32 rc_range = j.rc_range, rc_code = j.rc_code;
     u32 lc = j.lc, lp = j.lp, pb = j.pb;
     u32 state = j.state, rep0 = j.rep0, rep1 = j.rep1, rep2 = j.rep2, rep3 = j.rep3;
-    ZX_U32(ip); ZX_U32(lim); ZX_U32(rlim); ZX_U32(n); ZX_U32(D); ZX_U32(chunk_end);
+    ZX_U32(ip); ZX_U32(lim); ZX_U32(rlim); ZX_U32(n); ZX_U32(D); ZX_U32(Dfull); ZX_U32(chunk_end);
     ZX_U32(dict_start); ZX_U32(dsz); ZX_U32(u_end); ZX_U32(kstart); ZX_U32(csz); ZX_U32(fullw);
     ZX_U32(rc_range); ZX_U32(rc_code); ZX_U32(lc); ZX_U32(lp); ZX_U32(pb);
     ZX_U32(state); ZX_U32(rep0); ZX_U32(rep1); ZX_U32(rep2); ZX_U32(rep3);
@@ -319,7 +321,7 @@ ZX_HOT int lzma_symbols(IO& io_r, LzJob& j) {
             ZX_U32(rep0); ZX_U32(rep1); ZX_U32(rep2); ZX_U32(rep3);
             if (frv != ST_CONT) ZX_RET(frv);
             if ((u32)io.pos > u_end) ZX_RET(ST_INVALID);  // more than the declared size
-            if ((u32)io.pos == D && !full) ZX_SET_FULL();
+            if ((u32)io.pos >= Dfull && !full) ZX_SET_FULL();  // (a match may step over Dfull < D)
             const u32 dlim = chunk_end < D ? chunk_end : D;
             if ((u32)io.pos == dlim) {
                 // the main loop ends at the dictionary limit; one more
@@ -497,7 +499,11 @@ out:
 //   void sha256(u64 a, u64 b, u32* h);   SHA-256 state words of out[a,b)
 //   void finish();                       make all output visible in dst
 //   void apply_delta(u64 a, u64 b, u32 dist);  delta filter decode of out[a,b) in place
-//   void apply_bcj(u64 a, u64 b, u32 id, u32 start);  BCJ filter decode of out[a,b) (bcj_* below)
+//   BcjState apply_bcj(u64 a, u64 b, u32 id, u32 start);  BCJ filter decode of out[a,b) (bcj_run below):
+//                                        where its loop stopped, and the x86 state there
+//   void reset();                        output position back to 0 (the stream is decoded again)
+//   u32 tail_byte(u64 i);                output byte i >= D (decoded past the caller's end)
+//   void set_byte(u64 i, u32 v);         output byte i < D (after finish())
 //   u32 out_byte(u64 i);                 output byte i (after finish())
 // A block whose chain is delta + LZMA2 (liblzma's delta decoder passes the
 // LZMA2 output through, then adds the byte `dist` back: out[i] += out[i-dist],
@@ -508,9 +514,10 @@ out:
 // unfiltered dictionary, which a block never shares with the next (its first
 // chunk resets the dictionary).  A BCJ filter converts an instruction only
 // when all its bytes are known; liblzma's simple coder decodes past the
-// caller's output end to finish one, so when decoding stops inside a BCJ
-// block and its last bytes could start an instruction (bcj_tail_open), the
-// result is UNSUPPORTED rather than possibly different bytes.
+// caller's output end to finish one.  For one BCJ stage fed by LZMA2 that
+// look-past decode is modelled exactly (xz_decode); for other chains a stop
+// whose last bytes could start an instruction (bcj_tail_open) is
+// UNSUPPORTED rather than possibly different bytes.
 // Chains of up to three such filters before LZMA2 (liblzma's limit) decode
 // in reverse chain order, each over the previous one's output.
 struct FilterPending {
@@ -581,14 +588,31 @@ ZX_INL void bcj_ia64_bundle(B& buf, u64 i, u32 now) {
     }
 }
 ZX_INL bool bcj_x86_ms(u32 b) { return b == 0 || b == 0xFF; }
+// Scan state of a BCJ filter where its loop stopped: `stop` = the first
+// position (relative to the block start) the loop did not process (liblzma's
+// `filtered`), and for x86 the prev_mask / prev_pos carried to the next call.
+struct BcjState {
+    u64 stop;
+    u32 prev_mask, prev_pos;
+};
+// bytes per loop step window: x86 5 (opcode + rel32), IA-64 16 (a bundle),
+// the others 4 (a word or a Thumb BL pair)
+ZX_INL u32 bcj_window(u32 id) { return id == 4 ? 5u : id == 6 ? 16u : 4u; }
+// liblzma's simple coder keeps 2 x unfiltered_max bytes of buffer
+// (simple_coder.c): x86 5, IA-64 16, the others 4
+ZX_INL u32 bcj_allocated(u32 id) { return 2u * (id == 4 ? 5u : id == 6 ? 16u : 4u); }
+// The filter loop over buf[i0, len) from state st (liblzma simple/*.c;
+// whole-block equivalent to its incremental calls).  Returns the new state;
+// *last = the last position < lim_last the loop processed (or ~0).
 template <class B>
-ZX_INL void bcj_serial(B& buf, u64 len, u32 id, u32 pos0) {
+ZX_INL BcjState bcj_run(B& buf, u64 i0, u64 len, u32 id, u32 pos0, BcjState st, u64 lim_last = 0, u64* last = nullptr) {
+    u64 i = i0;
     if (id == 4) {  // x86: E8 (call) / E9 (jmp) rel32, with the prev_mask heuristic
-        if (len < 5) return;
         const bool allowed[8] = {true, true, true, false, true, false, false, false};
         const u32 bitnum[8] = {0, 1, 2, 2, 3, 3, 3, 3};
-        u32 prev_mask = 0, prev_pos = pos0 - 5;
-        for (u64 i = 0; i + 5 <= len;) {
+        u32 prev_mask = st.prev_mask, prev_pos = st.prev_pos;
+        while (i + 5 <= len) {
+            if (last && i < lim_last) *last = i;
             const u32 b0 = buf.get(i);
             if (b0 != 0xE8 && b0 != 0xE9) { i++; continue; }
             const u32 now = pos0 + (u32)i;
@@ -620,10 +644,13 @@ ZX_INL void bcj_serial(B& buf, u64 len, u32 id, u32 pos0) {
                 if (bcj_x86_ms(b4)) prev_mask |= 0x10;
             }
         }
-    } else if (id == 8) {  // ARM-Thumb: BL pairs, 2-byte steps
-        for (u64 i = 0; i + 4 <= len; i += 2) {
+        return BcjState{i, prev_mask, prev_pos};
+    }
+    if (id == 8) {  // ARM-Thumb: BL pairs, 2-byte steps
+        while (i + 4 <= len) {
+            if (last && i < lim_last) *last = i;
             const u32 b1 = buf.get(i + 1), b3 = buf.get(i + 3);
-            if ((b1 & 0xF8) != 0xF0 || (b3 & 0xF8) != 0xF8) continue;
+            if ((b1 & 0xF8) != 0xF0 || (b3 & 0xF8) != 0xF8) { i += 2; continue; }
             u32 src = ((b1 & 7) << 19) | (buf.get(i) << 11) | ((b3 & 7) << 8) | buf.get(i + 2);
             src <<= 1;
             u32 dest = (src - (pos0 + (u32)i + 4)) >> 1;
@@ -631,16 +658,25 @@ ZX_INL void bcj_serial(B& buf, u64 len, u32 id, u32 pos0) {
             buf.set(i, (dest >> 11) & 0xFF);
             buf.set(i + 3, 0xF8 | ((dest >> 8) & 7));
             buf.set(i + 2, dest & 0xFF);
-            i += 2;
+            i += 4;
         }
-    } else if (id == 6) {  // IA-64: 16-byte bundles, each independent
-        for (u64 i = 0; i + 16 <= len; i += 16) bcj_ia64_bundle(buf, i, pos0 + (u32)i);
-    } else {  // 4-byte words, each independent
-        for (u64 i = 0; i + 4 <= len; i += 4) bcj_word(buf, i, id, pos0 + (u32)i);
+        return BcjState{i, 0u, 0u};
     }
+    const u32 w = id == 6 ? 16u : 4u;  // IA-64 bundles / 4-byte words, each independent
+    for (; i + w <= len; i += w) {
+        if (last && i < lim_last) *last = i;
+        if (id == 6) bcj_ia64_bundle(buf, i, pos0 + (u32)i);
+        else bcj_word(buf, i, id, pos0 + (u32)i);
+    }
+    return BcjState{i, 0u, 0u};
+}
+template <class B>
+ZX_INL BcjState bcj_serial(B& buf, u64 len, u32 id, u32 pos0) {
+    return bcj_run(buf, 0, len, id, pos0, BcjState{0, 0u, pos0 - 5});
 }
 // After decoding stopped inside a BCJ block at io.pos: could its last bytes
 // start an instruction whose conversion depends on bytes not decoded?
+// (Kept for chains the tail decode below does not cover.)
 template <class IO>
 ZX_INL bool bcj_tail_open(IO& io, u64 a, u32 id) {
     const u64 len = io.pos - a;
@@ -674,18 +710,114 @@ ZX_INL bool apply_filters(IO& io, const FilterPending& fp, bool partial) {
     return true;
 }
 template <class IO>
-ZX_INL int xz_decode_blocks(IO& io, FilterPending& fp);
+ZX_INL int xz_decode_blocks(IO& io, FilterPending& fp, u64 Ddec, u64 Dfull, bool tail, u64* lzend);
+// Block-relative view of one block's output for the BCJ tail loop: bytes
+// below N from the output, bytes from N on (decoded past the caller's end)
+// from the IO's tail store; writes land only below N.
+template <class IO>
+struct BcjTailBuf {
+    IO* io;
+    u64 a, D;
+    bool write;
+    ZX_INL u32 get(u64 i) { return a + i < D ? io->out_byte(a + i) : io->tail_byte(a + i); }
+    ZX_INL void set(u64 i, u32 v) {
+        if (write && a + i < D) io->set_byte(a + i, v);
+    }
+};
+// A read that stops inside a block whose innermost filter (the one LZMA2
+// feeds) is BCJ and the only BCJ of the chain.  liblzma's simple coder
+// (simple_coder.c) holds back the bytes its loop has not processed and, to
+// release them, decodes past the caller's end into its buffer of
+// 2 x unfiltered_max bytes.  Modelled with two more decodes of the stream:
+//   A: past N with no input window limit (read_exact keeps calling read(),
+//      which refills the window), to find E, the least decoded extent at
+//      which the filter loop passes N (or the LZMA2 data ends): input that
+//      ends, or data that fail, before E give UnexpectedEof / InvalidData;
+//   C: up to U + allocated (U = where the loop stopped at N), with the
+//      window limit from E on (the call that releases byte N - 1 sees only
+//      its window): a data error there is InvalidData, running out is not.
+// The loop then runs over C's extent, and the outer (delta) filters over
+// [start, N).  Chains with a second BCJ, or a delta under the BCJ, keep the
+// open-tail rule (UNSUPPORTED).
 template <class IO>
 ZX_INL int xz_decode(IO& io) {
-    FilterPending fp;
+    const u64 D = io.D;
+    FilterPending fp, keep;
     fp.start = 0;
     fp.n = 0;
-    const int r = xz_decode_blocks(io, fp);
-    if (fp.n && !apply_filters(io, fp, r == ST_OK)) return ST_UNSUPPORTED;
-    return r;
+    keep = fp;
+    // pass 0: the read itself; 1: A; 2: C (one call site, so the stream
+    // decoder is inlined once)
+    u64 Ddec = D, Dfull = D, a = 0, U = 0, E = 0, lzend = ~0ull;
+    u32 id = 0, so = 0, nf = 0;
+    BcjState s0{0, 0u, 0u};
+    int rA = ST_OK;
+    for (u32 pass = 0;; pass++) {
+        if (pass > 0) {
+            io.reset();
+            fp.n = 0;
+        }
+        lzend = ~0ull;
+        const int r = xz_decode_blocks(io, fp, Ddec, Dfull, pass > 0, &lzend);
+        if (pass == 0) {
+            if (!fp.n) return r;
+            nf = fp.n;
+            id = fp.kind[nf - 1];
+            bool one_bcj = id != 3;
+            for (u32 k = 0; k + 1 < nf; k++)
+                if (fp.kind[k] != 3) one_bcj = false;
+            if (r != ST_OK || !one_bcj) {
+                if (!apply_filters(io, fp, r == ST_OK)) return ST_UNSUPPORTED;
+                return r;
+            }
+            a = fp.start;
+            so = fp.param[nf - 1];
+            keep = fp;
+            io.finish();
+            s0 = io.apply_bcj(a, D, id, so);  // [a, a + stop) converted
+            U = a + s0.stop;
+            if (U >= D) break;                // nothing held back
+            Ddec = U + bcj_allocated(id);
+            Dfull = ~0ull;                    // A: no window limit
+            continue;
+        }
+        if (pass == 1) {
+            rA = r;
+            const u64 XA = io.pos;
+            io.finish();
+            BcjTailBuf<IO> tb{&io, a, D, false};
+            u64 lastp = ~0ull;
+            const BcjState sA = bcj_run(tb, s0.stop, XA - a, id, so, s0, D - a, &lastp);
+            if (a + sA.stop >= D) {
+                E = lastp == ~0ull ? D : a + lastp + bcj_window(id);
+                if (E < D) E = D;
+                if (lzend != ~0ull && lzend < E) E = lzend;
+            } else if (lzend != ~0ull) {
+                E = lzend;  // end_was_reached: everything counts as filtered
+            } else {
+                return rA == ST_OK ? ST_INVALID : rA;  // (rA is EOF or InvalidData here)
+            }
+            Dfull = E;  // C: the window limit from E on
+            continue;
+        }
+        if (r != ST_OK) return r;
+        const u64 XC = io.pos;
+        fp = keep;
+        io.finish();
+        s0 = io.apply_bcj(a, D, id, so);
+        BcjTailBuf<IO> tw{&io, a, D, true};
+        bcj_run(tw, s0.stop, XC - a, id, so, s0);  // (at the LZMA2 end the unprocessed rest stays as decoded)
+        io.finish();
+        break;
+    }
+    for (u32 k = nf - 1; k-- > 0;) {  // outer delta stages over [start, N)
+        io.apply_delta(a, D, keep.param[k]);
+        io.finish();
+    }
+    return ST_OK;
 }
 template <class IO>
-ZX_INL int xz_decode_blocks(IO& io, FilterPending& fp) {
+ZX_INL int xz_decode_blocks(IO& io, FilterPending& fp, u64 Ddec, u64 Dfull, bool tail, u64* lzend) {
     const u64 n = io.n;
     const u64 D = io.D;
     u64 ip = 0;       // input position
@@ -840,7 +972,13 @@ ZX_INL int xz_decode_blocks(IO& io, FilterPending& fp) {
             ZX_NEED(1);
             if (ip >= c_end) return ST_INVALID;
             const u32 ctl = io.in(ip++);
-            if (ctl == 0) break;  // end of LZMA2 data
+            if (ctl == 0) {  // end of LZMA2 data
+                if (tail && io.pos >= D) {  // the simple coder's end_was_reached: nothing past it is read
+                    *lzend = io.pos;
+                    return ST_OK;
+                }
+                break;
+            }
             if (ctl >= 0xE0 || ctl == 1) {
                 need_props = true;
                 need_dict_reset = true;
@@ -863,7 +1001,7 @@ ZX_INL int xz_decode_blocks(IO& io, FilterPending& fp) {
             if (need_dict_reset) {
                 need_dict_reset = false;
                 dict_start = io.pos;  // dict_reset(): empty dictionary, prev byte 0
-                if (full) return ST_OK;  // decode_buffer returns after a reset when out is full
+                if (io.pos >= Ddec) return ST_OK;  // decode_buffer returns after a reset when out is full
             }
             if (ctl >= 0x80) {
                 // ---- LZMA chunk header ----
@@ -904,7 +1042,8 @@ ZX_INL int xz_decode_blocks(IO& io, FilterPending& fp) {
                     ZX_U32(rc_code);
                 }
                 LzJob j;
-                j.ip = (u32)ip; j.lim = (u32)lim; j.rlim = (u32)rlim; j.n = (u32)n; j.D = (u32)D;
+                j.ip = (u32)ip; j.lim = (u32)lim; j.rlim = (u32)rlim; j.n = (u32)n; j.D = (u32)Ddec;
+                j.Dfull = Dfull > 0xFFFFFFFFull ? 0xFFFFFFFFu : (u32)Dfull;
                 j.chunk_end = (u32)(io.pos + usz); j.dict_start = (u32)dict_start;
                 j.dsz = dsz > 0xFFFFFFFFull ? 0xFFFFFFFFu : (u32)dsz;
                 j.u_end = u_end > 0xFFFFFFFFull ? 0xFFFFFFFFu : (u32)u_end;
@@ -923,17 +1062,18 @@ ZX_INL int xz_decode_blocks(IO& io, FilterPending& fp) {
                 u32 left = ((io.in(ip) << 8) | io.in(ip + 1)) + 1;
                 ip += 2;
                 while (left > 0) {
-                    if (io.pos == D) return ST_OK;  // dict full: dict_write copies nothing
+                    if (io.pos == Ddec) return ST_OK;  // dict full: dict_write copies nothing
                     ZX_NEED(1);
                     u64 k = left;
                     if (k > lim - ip) k = lim - ip;
-                    if (k > D - io.pos) k = D - io.pos;
+                    if (k > Ddec - io.pos) k = Ddec - io.pos;
+                    if (!full && io.pos < Dfull && k > Dfull - io.pos) k = Dfull - io.pos;
                     if (ip + k > c_end) return ST_INVALID;
                     io.copy_in(ip, (u32)k);
                     ip += k;
                     left -= (u32)k;
                     if (io.pos > u_end) return ST_INVALID;
-                    if (io.pos == D && !full) ZX_SET_FULL();
+                    if (io.pos == Dfull && !full) ZX_SET_FULL();
                 }
             }
         }
