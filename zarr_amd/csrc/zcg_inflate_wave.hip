@@ -58,6 +58,9 @@
 #ifndef ZIW_DBG
 #define ZIW_DBG 1  // 0: the debug-counter code is compiled out (the flag is ignored)
 #endif
+#ifndef ZIW_NEARX
+#define ZIW_NEARX 1  // near batches: tagged markers (no clear) and a first read that settles final sources
+#endif
 
 namespace zcg {
 
@@ -140,7 +143,7 @@ struct IwLds {
             u32 bcache[BI_CACHE_WORDS];
             u32 hwin[130];  // 512 stream bytes from the code-length codes on (dynamic header)
         } h;
-        struct {       // H round: marked extent (bits) of each segment, staged tokens, mark windows
+        struct Hr {    // H round: marked extent (bits) of each segment, staged tokens, mark windows
             u32 mlim[65];
             u32 tst[2 * IW_K][64];  // ring of two aligned list blocks (slot = token index % 8)
             u32 mwin[IW_MWIN][64];
@@ -151,12 +154,16 @@ struct IwLds {
                 u32 desc[128];  // near token 2l + slot of the group: (offset - first near index) | dist << 16
                 u64 fd[64];     // far tokens of the group by rank: source of the first quad | (quad, r, L) << 32
             };
-            u8 mk[64];      // near batch: token id + 1 at the lane of its first byte in the batch
+            // near batch: batch tag << 8 | token id + 1 at the lane of the
+            // token's first byte in the batch (other slots hold older tags);
+            // past every other member of the union, so it is zeroed once per chunk
+            u32 mk[64];
         } st;
     } u;
     u32 dbgc[IW_NDBG];
 };
 static_assert(sizeof(IwLds) + 32 <= 10240, "16 chunks per CU");
+static_assert(2 * IW_S + 512 >= sizeof(decltype(IwLds::u)::Hr), "batch markers lie past the H-round scratch");
 
 // wave-local ordering point for LDS (and the compiler): a wave's LDS
 // operations are performed in issue order, so a fence at wavefront scope is
@@ -578,6 +585,8 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
     bool last = false, boundary = false, after_stored = false;
     int r = R_OK;
     u32 est = IW_EST0;
+    L.u.st.mk[lane] = 0;  // batch tags start at 1
+    u32 ntag = 0;
     if (dbg) {
         if (lane < IW_NDBG) L.dbgc[lane] = 0;
         wsync();
@@ -1000,12 +1009,21 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
                     // byte n0 + i; its token is the last one whose first byte in
                     // the batch is at or before it (marker + max scan)
                     for (u32 n0 = 0; n0 < NB; n0 += 64) {
+#if ZIW_NEARX
+                        const u32 tag = ++ntag << 8;
+                        if (nla && na < n0 + 64 && na + nla > n0) L.u.st.mk[na > n0 ? na - n0 : 0u] = tag | (ia + 1);
+                        if (nlb && nb < n0 + 64 && nb + nlb > n0) L.u.st.mk[nb > n0 ? nb - n0 : 0u] = tag | (ib + 1);
+                        wsync();
+                        const u32 mv = L.u.st.mk[lane];
+                        const int tid = iw_incl_max((mv & ~0xFFu) == tag ? (int)(mv & 0xFFu) : 0) - 1;
+#else
                         L.u.st.mk[lane] = 0;
                         wsync();
                         if (nla && na < n0 + 64 && na + nla > n0) L.u.st.mk[na > n0 ? na - n0 : 0u] = (u8)(ia + 1);
                         if (nlb && nb < n0 + 64 && nb + nlb > n0) L.u.st.mk[nb > n0 ? nb - n0 : 0u] = (u8)(ib + 1);
                         wsync();
                         const int tid = iw_incl_max((int)L.u.st.mk[lane]) - 1;
+#endif
                         const u32 i = n0 + lane;
                         bool done = i >= NB, strad = false;
                         u32 pos = 0, cur = 0;
@@ -1017,8 +1035,19 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
                             if (p >= d) cur = (S32 + p - d) & (IW_S - 1);
                             else cur = IE_VAL | (u32)gd[swap_pos32(S32 + p - d, tw)];  // before the stage
                             strad = p < d;
+#if ZIW_NEARX
+                            // a source that is already final settles the byte now: the
+                            // read precedes this batch's writes, and an entry of this
+                            // batch still reads as a pointer (zero or older), so only
+                            // final values are taken
+                            const u32 v0 = cur >= IE_VAL ? cur : (u32)L.u.st.ptr[cur];
+                            done = v0 >= IE_VAL;
+                            if (done) cur = v0;
+                            L.u.st.ptr[pos] = (u16)cur;
+#else
                             L.u.st.ptr[pos] = (u16)cur;
                             done = cur >= IE_VAL;
+#endif
                         }
                         wsync();
                         IW_ADD(IWD_NBATCH, 1);
