@@ -36,9 +36,43 @@ struct BitOut {
 };
 }  // namespace
 
+// zlib's head[] / prev[] (window-relative Pos, 0 = NIL) for zz::parse_fast
+struct FastTab {
+    std::vector<uint16_t> hd, pv;
+    FastTab() : hd(1u << 15, 0), pv(zz::WSIZE, 0) {}
+    uint32_t head(uint32_t h) const { return hd[h]; }
+    void set_head(uint32_t h, uint32_t v) { hd[h] = (uint16_t)v; }
+    uint32_t prev(uint32_t i) const { return pv[i]; }
+    void set_prev(uint32_t i, uint32_t v) { pv[i] = (uint16_t)v; }
+    void slide() {  // slide_hash
+        for (auto& x : hd) x = x >= zz::WSIZE ? (uint16_t)(x - zz::WSIZE) : 0;
+        for (auto& x : pv) x = x >= zz::WSIZE ? (uint16_t)(x - zz::WSIZE) : 0;
+    }
+};
+
+static int64_t emit_blocks(const uint8_t* src, const std::vector<uint32_t>& syms,
+                           const std::vector<zz::BlockRec>& blocks, uint8_t* out, uint64_t cap);
+
 extern "C" int64_t zz_host_deflate(const uint8_t* src, uint32_t D, int level, uint8_t* out, uint64_t cap) {
     using namespace zz;
     const Config cfg = level_config(level);
+    if (level >= 1 && level <= 3) {  // deflate_fast: the parse builds its chains
+        auto byte = [&](uint32_t i) -> uint32_t { return src[i]; };
+        auto byte4 = [&](uint32_t i) -> uint32_t {
+            uint32_t v;
+            memcpy(&v, src + i, 4);
+            return v;
+        };
+        FastTab tab;
+        std::vector<uint32_t> syms, pos;
+        auto emit = [&](uint32_t s, uint32_t at) { syms.push_back(s); pos.push_back(at); };
+        const uint32_t nsym = parse_fast(D, cfg, tab, byte4, byte, emit);
+        std::vector<BlockRec> blocks;
+        auto P = [&](uint32_t i) -> uint32_t { return pos[i]; };
+        auto Y = [&](uint32_t i) -> uint32_t { return syms[i]; };
+        for (uint32_t k = 0; k < num_blocks(nsym); k++) blocks.push_back(block_rec(k, nsym, nsym, D, P, Y, true));
+        return emit_blocks(src, syms, blocks, out, cap);
+    }
     std::vector<uint32_t> prev(D ? D : 1, NONE), head(1u << 15, NONE);
     for (uint32_t p = 0; p + MIN_MATCH <= D; p++) {
         const uint32_t h = hash3(src[p], src[p + 1], src[p + 2]);
@@ -60,6 +94,12 @@ extern "C" int64_t zz_host_deflate(const uint8_t* src, uint32_t D, int level, ui
     auto emit = [&](uint32_t, uint32_t s) { syms.push_back(s); };
     auto flush = [&](const BlockRec& b) { blocks.push_back(b); };
     parse(D, cfg, get, byte, emit, flush);
+    return emit_blocks(src, syms, blocks, out, cap);
+}
+
+static int64_t emit_blocks(const uint8_t* src, const std::vector<uint32_t>& syms,
+                           const std::vector<zz::BlockRec>& blocks, uint8_t* out, uint64_t cap) {
+    using namespace zz;
     BitOut bo{out, cap};
     BlockWork* bw = new BlockWork;
     for (const BlockRec& b : blocks) {

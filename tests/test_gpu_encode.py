@@ -210,8 +210,8 @@ def check_gzip_member(stream: bytes, content: bytes, level: int, exact=None):
     assert crc == zlib.crc32(content) and isize == len(content) & 0xFFFFFFFF
     d = zlib.decompressobj(-15)
     assert d.decompress(stream[10:-8]) == content and d.eof and not d.unused_data
-    if exact if exact is not None else eff >= 4:
-        # levels 4-9: byte-identical to zlib (gzip.rs:54-56 -> flate2 -> zlib deflate_slow)
+    if exact if exact is not None else eff >= 1:
+        # levels 1-9: byte-identical to zlib (gzip.rs:54-56 -> flate2 -> zlib deflate_fast / deflate_slow)
         ref = zlib_raw(content, eff)
         body = stream[10:-8]
         if body != ref:
@@ -292,9 +292,9 @@ def test_gzip_encode_quant_ratio():
     assert ours <= 1.4 * ref, (ours, ref)
 
 
-@pytest.mark.parametrize("level", [4, 5, 6, 7, 8, 9])
+@pytest.mark.parametrize("level", [1, 2, 3, 4, 5, 6, 7, 8, 9])
 def test_gzip_encode_matches_zlib_levels(level):
-    """write_chunk bytes = flate2/zlib's at every deflate_slow level, on a mixed
+    """write_chunk bytes = flate2/zlib's at every level (1-3 deflate_fast, 4-9 deflate_slow), on a mixed
     batch: the five DATASETS kinds, the C5 'quant' f32 chunk, and sizes that
     end blocks / windows at their edges."""
     import sys
@@ -310,15 +310,17 @@ def test_gzip_encode_matches_zlib_levels(level):
         check_gzip_member(s, a.tobytes(), level, exact=True)
 
 
+@pytest.mark.parametrize("level", [1, 6])
 @pytest.mark.parametrize("nbytes", [1, 2, 3, 258, 259, 16383, 32506, 32768, 65274, 65275, 65536, 98304 + 7])
-def test_gzip_encode_matches_zlib_edges(nbytes):
-    """Window-slide and block-flush edges: zlib's bytes exactly (level 6)."""
+def test_gzip_encode_matches_zlib_edges(nbytes, level):
+    """Window-slide and block-flush edges: zlib's bytes exactly (deflate_fast
+    at level 1, deflate_slow at level 6)."""
     arrays = [_data("text", nbytes, 4), _data("uniform", nbytes, 5), _data("zeros", nbytes), _data("ramp", nbytes)]
-    meta = ArrayMetadata.new([nbytes * 4], [nbytes], "u1", Gzip(6))
+    meta = ArrayMetadata.new([nbytes * 4], [nbytes], "u1", Gzip(level))
     st, outs = encode_batch(meta, arrays)
     assert (st == 0).all()
     for a, s in zip(arrays, outs):
-        check_gzip_member(s, a.tobytes(), 6, exact=True)
+        check_gzip_member(s, a.tobytes(), level, exact=True)
 
 
 # ---- Xz (xz.rs:34-43: xz2 XzEncoder = lzma_easy_encoder(preset, CRC64)) ----

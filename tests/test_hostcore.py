@@ -447,12 +447,13 @@ def zlib_raw(b: bytes, level: int) -> bytes:
     return c.compress(b) + c.flush()
 
 
-@pytest.mark.parametrize("level", [4, 5, 6, 7, 8, 9])
+@pytest.mark.parametrize("level", [1, 2, 3, 4, 5, 6, 7, 8, 9])
 def test_zlib_core_matches_zlib(level):
-    """The GPU gzip encoder's core (match search per position, lazy parse,
-    trees) driven serially: byte-identical to the system zlib 1.2.11 (the
-    library flate2 wraps, gzip.rs:54-56) on mixed inputs, incl. window-slide
-    and block-flush edges."""
+    """The GPU gzip encoder's core driven serially: deflate_fast (levels 1-3:
+    the greedy parse building its chains as it goes) and deflate_slow (4-9:
+    match search per position, lazy parse), then trees: byte-identical to the
+    system zlib 1.2.11 (the library flate2 wraps, gzip.rs:54-56) on mixed
+    inputs, incl. window-slide and block-flush edges."""
     rng = np.random.default_rng(level)
     cases = [b"", b"a", b"abcabcabcabc", bytes(70000), rng.integers(0, 256, 20000, dtype=np.uint8).tobytes(),
              rng.integers(0, 4, 100000, dtype=np.uint8).tobytes(),
@@ -464,12 +465,13 @@ def test_zlib_core_matches_zlib(level):
 
 
 def test_zlib_core_matches_zlib_quant():
-    """C5's 'quant' f32 chunk (1 MiB) at level 6: zlib's bytes."""
+    """C5's 'quant' f32 chunk (1 MiB) at levels 1 and 6: zlib's bytes."""
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     from bench import quant_chunk
     b = quant_chunk(2).tobytes()
-    assert host_deflate(b, 6) == zlib_raw(b, 6)
+    for level in (1, 6):
+        assert host_deflate(b, level) == zlib_raw(b, level)
 
 
 def test_xz_sha256_core_matches_liblzma():

@@ -1080,6 +1080,181 @@ __global__ __launch_bounds__(64) void dz_parse(const zcg_chunk* __restrict__ chu
     }
 }
 
+// deflate_fast (levels 1-3): zlib's greedy parse builds its hash chains as
+// it goes (positions inside a match longer than max_insert_length are never
+// inserted), so the parse is serial per chunk: one wave per chunk runs
+// zz::parse_fast's rules with zlib's head[] / prev[] as window-relative u16
+// Pos in LDS (64 KiB each, slid like slide_hash), the next 512 input bytes
+// in two registers per lane, and each chain candidate's match length from
+// one 4-byte compare per lane (a ballot finds the first difference).
+// Symbols leave 64 at a time in the same final-stream layout as dz_parse;
+// block records come from zz::block_rec(..., fast = true), so the plan /
+// emit kernels are shared.  tests/hostcore/zlib_ref.cpp (zz::parse_fast on
+// the CPU) and the GPU output are compared with zlib byte for byte.
+constexpr u32 DZF_LDS = 2 * 32768 * 2;  // head[] + prev[], u16 each
+__device__ __forceinline__ u32 dzf_ld4(const u8* src, u32 x, u32 D, const DType& t) {  // bytes past D read 0
+    if (x + 4 <= D) return df_ser4(src, x, t);
+    u32 v = 0;
+    for (u32 k = 0; k < 4; k++)
+        if (x + k < D) v |= df_ser1(src, x + k, t) << (8 * k);
+    return v;
+}
+__global__ __launch_bounds__(64) void dz_parse_fast(const zcg_chunk* __restrict__ chunks, u32 c0, u32 nc, u64 D,
+                                                   DType t, zz::Config cfg, u32* __restrict__ wbase, u64 off_m2,
+                                                   DzChunk* __restrict__ cst, DzBlock* __restrict__ blks, u32 nbmax) {
+    extern __shared__ __attribute__((aligned(16))) u8 smem_raw[];
+    u16* hd = (u16*)smem_raw;
+    u16* pv = hd + 32768;
+    const u32 c = blockIdx.x;
+    if (c >= nc) return;
+    const u32 lane = threadIdx.x;
+    const zcg_chunk ch = chunks[c0 + c];
+    DzChunk* cs = cst + c;
+    if (ch.src_len < D) {
+        if (lane == 0) { cs->nblocks = 0; cs->status = ZCG_ERR_INVALID_DATA; }
+        return;
+    }
+    const u8* src = (const u8*)ch.src;
+    const u32 D32 = (u32)D;
+    u32* fsy = wbase + off_m2 + (u64)c * 2 * D;  // final stream: symbols, then positions
+    u32* fps = fsy + D;
+    for (u32 i = lane; i < 32768; i += 64) ((u32*)smem_raw)[i] = 0u;  // both tables NIL
+    __syncthreads();
+    auto rd = [&](const u16* a, u32 i) -> u32 { return (u32)__builtin_amdgcn_readfirstlane((u32)a[i]); };
+    // input window: lane l holds bytes [wb + 4 l, +4) (w0) and [wb + 256 + 4 l, +4) (w1)
+    u32 wb = 0;
+    u32 w0 = dzf_ld4(src, 4 * lane, D32, t), w1 = dzf_ld4(src, 256 + 4 * lane, D32, t);
+    auto wbyte = [&](u32 q) -> u32 {  // q in [wb, wb + 512)
+        const u32 o = q - wb, wi = o >> 2;
+        const u32 v = (u32)__builtin_amdgcn_readlane((int)(wi < 64 ? w0 : w1), (int)(wi & 63));
+        return (v >> (8 * (o & 3))) & 0xFFu;
+    };
+    u32 base = 0, nsym = 0, rs = 0, rp = 0;
+    auto emit = [&](u32 sym, u32 at) {
+        const u32 k = nsym & 63;
+        if (lane == k) { rs = sym; rp = at; }
+        nsym++;
+        if (k == 63) {
+            fsy[nsym - 64 + lane] = rs;
+            fps[nsym - 64 + lane] = rp;
+        }
+    };
+    auto insert = [&](u32 q) -> u32 {  // INSERT_STRING: the previous head (relative, 0 = NIL)
+        const u32 h = zz::hash3(wbyte(q), wbyte(q + 1), wbyte(q + 2));
+        const u32 hh = rd(hd, h);
+        if (lane == 0) {
+            pv[(q - base) & zz::WMASK] = (u16)hh;
+            hd[h] = (u16)(q - base);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        return hh;
+    };
+    u32 p = 0;
+    while (p < D32) {
+        if (p - wb >= 252) {  // keep [p, p + 260) in the window (wb <= p always)
+            wb = p & ~3u;
+            w0 = dzf_ld4(src, wb + 4 * lane, D32, t);
+            w1 = dzf_ld4(src, wb + 256 + 4 * lane, D32, t);
+        }
+        {  // fill_window at the loop top: one slide when due
+            const u32 wend = (D32 - base) > 2 * zz::WSIZE ? base + 2 * zz::WSIZE : D32;
+            if (wend - p < zz::MIN_LOOKAHEAD && p - base >= zz::WSIZE + zz::MAX_DIST) {
+                for (u32 i = lane; i < 32768; i += 64) {
+                    const u32 x = ((u32*)smem_raw)[i];
+                    const u32 lo = x & 0xFFFFu, hi = x >> 16;
+                    ((u32*)smem_raw)[i] = (lo >= zz::WSIZE ? lo - zz::WSIZE : 0u) |
+                                          ((hi >= zz::WSIZE ? hi - zz::WSIZE : 0u) << 16);
+                }
+                __syncthreads();
+                base += zz::WSIZE;
+            }
+        }
+        u32 ml = 0, md = 0;
+        if (D32 - p >= zz::MIN_MATCH) {
+            const u32 hh = insert(p);
+            if (hh != 0 && (p - base) - hh <= zz::MAX_DIST) {
+                // longest_match (zz::search's rules) over the chain from hh
+                const u32 look = D32 - p;
+                const u32 mx = look < zz::MAX_MATCH ? look : zz::MAX_MATCH;
+                const u32 nice = cfg.nice < look ? cfg.nice : look;
+                const u32 lim = p > zz::MAX_DIST ? p - zz::MAX_DIST : 0u;
+                // my 4 bytes of p.. (lane l: p + 4 l ..) from the window
+                const u32 o = p - wb + 4 * lane, wi = o >> 2, sh = 8 * (o & 3);
+                const u32 a0 = __shfl(w0, (int)(wi & 63)), a1 = __shfl(w1, (int)(wi & 63));
+                const u32 b0 = __shfl(w0, (int)((wi + 1) & 63)), b1 = __shfl(w1, (int)((wi + 1) & 63));
+                const u32 lo = wi < 64 ? a0 : a1, hi = (wi + 1) < 64 ? b0 : b1;
+                const u32 pw = sh ? ((lo >> sh) | (hi << (32 - sh))) : lo;
+                u32 best = 0, bstart = 0, cand = hh + base;
+                for (u32 k = 0; k < cfg.chain; k++) {
+                    if (k > 0) {
+                        const u32 r = rd(pv, (cand - base) & zz::WMASK);
+                        if (r == 0) break;
+                        cand = r + base;
+                        if (cand <= lim) break;
+                    }
+                    const u32 cw = 4 * lane < mx ? dzf_ld4(src, cand + 4 * lane, D32, t) : pw;
+                    const u64 m = __ballot(pw != cw);
+                    u32 len;
+                    if (m) {
+                        const u32 j = (u32)__builtin_ctzll(m);
+                        const u32 x = (u32)__builtin_amdgcn_readlane((int)(pw ^ cw), (int)j);
+                        len = 4 * j + ((u32)__builtin_ctz(x) >> 3);
+                    } else {
+                        len = 256;
+                        while (len < mx && wbyte(p + len) == (u32)__builtin_amdgcn_readfirstlane(df_ser1(src, cand + len, t)))
+                            len++;
+                    }
+                    if (len > mx) len = mx;
+                    if (len > best) {
+                        best = len;
+                        bstart = cand;
+                        if (best >= nice) break;
+                    }
+                }
+                if (best >= zz::MIN_MATCH) {
+                    ml = best;
+                    md = p - bstart;
+                }
+            }
+        }
+        if (ml) {
+            emit(0x80000000u | ((ml - zz::MIN_MATCH) << 16) | (md - 1), p);
+            if (ml <= cfg.lazy && D32 - (p + ml) >= zz::MIN_MATCH)
+                for (u32 q = p + 1; q < p + ml; q++) insert(q);
+            p += ml;
+        } else {
+            emit(wbyte(p), p);
+            p++;
+        }
+    }
+    if (nsym & 63) {
+        const u32 b0 = nsym & ~63u;
+        if (lane < (nsym & 63)) {
+            fsy[b0 + lane] = rs;
+            fps[b0 + lane] = rp;
+        }
+    }
+    __syncthreads();  // the final stream is in place
+    const u32 nb = zz::num_blocks(nsym);
+    auto P = [&](u32 i) -> u32 { return fps[i]; };
+    auto Y = [&](u32 i) -> u32 { return fsy[i]; };
+    for (u32 k = lane; k < nb && k < nbmax; k += 64) {
+        const zz::BlockRec r = zz::block_rec(k, nsym, nsym, D32, P, Y, true);
+        DzBlock* o = blks + (u64)c * nbmax + k;
+        o->s0 = r.s0; o->s1 = r.s1; o->b0 = r.b0; o->b1 = r.b1; o->in_win = r.in_win; o->last = r.last;
+    }
+    if (lane == 0) {
+        cs->fsym = (u64)(fsy - wbase);
+        cs->fpos = (u64)(fps - wbase);
+        cs->nsym = nsym;
+        cs->nloop = nsym;
+        cs->nblocks = nb <= nbmax ? nb : 0u;
+        cs->status = nb <= nbmax ? ZCG_OK : ZCG_ERR_INVALID_DATA;
+    }
+}
+
 struct DzPlanLds {
     zz::BlockWork bw;
     u32 lf[zz::L_CODES], df[zz::D_CODES];
@@ -1381,9 +1556,13 @@ static hipError_t launch_deflate_exact(const zcg_array* a, const zcg_chunk* d_ch
     DzChunk* cst = (DzChunk*)(w + y.off_ch);
     DzBlock* blks = (DzBlock*)(w + y.off_blk);
     u8* out = w + y.off_out;
+    const bool fast = level <= 3;
+    if (fast) {
+        if (hipError_t e = lds_attr_once((const void*)dz_parse_fast, (int)DZF_LDS); e != hipSuccess) return e;
+    }
     for (u32 s0 = 0; s0 < n; s0 += y.sb) {
         const u32 scnt = (n - s0) < y.sb ? (n - s0) : y.sb;
-        for (u32 c0 = s0; c0 < s0 + scnt && D > 0; c0 += y.m) {
+        for (u32 c0 = s0; c0 < s0 + scnt && D > 0 && !fast; c0 += y.m) {
             const u32 cnt = (s0 + scnt - c0) < y.m ? (s0 + scnt - c0) : y.m;
             const u64 tot = (u64)cnt * D;
             u32 *ka = (u32*)(w + y.off_ka), *kb = (u32*)(w + y.off_kb);
@@ -1402,9 +1581,17 @@ static hipError_t launch_deflate_exact(const zcg_array* a, const zcg_chunk* d_ch
             hipLaunchKernelGGL(dz_best, dim3(G), dim3(256), 0, s, d_chunks, c0, D, tot, t, cfg,
                                (const u32*)(w + y.off_prev), m2 + (u64)(c0 - s0) * D);
         }
-        hipLaunchKernelGGL(dz_parse, dim3(scnt), dim3(64), 0, s, d_chunks, s0, scnt, D, t, cfg, (u32*)w,
-                           y.off_m2 / 4, y.off_sym / 4, y.off_pos / 4, y.off_bm / 4, y.off_tail / 4, cst, blks,
-                           y.nbmax);
+        // a parse that does not run leaves every chunk failed, so the kernels
+        // after it never read an unset record
+        if (hipError_t e = hipMemsetAsync(cst, 0xFF, sizeof(DzChunk) * (size_t)scnt, s); e != hipSuccess) return e;
+        if (fast) {
+            hipLaunchKernelGGL(dz_parse_fast, dim3(scnt), dim3(64), DZF_LDS, s, d_chunks, s0, scnt, D, t, cfg, (u32*)w,
+                               y.off_m2 / 4, cst, blks, y.nbmax);
+            if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
+        } else
+            hipLaunchKernelGGL(dz_parse, dim3(scnt), dim3(64), 0, s, d_chunks, s0, scnt, D, t, cfg, (u32*)w,
+                               y.off_m2 / 4, y.off_sym / 4, y.off_pos / 4, y.off_bm / 4, y.off_tail / 4, cst, blks,
+                               y.nbmax);
         const u64 nbk = (u64)scnt * y.nbmax;
         hipLaunchKernelGGL(dz_plan, dim3((u32)nbk), dim3(64), 0, s, scnt, cst, blks, y.nbmax, (const u32*)w, D);
         hipLaunchKernelGGL(dz_offsets, dim3((scnt + 63) / 64), dim3(64), 0, s, scnt, cst, blks, y.nbmax, out,
@@ -1422,9 +1609,11 @@ static hipError_t launch_deflate_exact(const zcg_array* a, const zcg_chunk* d_ch
     return hipGetLastError();
 }
 
+// levels 1-9 reproduce zlib's bytes (1-3 deflate_fast, 4-9 deflate_slow);
+// level 0 (stored) and ZCG_FLAG_GZIP_SEGMENTED take the segmented coder
 static bool deflate_exact_level(const zcg_array* a) {
     const int level = zcg_effective_gzip_level(a->compression.gzip_level);
-    return level >= 4 && (a->compression.flags & ZCG_FLAG_GZIP_SEGMENTED) == 0;
+    return level >= 1 && (a->compression.flags & ZCG_FLAG_GZIP_SEGMENTED) == 0;
 }
 
 uint64_t deflate_ws_bytes(const zcg_array* a, uint32_t n) {

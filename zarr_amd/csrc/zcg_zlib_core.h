@@ -70,9 +70,13 @@ constexpr int REP_3_6 = 16, REPZ_3_10 = 17, REPZ_11_138 = 18;
 struct Config {
     uint32_t good, lazy, nice, chain;
 };
-// zlib's configuration_table, deflate_slow rows
+// zlib's configuration_table: levels 1-3 run deflate_fast (`lazy` is then
+// max_insert_length), 4-9 deflate_slow
 ZZ_INL Config level_config(int level) {
     switch (level) {
+        case 1: return {4, 4, 8, 4};
+        case 2: return {4, 5, 16, 8};
+        case 3: return {4, 6, 32, 32};
         case 4: return {4, 4, 16, 16};
         case 5: return {8, 16, 32, 32};
         case 7: return {8, 32, 128, 256};
@@ -83,6 +87,16 @@ ZZ_INL Config level_config(int level) {
 }
 
 ZZ_INL uint32_t hash3(uint32_t b0, uint32_t b1, uint32_t b2) { return ((b0 << 10) ^ (b1 << 5) ^ b2) & 0x7FFFu; }
+
+// Window slides fill_window has done by the loop top at q (input fully
+// available, as flate2 feeds it: 1 KiB-multiple writes fill the 64 KiB window
+// the same way): slide k happens at the first loop top q with
+// q - 32768 (k - 1) >= 65274, plus one more position while q <= D - 262
+// (before the end, fill_window runs only once lookahead < 262).
+ZZ_INL uint32_t slides_at(uint32_t q, uint32_t D) {
+    const uint32_t thr = WSIZE + MAX_DIST + ((uint64_t)q + MIN_LOOKAHEAD <= D ? 1u : 0u);
+    return q >= thr ? (q - thr) / WSIZE + 1 : 0u;
+}
 
 // longest_match at p for both chain budgets.  Result word: len | dist << 9
 // (len 0 = no search; dist = p - the first candidate reaching len).  `full` walks cfg.chain candidates, `red` the first cfg.chain >> 2.
@@ -96,8 +110,10 @@ ZZ_FN Match2 search(uint32_t p, uint32_t D, const Config& cfg, const BYTE4& byte
     Match2 r{0u, 0u};
     if (p + MIN_MATCH > D) return r;
     uint32_t c = prev(p);
-    // deflate_slow: hash_head != NIL && strstart - hash_head <= MAX_DIST
-    if (c == NONE || c == 0 || p - c > MAX_DIST) return r;
+    // hash_head != NIL && strstart - hash_head <= MAX_DIST; hash_head is
+    // window-relative, so the position at the window's base (absolute 0, or
+    // k * 32768 after k slides) reads as NIL
+    if (c == NONE || c == slides_at(p, D) * WSIZE || p - c > MAX_DIST) return r;
     const uint32_t look = D - p;
     const uint32_t mx = look < MAX_MATCH ? look : MAX_MATCH;
     const uint32_t nice = cfg.nice < look ? cfg.nice : look;
@@ -264,15 +280,6 @@ ZZ_FN void step(PState& s, uint32_t D, const Config& cfg, const GET& get, const 
 
 ZZ_INL uint32_t sym_len(uint32_t sym) { return (sym & 0x80000000u) ? ((sym >> 16) & 0xFF) + MIN_MATCH : 1u; }
 
-// Window slides fill_window has done by the loop top at q (input fully
-// available, as flate2 feeds it: 1 KiB-multiple writes fill the 64 KiB window
-// the same way): slide k happens at the first loop top q with
-// q - 32768 (k - 1) >= 65274, plus one more position while q <= D - 262
-// (before the end, fill_window runs only once lookahead < 262).
-ZZ_INL uint32_t slides_at(uint32_t q, uint32_t D) {
-    const uint32_t thr = WSIZE + MAX_DIST + ((uint64_t)q + MIN_LOOKAHEAD <= D ? 1u : 0u);
-    return q >= thr ? (q - thr) / WSIZE + 1 : 0u;
-}
 
 // Block k of a chunk whose parse emitted nsym symbols, nloop of them inside
 // deflate_slow's loop (the last may be the pending literal tallied at
@@ -280,8 +287,12 @@ ZZ_INL uint32_t slides_at(uint32_t q, uint32_t D) {
 // symbol is tallied; the final block takes the rest (possibly none).
 // pos(i) / sym(i): start position and word of symbol i.
 ZZ_INL uint32_t num_blocks(uint32_t nloop) { return nloop / BLOCK_SYMS + 1; }
+// (deflate_fast, `fast`: every symbol is tallied in the loop iteration that
+// starts at it, so a block's flush comes at the top at its last symbol's
+// start; deflate_slow tallies a symbol one iteration later)
 template <class POS, class SYM>
-ZZ_FN BlockRec block_rec(uint32_t k, uint32_t nsym, uint32_t nloop, uint32_t D, const POS& pos, const SYM& sym) {
+ZZ_FN BlockRec block_rec(uint32_t k, uint32_t nsym, uint32_t nloop, uint32_t D, const POS& pos, const SYM& sym,
+                         bool fast = false) {
     const uint32_t nfl = nloop / BLOCK_SYMS;  // in-loop flushes
     BlockRec b{};
     b.s0 = k * BLOCK_SYMS;
@@ -295,10 +306,72 @@ ZZ_FN BlockRec block_rec(uint32_t k, uint32_t nsym, uint32_t nloop, uint32_t D, 
     } else {
         const uint32_t l = b.s1 - 1;
         b.b1 = pos(l) + sym_len(sym(l));
-        top = pos(l) + 1;
+        top = fast ? pos(l) : pos(l) + 1;
     }
     b.in_win = b.b0 >= slides_at(top, D) * WSIZE ? 1u : 0u;
     return b;
+}
+
+// ---- deflate_fast (levels 1-3) ------------------------------------------------
+// Greedy parse with the hash chains built as it goes: a position is inserted
+// when it is a loop top, or inside a match no longer than max_insert_length
+// (cfg.lazy), so unlike deflate_slow the chains depend on the parse and the
+// parse runs serially.  TAB holds zlib's head[] and prev[] as window-relative
+// Pos values (0 = NIL), slid like slide_hash:
+//   u32 head(u32 h); void set_head(u32 h, u32 v); u32 prev(u32 i);
+//   void set_prev(u32 i, u32 v); void slide();   (i = position & WMASK)
+// emit(sym, start position) per symbol; returns the symbol count.  Every
+// symbol is an in-loop tally (nloop = nsym; block_rec(..., fast = true)).
+constexpr uint32_t WMASK = WSIZE - 1;
+template <class TAB, class BYTE4, class BYTE, class EMIT>
+ZZ_FN uint32_t parse_fast(uint32_t D, const Config& cfg, TAB& tab, const BYTE4& byte4, const BYTE& byte, EMIT& emit) {
+    uint32_t p = 0, nsym = 0, base = 0;  // base: absolute position of window-relative 0
+    auto insert = [&](uint32_t q) -> uint32_t {  // INSERT_STRING: the previous head (relative, 0 = NIL)
+        const uint32_t h = hash3(byte(q), byte(q + 1), byte(q + 2));
+        const uint32_t hh = tab.head(h);
+        tab.set_prev((q - base) & WMASK, hh);
+        tab.set_head(h, q - base);
+        return hh;
+    };
+    while (p < D) {
+        {  // fill_window at the loop top: one slide when due
+            const uint32_t wend = (D - base) > 2 * WSIZE ? base + 2 * WSIZE : D;
+            if (wend - p < MIN_LOOKAHEAD && p - base >= WSIZE + MAX_DIST) {
+                tab.slide();
+                base += WSIZE;
+            }
+        }
+        uint32_t ml = 0, md = 0;
+        if (D - p >= MIN_MATCH) {
+            const uint32_t hh = insert(p);
+            if (hh != 0 && (p - base) - hh <= MAX_DIST) {
+                const uint32_t first = hh + base;
+                auto pv = [&](uint32_t x) -> uint32_t {
+                    if (x == p) return first;
+                    const uint32_t r = tab.prev((x - base) & WMASK);
+                    return r == 0 ? NONE : r + base;
+                };
+                const Match2 g = search(p, D, cfg, byte4, byte, pv);
+                const uint32_t len = g.full & 511u;
+                if (len >= MIN_MATCH) {
+                    ml = len;
+                    md = g.full >> 9;
+                }
+            }
+        }
+        if (ml) {
+            emit(0x80000000u | ((ml - MIN_MATCH) << 16) | (md - 1), p);
+            nsym++;
+            if (ml <= cfg.lazy && D - (p + ml) >= MIN_MATCH)
+                for (uint32_t q = p + 1; q < p + ml; q++) insert(q);
+            p += ml;
+        } else {
+            emit(byte(p), p);
+            nsym++;
+            p++;
+        }
+    }
+    return nsym;
 }
 
 // ---- trees (trees.c) ---------------------------------------------------------
