@@ -97,11 +97,11 @@ enum zcg_status {
  * kernel (coarse segments, 16 chunks per CU).  These flags force one. */
 #define ZCG_FLAG_INFLATE_BLOCK_PAR 0x2000u
 #define ZCG_FLAG_INFLATE_WAVE 0x4000u
-/* Gzip encode at levels 4-9 is byte-identical to zlib 1.2.11 / flate2
- * (gzip.rs:54-56) by default.  This flag selects the faster segmented coder
- * instead (16 KiB blocks, each ended by an empty stored block; the stream
- * inflates to the same data, but its bytes differ from zlib's).  Levels 1-3
- * always use the segmented coder. */
+/* Gzip encode at levels 1-9 is byte-identical to zlib 1.2.11 / flate2
+ * (gzip.rs:54-56) by default (deflate_fast for 1-3, deflate_slow for 4-9).
+ * This flag selects the faster segmented coder instead (16 KiB blocks, each
+ * ended by an empty stored block; the stream inflates to the same data, but
+ * its bytes differ from zlib's).  Level 0 always uses the segmented coder. */
 #define ZCG_FLAG_GZIP_SEGMENTED 0x8000u
 
 /* CompressionType + its configuration (camelCase JSON keys in the reference). */
