@@ -742,7 +742,16 @@ __global__ __launch_bounds__(256) void lz4_blocks_kernel(const zcg_chunk* __rest
 constexpr u32 LZ_LRB = 128;         // ring bytes per lane (>= 2 * LZ_LPC)
 constexpr u32 LZ_LPC = LZ_LRB / 2;  // flush granularity = longest piece written between flushes
 constexpr u32 LZ_LRM = LZ_LRB - 1;
-constexpr u32 LZ_LWG = 64;          // lanes (blocks) per workgroup
+constexpr u32 LZ_LWG = 64;          // lanes per workgroup of the lane kernel
+#ifndef LZ_LPW_SMALL
+#define LZ_LPW_SMALL 64  // blocks per wave below LZ_LPW_THRESH blocks (fewer blocks per wave: more waves in flight)
+#endif
+#ifndef LZ_LPW_CORUN
+#define LZ_LPW_CORUN 64  // blocks per wave of the lane kernel when it shares the GPU with the wave kernel
+#endif
+#ifndef LZ_LPW_THRESH
+#define LZ_LPW_THRESH 262144
+#endif
 constexpr u64 LZ_LANE_MIN_BLOCKS = 131072;
 // From 131 072 blocks (measured at 8 192 C4 chunks: lanes 50.6 ms, waves 54.3
 // ms, 55 % lanes + 45 % waves side by side 45.0 ms) both kernels run at once on
@@ -999,9 +1008,10 @@ __device__ __forceinline__ int lz4_lane_block(const u8* __restrict__ src, u32 ie
 __global__ __launch_bounds__(LZ_LWG, 1) void lz4_lanes_kernel(const zcg_chunk* __restrict__ chunks, u32 n, u64 D,
                                                            u32 S, u32 vflags,
                                                            const Lz4ChunkInfo* __restrict__ info,
-                                                           Lz4Slot* __restrict__ slots) {
+                                                           Lz4Slot* __restrict__ slots, u32 lpw) {
     __shared__ __attribute__((aligned(16))) u8 rings[LZ_LWG * LZ_LSTRIDE];
-    const u64 g = (u64)blockIdx.x * LZ_LWG + threadIdx.x;
+    if (threadIdx.x >= lpw) return;  // lpw blocks per wave
+    const u64 g = (u64)blockIdx.x * lpw + threadIdx.x;
     const u32 c = (u32)(g / S);
     const u32 k = (u32)(g - (u64)c * S);
     if (c >= n) return;
@@ -1138,14 +1148,16 @@ hipError_t launch_lz4_decode(const zcg_array* a, const zcg_chunk* d_chunks, uint
                                D, (u32)S, a->compression.flags, (const Lz4ChunkInfo*)info + n1, slots + (u64)n1 * S);
             const u64 w1 = (u64)n1 * S;
             if (w1)
-                hipLaunchKernelGGL(lz4_lanes_kernel, dim3((u32)((w1 + LZ_LWG - 1) / LZ_LWG)), dim3(LZ_LWG), 0, s,
-                                   d_chunks, n1, D, (u32)S, a->compression.flags, (const Lz4ChunkInfo*)info, slots);
+                hipLaunchKernelGGL(lz4_lanes_kernel, dim3((u32)((w1 + LZ_LPW_CORUN - 1) / LZ_LPW_CORUN)), dim3(LZ_LWG),
+                                   0, s, d_chunks, n1, D, (u32)S, a->compression.flags, (const Lz4ChunkInfo*)info,
+                                   slots, (u32)LZ_LPW_CORUN);
             e = hipEventRecord(join, s2);
             if (e == hipSuccess) e = hipStreamWaitEvent(s, join, 0);
             if (e != hipSuccess) return e;
         } else {
-            hipLaunchKernelGGL(lz4_lanes_kernel, dim3((u32)((waves + LZ_LWG - 1) / LZ_LWG)), dim3(LZ_LWG), 0, s,
-                               d_chunks, n, D, (u32)S, a->compression.flags, (const Lz4ChunkInfo*)info, slots);
+            const u32 lpw = waves < LZ_LPW_THRESH ? LZ_LPW_SMALL : LZ_LWG;
+            hipLaunchKernelGGL(lz4_lanes_kernel, dim3((u32)((waves + lpw - 1) / lpw)), dim3(LZ_LWG), 0, s,
+                               d_chunks, n, D, (u32)S, a->compression.flags, (const Lz4ChunkInfo*)info, slots, lpw);
         }
     }
     hipLaunchKernelGGL(lz4_finish_kernel, dim3(n), dim3(64), 0, s, d_chunks, n, D, t, a->compression.flags,
