@@ -766,6 +766,15 @@ __global__ void df_best(const zcg_chunk* __restrict__ chunks, u32 c0, u64 D, u64
 namespace {
 
 constexpr u64 DZ_SUPER_BYTES = 512ull << 20;  // input bytes per super-batch (match results kept for all)
+// 1: the parse runs each match search where it needs it (only at the loop
+// tops its speculative parses visit, ~40 % of the positions), per sub-batch
+// over the sub-batch's chains; 0 (default): dz_best searches every position
+// first.  Measured on C5 (512 chunks, level 6): 5 347 vs 217 ms -- a
+// sub-batch is 128 waves, and each lane's searches are a serial chain of
+// dependent loads, so the on-demand form starves for parallelism.
+#ifndef ZDZ_ONDEMAND
+#define ZDZ_ONDEMAND 0
+#endif
 constexpr u32 DZ_TAILCAP = 2048;               // symbols a segment's parse may run past its end before syncing
 constexpr u32 DZ_HDRW = 96;                 // header bit-string words per block (<= 14 + 57 + 316 * 14 bits)
 
@@ -894,14 +903,20 @@ __global__ void dz_best(const zcg_chunk* __restrict__ chunks, u32 c0, u64 D, u64
 // sync within DZ_TAILCAP symbols sends the chunk to a serial parse.  The
 // stitched stream and block records equal deflate_slow's
 // (tests/hostcore/zlib_ref.cpp zz_host_deflate_seg restates this exactly).
+// prevs != nullptr: the match searches run on demand, at the loop tops the
+// parses visit (zz::step asks only where prev_len < max_lazy), over the
+// sub-batch's chains (chunk c of the launch = chunk cb + c of the
+// super-batch's records); nullptr: from dz_best's per-position results.
 __global__ __launch_bounds__(64) void dz_parse(const zcg_chunk* __restrict__ chunks, u32 c0, u32 nc, u64 D, DType t,
                                               zz::Config cfg, u32* __restrict__ wbase, u64 off_m2, u64 off_sym,
                                               u64 off_pos, u64 off_bm, u64 off_tail, DzChunk* __restrict__ cst,
-                                              DzBlock* __restrict__ blks, u32 nbmax) {
-    const u32 c = blockIdx.x;
-    if (c >= nc) return;
+                                              DzBlock* __restrict__ blks, u32 nbmax, const u32* __restrict__ prevs,
+                                              u32 cb) {
+    const u32 cl = blockIdx.x;  // chunk of this launch (of the sub-batch when prevs != nullptr)
+    if (cl >= nc) return;
+    const u32 c = cb + cl;      // chunk of the super-batch's records
     const u32 lane = threadIdx.x;
-    const zcg_chunk ch = chunks[c0 + c];
+    const zcg_chunk ch = chunks[c0 + cl];
     DzChunk* cs = cst + c;
     if (ch.src_len < D) {
         if (lane == 0) { cs->nblocks = 0; cs->status = ZCG_ERR_INVALID_DATA; }
@@ -921,11 +936,19 @@ __global__ __launch_bounds__(64) void dz_parse(const zcg_chunk* __restrict__ chu
     const u32 nseg = D32 ? (D32 + seg - 1) / seg : 1u;
     const bool act = lane < nseg;
     const u32 S0 = lane * seg, S1 = (lane + 1 == nseg) ? D32 : (lane + 1) * seg;
+    auto b4 = [&](u32 i) -> u32 { return df_ser4(src, i, t); };
+    const u32* pvc = prevs ? prevs + (u64)cl * D : nullptr;
+    const u64 gbase = (u64)cl * D;  // chain links are indices into the sub-batch
+    auto pv = [&](u32 i) -> u32 {
+        const u32 q = pvc[i];
+        return q == 0xFFFFFFFFu ? zz::NONE : (u32)(q - gbase);
+    };
+    auto byte = [&](u32 i) -> u32 { return df_ser1(src, i, t); };
     auto get = [&](u32 p) -> zz::Match2 {
+        if (pvc) return zz::search(p, D32, cfg, b4, byte, pv);
         const uint2 v = mc[p];
         return zz::Match2{v.x, v.y};
     };
-    auto byte = [&](u32 i) -> u32 { return df_ser1(src, i, t); };
     // ---- pass 1 ----
     zz::PState st = zz::fresh_state(S0);
     u32 n1 = 0, fin1 = 0;
@@ -1047,8 +1070,8 @@ __global__ __launch_bounds__(64) void dz_parse(const zcg_chunk* __restrict__ chu
             k++;
         };
         auto gu = [&](u32 p) -> zz::Match2 {
-            const uint2 v = mc[p];
-            return zz::Match2{(u32)__builtin_amdgcn_readfirstlane(v.x), (u32)__builtin_amdgcn_readfirstlane(v.y)};
+            const zz::Match2 v = get(p);
+            return zz::Match2{(u32)__builtin_amdgcn_readfirstlane(v.full), (u32)__builtin_amdgcn_readfirstlane(v.red)};
         };
         auto bu = [&](u32 i) -> u32 { return (u32)__builtin_amdgcn_readfirstlane(df_ser1(src, i, t)); };
         while (s2.p < D32) zz::step(s2, D32, cfg, gu, bu, em);
@@ -1562,7 +1585,7 @@ static hipError_t launch_deflate_exact(const zcg_array* a, const zcg_chunk* d_ch
     }
     for (u32 s0 = 0; s0 < n; s0 += y.sb) {
         const u32 scnt = (n - s0) < y.sb ? (n - s0) : y.sb;
-        for (u32 c0 = s0; c0 < s0 + scnt && D > 0 && !fast; c0 += y.m) {
+        for (u32 c0 = s0; c0 < s0 + scnt && D > 0 && !fast; c0 += y.m) {  // (ZDZ_ONDEMAND: the parse per sub-batch)
             const u32 cnt = (s0 + scnt - c0) < y.m ? (s0 + scnt - c0) : y.m;
             const u64 tot = (u64)cnt * D;
             u32 *ka = (u32*)(w + y.off_ka), *kb = (u32*)(w + y.off_kb);
@@ -1578,20 +1601,33 @@ static hipError_t launch_deflate_exact(const zcg_array* a, const zcg_chunk* d_ch
             if (e != hipSuccess) return e;
             hipLaunchKernelGGL(dz_chain, dim3(G), dim3(256), 0, s, tot, dk.Current(), dv.Current(),
                                (u32*)(w + y.off_prev));
-            hipLaunchKernelGGL(dz_best, dim3(G), dim3(256), 0, s, d_chunks, c0, D, tot, t, cfg,
-                               (const u32*)(w + y.off_prev), m2 + (u64)(c0 - s0) * D);
+            if (ZDZ_ONDEMAND) {
+                if (c0 == s0) {
+                    if (hipError_t e = hipMemsetAsync(cst, 0xFF, sizeof(DzChunk) * (size_t)scnt, s); e != hipSuccess)
+                        return e;
+                }
+                hipLaunchKernelGGL(dz_parse, dim3(cnt), dim3(64), 0, s, d_chunks, c0, cnt, D, t, cfg, (u32*)w,
+                                   y.off_m2 / 4, y.off_sym / 4, y.off_pos / 4, y.off_bm / 4, y.off_tail / 4, cst,
+                                   blks, y.nbmax, (const u32*)(w + y.off_prev), c0 - s0);
+            } else {
+                hipLaunchKernelGGL(dz_best, dim3(G), dim3(256), 0, s, d_chunks, c0, D, tot, t, cfg,
+                                   (const u32*)(w + y.off_prev), m2 + (u64)(c0 - s0) * D);
+            }
         }
         // a parse that does not run leaves every chunk failed, so the kernels
         // after it never read an unset record
-        if (hipError_t e = hipMemsetAsync(cst, 0xFF, sizeof(DzChunk) * (size_t)scnt, s); e != hipSuccess) return e;
+        if (fast || !ZDZ_ONDEMAND) {
+            if (hipError_t e = hipMemsetAsync(cst, 0xFF, sizeof(DzChunk) * (size_t)scnt, s); e != hipSuccess) return e;
+        }
         if (fast) {
             hipLaunchKernelGGL(dz_parse_fast, dim3(scnt), dim3(64), DZF_LDS, s, d_chunks, s0, scnt, D, t, cfg, (u32*)w,
                                y.off_m2 / 4, cst, blks, y.nbmax);
             if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
-        } else
+        } else if (!ZDZ_ONDEMAND) {
             hipLaunchKernelGGL(dz_parse, dim3(scnt), dim3(64), 0, s, d_chunks, s0, scnt, D, t, cfg, (u32*)w,
                                y.off_m2 / 4, y.off_sym / 4, y.off_pos / 4, y.off_bm / 4, y.off_tail / 4, cst, blks,
-                               y.nbmax);
+                               y.nbmax, (const u32*)nullptr, 0u);
+        }
         const u64 nbk = (u64)scnt * y.nbmax;
         hipLaunchKernelGGL(dz_plan, dim3((u32)nbk), dim3(64), 0, s, scnt, cst, blks, y.nbmax, (const u32*)w, D);
         hipLaunchKernelGGL(dz_offsets, dim3((scnt + 63) / 64), dim3(64), 0, s, scnt, cst, blks, y.nbmax, out,
