@@ -222,6 +222,7 @@ struct BzDevIO {
     __device__ __forceinline__ u32 mtf_front() { return __builtin_amdgcn_readlane(mtfw, 0) & 0xFF; }
     __device__ __forceinline__ u32 mtf_take(u32 nn) {
         const u32 wn = nn >> 2, sh = (nn & 3) * 8;
+
         const u32 v = (__builtin_amdgcn_readlane(mtfw, wn) >> sh) & 0xFF;
         // lanes 0..wn shift by one lane: within DPP row 0 (row_shr:1) when
         // nn < 64, the common case; across rows through ds_bpermute
