@@ -772,6 +772,9 @@ constexpr u64 DZ_SUPER_BYTES = 512ull << 20;  // input bytes per super-batch (ma
 // first.  Measured on C5 (512 chunks, level 6): 5 347 vs 217 ms -- a
 // sub-batch is 128 waves, and each lane's searches are a serial chain of
 // dependent loads, so the on-demand form starves for parallelism.
+#ifndef ZDZF_RING
+#define ZDZF_RING 1  // deflate_fast: the 32 KiB input ring in LDS (160 KiB workgroup) when the device allows it
+#endif
 #ifndef ZDZ_ONDEMAND
 #define ZDZ_ONDEMAND 0
 #endif
@@ -1115,6 +1118,12 @@ __global__ __launch_bounds__(64) void dz_parse(const zcg_chunk* __restrict__ chu
 // emit kernels are shared.  tests/hostcore/zlib_ref.cpp (zz::parse_fast on
 // the CPU) and the GPU output are compared with zlib byte for byte.
 constexpr u32 DZF_LDS = 2 * 32768 * 2;  // head[] + prev[], u16 each
+// RING: the last 32 KiB of input (positions (p + 262 - 32768, p + 262],
+// which covers every candidate within MAX_DIST and its 258 bytes) also live
+// in LDS, so a chain candidate's compare is two LDS reads per side instead
+// of a global-memory round trip; 160 KiB, the whole CU's LDS
+constexpr u32 DZF_RING = 32768;
+constexpr u32 DZF_LDS_RING = DZF_LDS + DZF_RING;
 __device__ __forceinline__ u32 dzf_ld4(const u8* src, u32 x, u32 D, const DType& t) {  // bytes past D read 0
     if (x + 4 <= D) return df_ser4(src, x, t);
     u32 v = 0;
@@ -1122,12 +1131,14 @@ __device__ __forceinline__ u32 dzf_ld4(const u8* src, u32 x, u32 D, const DType&
         if (x + k < D) v |= df_ser1(src, x + k, t) << (8 * k);
     return v;
 }
+template <bool RING>
 __global__ __launch_bounds__(64) void dz_parse_fast(const zcg_chunk* __restrict__ chunks, u32 c0, u32 nc, u64 D,
                                                    DType t, zz::Config cfg, u32* __restrict__ wbase, u64 off_m2,
                                                    DzChunk* __restrict__ cst, DzBlock* __restrict__ blks, u32 nbmax) {
     extern __shared__ __attribute__((aligned(16))) u8 smem_raw[];
     u16* hd = (u16*)smem_raw;
     u16* pv = hd + 32768;
+    u8* ring = smem_raw + DZF_LDS;  // (RING) byte q at ring[q & (DZF_RING - 1)]
     const u32 c = blockIdx.x;
     if (c >= nc) return;
     const u32 lane = threadIdx.x;
@@ -1174,12 +1185,37 @@ __global__ __launch_bounds__(64) void dz_parse_fast(const zcg_chunk* __restrict_
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         return hh;
     };
+    // (RING) bytes [rf, F) into the ring from the register window, 64 per round
+    u32 rf = 0;
+    auto ring_fill = [&](u32 F) {
+        for (u32 q0 = rf; q0 < F; q0 += 64) {
+            const u32 q = q0 + lane;
+            const u32 o = q - wb, wi = o >> 2;
+            const u32 a0 = __shfl(w0, (int)(wi & 63)), a1 = __shfl(w1, (int)(wi & 63));
+            const u32 v = ((wi < 64 ? a0 : a1) >> (8 * (o & 3))) & 0xFFu;
+            if (q < F) ring[q & (DZF_RING - 1)] = (u8)v;
+        }
+        rf = F;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+    auto ring4 = [&](u32 x) -> u32 {  // ring bytes x..x+3 (LE)
+        const u32 a = x & ~3u, sh = 8 * (x & 3);
+        const u32 lo = *(const u32*)(ring + (a & (DZF_RING - 1)));
+        const u32 hi = *(const u32*)(ring + ((a + 4) & (DZF_RING - 1)));
+        return sh ? ((lo >> sh) | (hi << (32 - sh))) : lo;
+    };
     u32 p = 0;
     while (p < D32) {
-        if (p - wb >= 252) {  // keep [p, p + 260) in the window (wb <= p always)
+        if (p - wb >= 250) {  // keep [p, p + 262) in the window (wb <= p always)
             wb = p & ~3u;
             w0 = dzf_ld4(src, wb + 4 * lane, D32, t);
             w1 = dzf_ld4(src, wb + 256 + 4 * lane, D32, t);
+        }
+        if (RING) {
+            const u32 F = p + 262 < D32 ? p + 262 : D32;
+            if (F > rf) ring_fill(F);
         }
         {  // fill_window at the loop top: one slide when due
             const u32 wend = (D32 - base) > 2 * zz::WSIZE ? base + 2 * zz::WSIZE : D32;
@@ -1204,11 +1240,16 @@ __global__ __launch_bounds__(64) void dz_parse_fast(const zcg_chunk* __restrict_
                 const u32 nice = cfg.nice < look ? cfg.nice : look;
                 const u32 lim = p > zz::MAX_DIST ? p - zz::MAX_DIST : 0u;
                 // my 4 bytes of p.. (lane l: p + 4 l ..) from the window
-                const u32 o = p - wb + 4 * lane, wi = o >> 2, sh = 8 * (o & 3);
-                const u32 a0 = __shfl(w0, (int)(wi & 63)), a1 = __shfl(w1, (int)(wi & 63));
-                const u32 b0 = __shfl(w0, (int)((wi + 1) & 63)), b1 = __shfl(w1, (int)((wi + 1) & 63));
-                const u32 lo = wi < 64 ? a0 : a1, hi = (wi + 1) < 64 ? b0 : b1;
-                const u32 pw = sh ? ((lo >> sh) | (hi << (32 - sh))) : lo;
+                u32 pw;
+                if (RING) {
+                    pw = ring4(p + 4 * lane);
+                } else {
+                    const u32 o = p - wb + 4 * lane, wi = o >> 2, sh = 8 * (o & 3);
+                    const u32 a0 = __shfl(w0, (int)(wi & 63)), a1 = __shfl(w1, (int)(wi & 63));
+                    const u32 b0 = __shfl(w0, (int)((wi + 1) & 63)), b1 = __shfl(w1, (int)((wi + 1) & 63));
+                    const u32 lo = wi < 64 ? a0 : a1, hi = (wi + 1) < 64 ? b0 : b1;
+                    pw = sh ? ((lo >> sh) | (hi << (32 - sh))) : lo;
+                }
                 u32 best = 0, bstart = 0, cand = hh + base;
                 for (u32 k = 0; k < cfg.chain; k++) {
                     if (k > 0) {
@@ -1217,7 +1258,7 @@ __global__ __launch_bounds__(64) void dz_parse_fast(const zcg_chunk* __restrict_
                         cand = r + base;
                         if (cand <= lim) break;
                     }
-                    const u32 cw = 4 * lane < mx ? dzf_ld4(src, cand + 4 * lane, D32, t) : pw;
+                    const u32 cw = 4 * lane < mx ? (RING ? ring4(cand + 4 * lane) : dzf_ld4(src, cand + 4 * lane, D32, t)) : pw;
                     const u64 m = __ballot(pw != cw);
                     u32 len;
                     if (m) {
@@ -1226,7 +1267,8 @@ __global__ __launch_bounds__(64) void dz_parse_fast(const zcg_chunk* __restrict_
                         len = 4 * j + ((u32)__builtin_ctz(x) >> 3);
                     } else {
                         len = 256;
-                        while (len < mx && wbyte(p + len) == (u32)__builtin_amdgcn_readfirstlane(df_ser1(src, cand + len, t)))
+                        while (len < mx && wbyte(p + len) == (RING ? (u32)__builtin_amdgcn_readfirstlane((u32)ring[(cand + len) & (DZF_RING - 1)])
+                                                                   : (u32)__builtin_amdgcn_readfirstlane(df_ser1(src, cand + len, t))))
                             len++;
                     }
                     if (len > mx) len = mx;
@@ -1580,8 +1622,12 @@ static hipError_t launch_deflate_exact(const zcg_array* a, const zcg_chunk* d_ch
     DzBlock* blks = (DzBlock*)(w + y.off_blk);
     u8* out = w + y.off_out;
     const bool fast = level <= 3;
+    bool ring = false;  // the 160 KiB LDS form when the device grants it to one workgroup
     if (fast) {
-        if (hipError_t e = lds_attr_once((const void*)dz_parse_fast, (int)DZF_LDS); e != hipSuccess) return e;
+        ring = ZDZF_RING && lds_attr_once((const void*)dz_parse_fast<true>, (int)DZF_LDS_RING) == hipSuccess;
+        if (!ring) {
+            if (hipError_t e = lds_attr_once((const void*)dz_parse_fast<false>, (int)DZF_LDS); e != hipSuccess) return e;
+        }
     }
     for (u32 s0 = 0; s0 < n; s0 += y.sb) {
         const u32 scnt = (n - s0) < y.sb ? (n - s0) : y.sb;
@@ -1620,8 +1666,12 @@ static hipError_t launch_deflate_exact(const zcg_array* a, const zcg_chunk* d_ch
             if (hipError_t e = hipMemsetAsync(cst, 0xFF, sizeof(DzChunk) * (size_t)scnt, s); e != hipSuccess) return e;
         }
         if (fast) {
-            hipLaunchKernelGGL(dz_parse_fast, dim3(scnt), dim3(64), DZF_LDS, s, d_chunks, s0, scnt, D, t, cfg, (u32*)w,
-                               y.off_m2 / 4, cst, blks, y.nbmax);
+            if (ring)
+                hipLaunchKernelGGL(dz_parse_fast<true>, dim3(scnt), dim3(64), DZF_LDS_RING, s, d_chunks, s0, scnt, D, t,
+                                   cfg, (u32*)w, y.off_m2 / 4, cst, blks, y.nbmax);
+            else
+                hipLaunchKernelGGL(dz_parse_fast<false>, dim3(scnt), dim3(64), DZF_LDS, s, d_chunks, s0, scnt, D, t,
+                                   cfg, (u32*)w, y.off_m2 / 4, cst, blks, y.nbmax);
             if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
         } else if (!ZDZ_ONDEMAND) {
             hipLaunchKernelGGL(dz_parse, dim3(scnt), dim3(64), 0, s, d_chunks, s0, scnt, D, t, cfg, (u32*)w,
