@@ -12,7 +12,7 @@ for set in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD S
            "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_SMEM SQ_ACTIVE_INST_VMEM SQ_INST_CYCLES_VMEM_RD SQ_ACTIVE_INST_MISC SQ_ACTIVE_INST_FLAT SQ_INSTS_FLAT"; do
   i=$((i+1))
   timeout -s KILL 240 rocprofv3 --pmc $set --output-format csv -d "$R/gpurun_out/infpmc/p$i" -o pmc -- \
-    python3 "$R/bench.py" --codec gzip --steps 1 --warmup 1 --no-extra --no-cpu-baseline \
+    python3 "$R/bench.py" --codec ${CODEC:-gzip} --steps 1 --warmup 1 --no-extra --no-cpu-baseline \
     > "$R/gpurun_out/infpmc/p$i.log" 2>&1 || { echo "pass $i failed"; tail -5 "$R/gpurun_out/infpmc/p$i.log"; exit 1; }
 done
 K="$K" python3 - <<'PY'
