@@ -72,6 +72,9 @@ constexpr u32 IW_SEGMIN = 128;   // bits per lane segment
 constexpr u32 IW_SEGMAX = 4096;
 constexpr u32 IW_K = 4;          // decode steps between staged-token / mark flushes
 constexpr u32 IW_KH = 2;         // flush periods per outer step (reader loads at its top, absorbs at its bottom)
+#ifndef ZIW_GRB
+#define ZIW_GRB 1  // stream reader: bit cursor + barrel select (0: round-4 shifted 96-bit window)
+#endif
 #ifndef ZIW_G
 #define ZIW_G 4
 #endif
@@ -207,6 +210,61 @@ __device__ __forceinline__ u32 iw_wave_sum(u32 v) {
 // every step; a loop-carried register in flight is copied at the loop header,
 // which waits as well; and a flat (generic) load would also hold every LDS
 // table lookup.
+#if ZIW_GRB
+// Round 5: a bit cursor bp into the 256 bits of A:B instead of a shifted
+// window.  Each step selects the three words from bp >> 5 by a 3-level
+// barrel select (11 selects) and funnel-shifts them (2 v_alignbit), so a
+// step costs no word appends and no 64-bit shifts; dropping bits is one add.
+// Same run-dry rule as the window reader: a lane decodes while >= 48 bits of
+// A:B are left (bp <= 208).
+struct GRd {
+    u32x4 A, B;
+    u32 bp;  // bit cursor into A:B (0..256)
+    u32 vc;  // vector index after B
+    u64 lo;  // 64 stream bits from bp (>= 48 valid), set by gr_fill
+};
+
+typedef __attribute__((address_space(1))) u32x4 gu32x4;
+__device__ __forceinline__ u32x4 gr_vec(const u8* base, u32 nvec, u32 v) {
+    const u32 vc = v < nvec ? v : (nvec ? nvec - 1 : 0u);
+    return *(const gu32x4*)((const gu8*)base + 16ull * vc);
+}
+
+__device__ __forceinline__ bool gr_fill(GRd& s) {
+    const u32 bp = s.bp;
+    if (bp > 208) return false;
+    const bool b4 = (bp & 128) != 0, b2 = (bp & 64) != 0, b1 = (bp & 32) != 0;
+    // word i = bp >> 5 <= 6 of R = A:B: T[k] = R[k + 4 b4], U[k] = T[k + 2 b2],
+    // W[k] = U[k + b1]; R[8] (needed only as W2 at i = 6) is don't-care
+    const u32 t0 = b4 ? s.B.x : s.A.x, t1 = b4 ? s.B.y : s.A.y, t2 = b4 ? s.B.z : s.A.z,
+              t3 = b4 ? s.B.w : s.A.w, t4 = s.B.x, t5 = s.B.y;
+    const u32 u0 = b2 ? t2 : t0, u1 = b2 ? t3 : t1, u2 = b2 ? t4 : t2, u3 = b2 ? t5 : t3;
+    const u32 w0 = b1 ? u1 : u0, w1 = b1 ? u2 : u1, w2 = b1 ? u3 : u2;
+    const u32 lo = __builtin_amdgcn_alignbit(w1, w0, bp & 31);
+    const u32 hi = __builtin_amdgcn_alignbit(w2, w1, bp & 31);
+    s.lo = ((u64)hi << 32) | lo;
+    return true;
+}
+
+__device__ __forceinline__ void gr_drop(GRd& s, u32 k) { s.bp += k; }
+
+__device__ __forceinline__ void gr_absorb(GRd& s, const u32x4& C, const u32x4& D) {
+    const u32 sh = s.bp >= 256 ? 2u : s.bp >= 128 ? 1u : 0u;
+    s.A = sh == 2 ? C : sh == 1 ? s.B : s.A;
+    s.B = sh == 2 ? D : sh == 1 ? C : s.B;
+    s.vc += sh;
+    s.bp -= 128 * sh;
+}
+
+__device__ __forceinline__ void gr_init(GRd& s, const u8* base, u32 nvec, u32 qa) {
+    const u32 v0 = qa >> 7;
+    s.A = gr_vec(base, nvec, v0);
+    s.B = gr_vec(base, nvec, v0 + 1);
+    s.vc = v0 + 2;
+    s.bp = qa & 127;
+    s.lo = 0;
+}
+#else
 struct GRd {
     u64 lo;
     u32 hi;
@@ -276,6 +334,7 @@ __device__ __forceinline__ void gr_init(GRd& s, const u8* base, u32 nvec, u32 qa
     const u32 k = qa & 31;
     if (k) gr_drop(s, k);
 }
+#endif
 
 // Decode one token from >= 48 valid bits: both table lookups always run, so
 // lanes holding different token kinds do not serialise.
