@@ -72,6 +72,9 @@ constexpr u32 IW_SEGMIN = 128;   // bits per lane segment
 constexpr u32 IW_SEGMAX = 4096;
 constexpr u32 IW_K = 4;          // decode steps between staged-token / mark flushes
 constexpr u32 IW_KH = 2;         // flush periods per outer step (reader loads at its top, absorbs at its bottom)
+#ifndef ZIW_BCAST
+#define ZIW_BCAST 1  // wave scans finish with DPP row_bcast:15/31 (0: lane 15/31/47 readlanes and selects)
+#endif
 #ifndef ZIW_GRB
 #define ZIW_GRB 1  // stream reader: bit cursor + barrel select (0: round-4 shifted 96-bit window)
 #endif
@@ -182,11 +185,18 @@ __device__ __forceinline__ u32 iw_incl_scan(u32 v) {
     v += (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
     v += (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
     v += (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
+#if ZIW_BCAST
+    // rows -> wave: lane 15 into rows 1 and 3, then lane 31 into rows 2 and 3
+    v += (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    v += (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+    return v;
+#else
     const u32 t0 = (u32)__builtin_amdgcn_readlane((int)v, 15);
     const u32 t1 = t0 + (u32)__builtin_amdgcn_readlane((int)v, 31);
     const u32 t2 = t1 + (u32)__builtin_amdgcn_readlane((int)v, 47);
     const u32 lane = (u32)lane_id();
     return v + (lane < 16 ? 0u : (lane < 32 ? t0 : (lane < 48 ? t1 : t2)));
+#endif
 }
 
 __device__ __forceinline__ u32 iw_wave_sum(u32 v) {
@@ -441,11 +451,17 @@ __device__ __forceinline__ int iw_incl_max(int v) {
     v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x112, 0xf, 0xf, false));  // row_shr:2
     v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x114, 0xf, 0xf, false));  // row_shr:4
     v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x118, 0xf, 0xf, false));  // row_shr:8
+#if ZIW_BCAST
+    v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x142, 0xa, 0xf, false));  // row_bcast:15
+    v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x143, 0xc, 0xf, false));  // row_bcast:31
+    return v;
+#else
     const int t0 = __builtin_amdgcn_readlane(v, 15);
     const int t1 = max(t0, __builtin_amdgcn_readlane(v, 31));
     const int t2 = max(t1, __builtin_amdgcn_readlane(v, 47));
     const u32 lane = (u32)lane_id();
     return lane < 16 ? v : max(v, lane < 32 ? t0 : (lane < 48 ? t1 : t2));
+#endif
 }
 
 __device__ __forceinline__ u32 swap_pos32(u32 p, const DType& t) {
