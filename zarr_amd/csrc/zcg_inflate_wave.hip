@@ -75,6 +75,12 @@ constexpr u32 IW_KH = 2;         // flush periods per outer step (reader loads a
 #ifndef ZIW_BCAST
 #define ZIW_BCAST 1  // wave scans finish with DPP row_bcast:15/31 (0: lane 15/31/47 readlanes and selects)
 #endif
+#ifndef ZIW_S1
+#define ZIW_S1 1  // chain member successors' first tokens shifted into the member's lane once per round
+#endif
+#ifndef ZIW_FARV1
+#define ZIW_FARV1 1  // far tokens: the second 16-byte piece loaded unconditionally
+#endif
 #ifndef ZIW_GRB
 #define ZIW_GRB 1  // stream reader: bit cursor + barrel select (0: round-4 shifted 96-bit window)
 #endif
@@ -891,7 +897,14 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
             // lane's token at the cursor + lane (a member's list may end inside a group)
             auto mL = [&](u32 m) -> u32 { return (u32)__builtin_amdgcn_readlane((int)chL, (int)m); };
             auto mE = [&](u32 m) -> u32 { return (u32)__builtin_amdgcn_readlane((int)chE, (int)m); };
+#if ZIW_S1
+            // member m's successor's first valid token, in lane m (0 past the chain)
+            const u32 chSn = (u32)__shfl_down((int)chS, 1, 64);  // (every lane: a lane reads an active lane)
+            const u32 chS1 = lane + 1 < ncm ? chSn : 0u;
+            auto mS1 = [&](u32 m) -> u32 { return (u32)__builtin_amdgcn_readlane((int)chS1, (int)m); };
+#else
             auto mS1 = [&](u32 m) -> u32 { return m + 1 < ncm ? (u32)__builtin_amdgcn_readlane((int)chS, (int)(m + 1)) : 0u; };
+#endif
             auto advance = [&](u32& cm0, u32& cj0, u32 k) {
                 cj0 += k;
                 while (cm0 < ncm) {
@@ -1043,8 +1056,15 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
                                 const u32 qb = hi & (IW_S - 1), r = (hi >> 11) & 3u, e = r + (hi >> 16);
                                 const u32 np = (e + 15) >> 4;
                                 const u32x4 V0 = *(const gu32x4_ua*)(gd + src);
+#if ZIW_FARV1
+                                // unconditional (a second read of the first piece when
+                                // there is one piece): a load kept under a branch waited
+                                // for the first one before issuing
+                                const u32x4 V1 = *(const gu32x4_ua*)(gd + src + (np > 1 ? 16u : 0u));
+#else
                                 u32x4 V1 = V0;
                                 if (np > 1) V1 = *(const gu32x4_ua*)(gd + src + 16);
+#endif
                                 auto piece = [&](const u32x4& V, u32 p) {
 #pragma unroll
                                     for (u32 q = 0; q < 4; q++) {

@@ -444,17 +444,16 @@ __device__ __forceinline__ LzSeq lz4_seq_at(const gu8* __restrict__ s, u32 iend,
 }
 
 // inclusive prefix sum over the wave: DPP row shifts within each 16-lane row,
-// then the three row totals (v_readlane) added to the rows above them
+// then the row totals broadcast down (row_bcast:15 into rows 1 and 3,
+// row_bcast:31 into rows 2 and 3)
 __device__ __forceinline__ u32 wave_incl_scan(u32 v) {
     v += (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
     v += (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
     v += (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
     v += (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
-    const u32 t0 = (u32)__builtin_amdgcn_readlane((int)v, 15);
-    const u32 t1 = t0 + (u32)__builtin_amdgcn_readlane((int)v, 31);
-    const u32 t2 = t1 + (u32)__builtin_amdgcn_readlane((int)v, 47);
-    const u32 lane = (u32)lane_id();
-    return v + (lane < 16 ? 0u : (lane < 32 ? t0 : (lane < 48 ? t1 : t2)));
+    v += (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    v += (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+    return v;
 }
 
 struct LzRing {
