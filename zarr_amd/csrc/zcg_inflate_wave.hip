@@ -81,6 +81,12 @@ constexpr u32 IW_KH = 2;         // flush periods per outer step (reader loads a
 #ifndef ZIW_FARV1
 #define ZIW_FARV1 1  // far tokens: the second 16-byte piece loaded unconditionally
 #endif
+#ifndef ZIW_MUL24
+#define ZIW_MUL24 1  // token-list addresses with the 24-bit multiply
+#endif
+#ifndef ZIW_SCUR
+#define ZIW_SCUR 1  // group cursor walks on scalar registers
+#endif
 #ifndef ZIW_GRB
 #define ZIW_GRB 1  // stream reader: bit cursor + barrel select (0: round-4 shifted 96-bit window)
 #endif
@@ -94,7 +100,12 @@ static_assert(IW_TSTR % 4 == 0 && 64 % IW_G == 0, "list blocks");
 // are interleaved by aligned 4-word blocks, so one flush of those lanes fills
 // whole cache lines ([lane / G][j / 4][lane % G][j % 4]; G = 1: [lane][j])
 __device__ __forceinline__ u32 iw_ta(u32 l, u32 j) {
+#if ZIW_MUL24
+    // (< 2^24 operands: the full-rate 24-bit multiply, not the quarter-rate 32-bit one)
+    return __umul24(l / IW_G, IW_G * IW_TSTR) + (((j >> 2) * IW_G + (l % IW_G)) << 2) + (j & 3);
+#else
     return (l / IW_G) * (IW_G * IW_TSTR) + (((j >> 2) * IW_G + (l % IW_G)) << 2) + (j & 3);
+#endif
 }
 constexpr u32 IW_MWIN = 8;                       // mark words a lane keeps in LDS between flushes
 #ifndef ZIW_MARKW
@@ -906,6 +917,18 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
             auto mS1 = [&](u32 m) -> u32 { return m + 1 < ncm ? (u32)__builtin_amdgcn_readlane((int)chS, (int)(m + 1)) : 0u; };
 #endif
             auto advance = [&](u32& cm0, u32& cj0, u32 k) {
+#if ZIW_SCUR
+                // (wave-uniform: kept in scalar registers)
+                u32 m = (u32)__builtin_amdgcn_readfirstlane((int)cm0), j = (u32)__builtin_amdgcn_readfirstlane((int)(cj0 + k));
+                while (m < ncm) {
+                    const u32 e = mE(m);
+                    if (j < e) break;
+                    j = j - e + mS1(m);
+                    m++;
+                }
+                cm0 = m;
+                cj0 = j;
+#else
                 cj0 += k;
                 while (cm0 < ncm) {
                     const u32 e = mE(cm0);
@@ -913,6 +936,7 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
                     cj0 = cj0 - e + mS1(cm0);
                     cm0++;
                 }
+#endif
             };
             // The token words of the next IW_GK groups are in flight while a
             // group is placed (the lists sit in MALL/HBM: ~2 K cycles away).
@@ -931,7 +955,11 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
             // register, even a select, waits for it.
             auto fetch2 = [&](u32 cm0, u32 cj0, u32& ta, u32& tb, u32& ok) {
                 u32 ja = cj0 + 2 * lane, jb = ja + 1, la = 0xFFFFFFFFu, lb = 0xFFFFFFFFu, pa = 0, pb = 0;
+#if ZIW_SCUR
+                for (u32 m = (u32)__builtin_amdgcn_readfirstlane((int)cm0); m < ncm; m++) {
+#else
                 for (u32 m = cm0; m < ncm; m++) {
+#endif
                     const u32 e = mE(m), ln = mL(m), s1 = mS1(m);
                     if (la == 0xFFFFFFFFu && ja < e) { la = ln; pa = ja; }
                     if (lb == 0xFFFFFFFFu && jb < e) { lb = ln; pb = jb; }
