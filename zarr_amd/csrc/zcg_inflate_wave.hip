@@ -87,6 +87,9 @@ constexpr u32 IW_KH = 2;         // flush periods per outer step (reader loads a
 #ifndef ZIW_SCUR
 #define ZIW_SCUR 1  // group cursor walks on scalar registers
 #endif
+#ifndef ZIW_DEC32
+#define ZIW_DEC32 1  // token decode on 32-bit fields (one v_alignbit instead of 64-bit shifts)
+#endif
 #ifndef ZIW_GRB
 #define ZIW_GRB 1  // stream reader: bit cursor + barrel select (0: round-4 shifted 96-bit window)
 #endif
@@ -371,6 +374,17 @@ __device__ __forceinline__ u32 iw_decode(const IwLds& L, u64 v, u32* adv) {
         e = L.ltab[(e & 0xFFFF) + (((u32)v >> W_LB) & ((1u << ((e >> 16) & 0xFF)) - 1))];
     const u32 l = e >> 28, kind = (e >> 24) & 15, ex = (e >> 16) & 0xFF;
     const u32 t = l + ex;
+#if ZIW_DEC32
+    // 32-bit fields only: the length code and its extra bits end by bit 20,
+    // and the distance code and its extra bits take <= 28 bits from t
+    const u32 vd = __builtin_amdgcn_alignbit((u32)(v >> 32), (u32)v, t);
+    u32 de = L.dtab[vd & ((1u << W_DB) - 1)];
+    if (((de >> 24) & 15) == K_SUB)
+        de = L.dtab[(de & 0xFFFF) + ((vd >> W_DB) & ((1u << ((de >> 16) & 0xFF)) - 1))];
+    const u32 dl = de >> 28, dex = (de >> 16) & 0xFF;
+    const u32 len = (e & 0xFFFF) + (((u32)v >> l) & ((1u << ex) - 1));
+    const u32 dist = (de & 0xFFFF) + ((vd >> dl) & ((1u << dex) - 1));
+#else
     const u64 vd = v >> t;
     u32 de = L.dtab[(u32)vd & ((1u << W_DB) - 1)];
     if (((de >> 24) & 15) == K_SUB)
@@ -378,6 +392,7 @@ __device__ __forceinline__ u32 iw_decode(const IwLds& L, u64 v, u32* adv) {
     const u32 dl = de >> 28, dex = (de >> 16) & 0xFF;
     const u32 len = (e & 0xFFFF) + ((u32)(v >> l) & ((1u << ex) - 1));
     const u32 dist = (de & 0xFFFF) + ((u32)(vd >> dl) & ((1u << dex) - 1));
+#endif
     const u32 madv = t + dl + dex;
     const bool dok = ((de >> 24) & 15) == K_DIST;
     u32 a = l ? l : 1;
