@@ -79,7 +79,9 @@ enum zcg_status {
 /* Use the wave-serial inflate kernel instead of the parallel one (the two are
  * bit-identical; the serial one is kept as a differential reference). */
 #define ZCG_FLAG_SERIAL_INFLATE 0x100u
-/* Accumulate internal kernel statistics (development builds / profiling). */
+/* Accumulate internal kernel statistics (development builds / profiling; the
+ * default build compiles the inflate wave kernel's counters out, so there the
+ * flag changes nothing). */
 #define ZCG_FLAG_DEBUG_COUNTERS 0x200u
 /* Xz decode keeps 32 KiB of history in LDS instead of 4 KiB: far matches
  * stop re-reading the output from L2/HBM, at 3 instead of 8 chunks per CU. */

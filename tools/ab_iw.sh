@@ -1,7 +1,9 @@
 #!/bin/bash
 # Inflate (wave per chunk) A/B: gzip parity tests, then tools/iw_stats.py
 # (HIP-event time, all chunks checked, phase counters) per variant.
-#   tools/ab_iw.sh name1 name2 ...   (variants/<name>.so)
+#   tools/ab_iw.sh name1 name2 ...   (variants/<name>.so; build them with
+#   -DZIW_DBG=1 for the phase cycle shares: the product build compiles the
+#   debug counters out and reports zero shares)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
