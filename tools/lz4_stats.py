@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""LZ4 block-decoder phase counters (ZCG_FLAG_DEBUG_COUNTERS) on C4-shaped
+"""LZ4 block-decoder phase counters (ZCG_FLAG_DEBUG_COUNTERS; needs a -DLZ_DBG=1 build) on C4-shaped
 chunks: liblz4 streams with lz4-rs settings, n chunks (GPU box)."""
 import ctypes, json, os, sys, time
 import numpy as np

@@ -514,7 +514,10 @@ struct LzRing {
     }
 };
 
-// Debug counters (flag ZCG_FLAG_DEBUG_COUNTERS), summed over all blocks:
+#ifndef LZ_DBG
+#define LZ_DBG 0  // 1: the wave decoder's debug counters compiled in (tools/lz4_stats.py)
+#endif
+// Debug counters (flag ZCG_FLAG_DEBUG_COUNTERS; LZ_DBG builds), summed over all blocks:
 // steps, heavy steps, bytes, cycles of parse / chain / entries / finish / total.
 __device__ unsigned long long g_lz_dbg[16];
 extern "C" int zcg__debug_lz4_counters(unsigned long long* out, int reset) {
@@ -715,7 +718,7 @@ __global__ __launch_bounds__(256) void lz4_blocks_kernel(const zcg_chunk* __rest
         } else {
             const u64 lb = D - op0 < ci.bmax ? D - op0 : ci.bmax;
             lz4_block_wave(s, cs, ch.src_len - so, dst + op0, ci.bmax, (u32)lb, ring,
-                           (vflags & ZCG_FLAG_DEBUG_COUNTERS) != 0, &got, &st);
+                           LZ_DBG && (vflags & ZCG_FLAG_DEBUG_COUNTERS) != 0, &got, &st);
         }
     }
     if (lane == 0) {
