@@ -275,6 +275,13 @@ ZB_INL int bz_block(IO& io, BzState& s) {
     u32 nblock = 0;
     u32 es = 0, nrun = 0;  // pending RUNA/RUNB run: es+1 copies after the run ends
     bool in_run = false;
+#ifndef ZB_GSAFE
+#define ZB_GSAFE 1
+#endif
+    // a group's G_SIZE symbols take <= 20 bits each: when that many bits (plus
+    // the table peek) are left at its start, no symbol of the group can reach
+    // the input limit and the per-symbol check is skipped
+    bool gsafe = false;
     for (;;) {
         // GET_MTF_VAL
         if (group_pos == 0) {
@@ -283,12 +290,13 @@ ZB_INL int bz_block(IO& io, BzState& s) {
             group_pos = G_SIZE;
             gsel = io.sel_get(group_no);
             ZB_U32(gsel);
+            gsafe = ZB_GSAFE && !ZB_LT(limbits - bp, G_SIZE * 20 + LUT_BITS);
         }
         group_pos--;
         u32 sym;
         {
             u32 hit = 0;
-            if (!ZB_LT(limbits - bp, LUT_BITS)) {
+            if (gsafe || !ZB_LT(limbits - bp, LUT_BITS)) {
                 const u32 e = io.lut_get(gsel, io.peek(bp, LUT_BITS));
                 if (e) {
                     bp += e & 31;
