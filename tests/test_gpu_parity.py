@@ -222,6 +222,20 @@ def test_gzip_large(data, variant):
     check("gzip", s, "u1", len(payload))
 
 
+@pytest.mark.parametrize("data", ["zeros", "text_like", "quant_f4", "randwalk_i2"])
+def test_inflate_wave_near_tag_wrap(data):
+    """The wave kernel tags its near-batch markers with a 24-bit counter
+    (zcg_inflate_wave.hip); when it wraps, every older marker is cleared.
+    ZCG_FLAG_DEBUG_TAG_WRAP starts the counter 16 below the wrap, so the wrap
+    runs in the first batches of each chunk; the bytes must not change."""
+    from zarr_amd._native import FLAG_DEBUG_TAG_WRAP
+    payload = DATASETS[data]()
+    st, s = zref.encode(zref.GZIP, 6, np.frombuffer(payload, np.uint8))
+    assert st == 0
+    for flags in (FLAG_INFLATE_WAVE, FLAG_INFLATE_WAVE | FLAG_DEBUG_TAG_WRAP):
+        assert gpu_decode("gzip", s, "u1", len(payload), flags=flags) == ("Ok", payload), flags
+
+
 @pytest.mark.parametrize("dt", ["<i2", ">i2", ">f4", ">u8", "bool"])
 def test_gzip_transform_large(dt):
     es, be, isb, npdt = dtype_info(dt)

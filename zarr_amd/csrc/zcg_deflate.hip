@@ -766,18 +766,6 @@ __global__ void df_best(const zcg_chunk* __restrict__ chunks, u32 c0, u64 D, u64
 namespace {
 
 constexpr u64 DZ_SUPER_BYTES = 512ull << 20;  // input bytes per super-batch (match results kept for all)
-// 1: the parse runs each match search where it needs it (only at the loop
-// tops its speculative parses visit, ~40 % of the positions), per sub-batch
-// over the sub-batch's chains; 0 (default): dz_best searches every position
-// first.  Measured on C5 (512 chunks, level 6): 5 347 vs 217 ms -- a
-// sub-batch is 128 waves, and each lane's searches are a serial chain of
-// dependent loads, so the on-demand form starves for parallelism.
-#ifndef ZDZF_RING
-#define ZDZF_RING 1  // deflate_fast: the 32 KiB input ring in LDS (160 KiB workgroup) when the device allows it
-#endif
-#ifndef ZDZ_ONDEMAND
-#define ZDZ_ONDEMAND 0
-#endif
 constexpr u32 DZ_TAILCAP = 2048;               // symbols a segment's parse may run past its end before syncing
 constexpr u32 DZ_HDRW = 96;                 // header bit-string words per block (<= 14 + 57 + 316 * 14 bits)
 
@@ -906,18 +894,17 @@ __global__ void dz_best(const zcg_chunk* __restrict__ chunks, u32 c0, u64 D, u64
 // sync within DZ_TAILCAP symbols sends the chunk to a serial parse.  The
 // stitched stream and block records equal deflate_slow's
 // (tests/hostcore/zlib_ref.cpp zz_host_deflate_seg restates this exactly).
-// prevs != nullptr: the match searches run on demand, at the loop tops the
-// parses visit (zz::step asks only where prev_len < max_lazy), over the
-// sub-batch's chains (chunk c of the launch = chunk cb + c of the
-// super-batch's records); nullptr: from dz_best's per-position results.
+// The match results come from dz_best (every position searched first:
+// searching on demand at the loop tops the parses visit, ~40 % of the
+// positions, measured 5 347 vs 217 ms per C5 call -- each lane's searches
+// are a serial chain of dependent loads).
 __global__ __launch_bounds__(64) void dz_parse(const zcg_chunk* __restrict__ chunks, u32 c0, u32 nc, u64 D, DType t,
                                               zz::Config cfg, u32* __restrict__ wbase, u64 off_m2, u64 off_sym,
                                               u64 off_pos, u64 off_bm, u64 off_tail, DzChunk* __restrict__ cst,
-                                              DzBlock* __restrict__ blks, u32 nbmax, const u32* __restrict__ prevs,
-                                              u32 cb) {
-    const u32 cl = blockIdx.x;  // chunk of this launch (of the sub-batch when prevs != nullptr)
+                                              DzBlock* __restrict__ blks, u32 nbmax) {
+    const u32 cl = blockIdx.x;  // chunk of this launch
     if (cl >= nc) return;
-    const u32 c = cb + cl;      // chunk of the super-batch's records
+    const u32 c = cl;
     const u32 lane = threadIdx.x;
     const zcg_chunk ch = chunks[c0 + cl];
     DzChunk* cs = cst + c;
@@ -940,15 +927,8 @@ __global__ __launch_bounds__(64) void dz_parse(const zcg_chunk* __restrict__ chu
     const bool act = lane < nseg;
     const u32 S0 = lane * seg, S1 = (lane + 1 == nseg) ? D32 : (lane + 1) * seg;
     auto b4 = [&](u32 i) -> u32 { return df_ser4(src, i, t); };
-    const u32* pvc = prevs ? prevs + (u64)cl * D : nullptr;
-    const u64 gbase = (u64)cl * D;  // chain links are indices into the sub-batch
-    auto pv = [&](u32 i) -> u32 {
-        const u32 q = pvc[i];
-        return q == 0xFFFFFFFFu ? zz::NONE : (u32)(q - gbase);
-    };
     auto byte = [&](u32 i) -> u32 { return df_ser1(src, i, t); };
     auto get = [&](u32 p) -> zz::Match2 {
-        if (pvc) return zz::search(p, D32, cfg, b4, byte, pv);
         const uint2 v = mc[p];
         return zz::Match2{v.x, v.y};
     };
@@ -1131,14 +1111,13 @@ __device__ __forceinline__ u32 dzf_ld4(const u8* src, u32 x, u32 D, const DType&
         if (x + k < D) v |= df_ser1(src, x + k, t) << (8 * k);
     return v;
 }
-template <bool RING>
 __global__ __launch_bounds__(64) void dz_parse_fast(const zcg_chunk* __restrict__ chunks, u32 c0, u32 nc, u64 D,
                                                    DType t, zz::Config cfg, u32* __restrict__ wbase, u64 off_m2,
                                                    DzChunk* __restrict__ cst, DzBlock* __restrict__ blks, u32 nbmax) {
     extern __shared__ __attribute__((aligned(16))) u8 smem_raw[];
     u16* hd = (u16*)smem_raw;
     u16* pv = hd + 32768;
-    u8* ring = smem_raw + DZF_LDS;  // (RING) byte q at ring[q & (DZF_RING - 1)]
+    u8* ring = smem_raw + DZF_LDS;  // byte q at ring[q & (DZF_RING - 1)]
     const u32 c = blockIdx.x;
     if (c >= nc) return;
     const u32 lane = threadIdx.x;
@@ -1185,7 +1164,7 @@ __global__ __launch_bounds__(64) void dz_parse_fast(const zcg_chunk* __restrict_
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         return hh;
     };
-    // (RING) bytes [rf, F) into the ring from the register window, 64 per round
+    // bytes [rf, F) into the ring from the register window, 64 per round
     u32 rf = 0;
     auto ring_fill = [&](u32 F) {
         for (u32 q0 = rf; q0 < F; q0 += 64) {
@@ -1213,7 +1192,7 @@ __global__ __launch_bounds__(64) void dz_parse_fast(const zcg_chunk* __restrict_
             w0 = dzf_ld4(src, wb + 4 * lane, D32, t);
             w1 = dzf_ld4(src, wb + 256 + 4 * lane, D32, t);
         }
-        if (RING) {
+        {
             const u32 F = p + 262 < D32 ? p + 262 : D32;
             if (F > rf) ring_fill(F);
         }
@@ -1240,16 +1219,7 @@ __global__ __launch_bounds__(64) void dz_parse_fast(const zcg_chunk* __restrict_
                 const u32 nice = cfg.nice < look ? cfg.nice : look;
                 const u32 lim = p > zz::MAX_DIST ? p - zz::MAX_DIST : 0u;
                 // my 4 bytes of p.. (lane l: p + 4 l ..) from the window
-                u32 pw;
-                if (RING) {
-                    pw = ring4(p + 4 * lane);
-                } else {
-                    const u32 o = p - wb + 4 * lane, wi = o >> 2, sh = 8 * (o & 3);
-                    const u32 a0 = __shfl(w0, (int)(wi & 63)), a1 = __shfl(w1, (int)(wi & 63));
-                    const u32 b0 = __shfl(w0, (int)((wi + 1) & 63)), b1 = __shfl(w1, (int)((wi + 1) & 63));
-                    const u32 lo = wi < 64 ? a0 : a1, hi = (wi + 1) < 64 ? b0 : b1;
-                    pw = sh ? ((lo >> sh) | (hi << (32 - sh))) : lo;
-                }
+                const u32 pw = ring4(p + 4 * lane);
                 u32 best = 0, bstart = 0, cand = hh + base;
                 for (u32 k = 0; k < cfg.chain; k++) {
                     if (k > 0) {
@@ -1258,7 +1228,7 @@ __global__ __launch_bounds__(64) void dz_parse_fast(const zcg_chunk* __restrict_
                         cand = r + base;
                         if (cand <= lim) break;
                     }
-                    const u32 cw = 4 * lane < mx ? (RING ? ring4(cand + 4 * lane) : dzf_ld4(src, cand + 4 * lane, D32, t)) : pw;
+                    const u32 cw = 4 * lane < mx ? ring4(cand + 4 * lane) : pw;
                     const u64 m = __ballot(pw != cw);
                     u32 len;
                     if (m) {
@@ -1267,8 +1237,7 @@ __global__ __launch_bounds__(64) void dz_parse_fast(const zcg_chunk* __restrict_
                         len = 4 * j + ((u32)__builtin_ctz(x) >> 3);
                     } else {
                         len = 256;
-                        while (len < mx && wbyte(p + len) == (RING ? (u32)__builtin_amdgcn_readfirstlane((u32)ring[(cand + len) & (DZF_RING - 1)])
-                                                                   : (u32)__builtin_amdgcn_readfirstlane(df_ser1(src, cand + len, t))))
+                        while (len < mx && wbyte(p + len) == (u32)__builtin_amdgcn_readfirstlane((u32)ring[(cand + len) & (DZF_RING - 1)]))
                             len++;
                     }
                     if (len > mx) len = mx;
@@ -1622,16 +1591,13 @@ static hipError_t launch_deflate_exact(const zcg_array* a, const zcg_chunk* d_ch
     DzBlock* blks = (DzBlock*)(w + y.off_blk);
     u8* out = w + y.off_out;
     const bool fast = level <= 3;
-    bool ring = false;  // the 160 KiB LDS form when the device grants it to one workgroup
+    // deflate_fast takes the whole CU's 160 KiB of LDS (head/prev + the input ring)
     if (fast) {
-        ring = ZDZF_RING && lds_attr_once((const void*)dz_parse_fast<true>, (int)DZF_LDS_RING) == hipSuccess;
-        if (!ring) {
-            if (hipError_t e = lds_attr_once((const void*)dz_parse_fast<false>, (int)DZF_LDS); e != hipSuccess) return e;
-        }
+        if (hipError_t e = lds_attr_once((const void*)dz_parse_fast, (int)DZF_LDS_RING); e != hipSuccess) return e;
     }
     for (u32 s0 = 0; s0 < n; s0 += y.sb) {
         const u32 scnt = (n - s0) < y.sb ? (n - s0) : y.sb;
-        for (u32 c0 = s0; c0 < s0 + scnt && D > 0 && !fast; c0 += y.m) {  // (ZDZ_ONDEMAND: the parse per sub-batch)
+        for (u32 c0 = s0; c0 < s0 + scnt && D > 0 && !fast; c0 += y.m) {
             const u32 cnt = (s0 + scnt - c0) < y.m ? (s0 + scnt - c0) : y.m;
             const u64 tot = (u64)cnt * D;
             u32 *ka = (u32*)(w + y.off_ka), *kb = (u32*)(w + y.off_kb);
@@ -1647,36 +1613,20 @@ static hipError_t launch_deflate_exact(const zcg_array* a, const zcg_chunk* d_ch
             if (e != hipSuccess) return e;
             hipLaunchKernelGGL(dz_chain, dim3(G), dim3(256), 0, s, tot, dk.Current(), dv.Current(),
                                (u32*)(w + y.off_prev));
-            if (ZDZ_ONDEMAND) {
-                if (c0 == s0) {
-                    if (hipError_t e = hipMemsetAsync(cst, 0xFF, sizeof(DzChunk) * (size_t)scnt, s); e != hipSuccess)
-                        return e;
-                }
-                hipLaunchKernelGGL(dz_parse, dim3(cnt), dim3(64), 0, s, d_chunks, c0, cnt, D, t, cfg, (u32*)w,
-                                   y.off_m2 / 4, y.off_sym / 4, y.off_pos / 4, y.off_bm / 4, y.off_tail / 4, cst,
-                                   blks, y.nbmax, (const u32*)(w + y.off_prev), c0 - s0);
-            } else {
-                hipLaunchKernelGGL(dz_best, dim3(G), dim3(256), 0, s, d_chunks, c0, D, tot, t, cfg,
-                                   (const u32*)(w + y.off_prev), m2 + (u64)(c0 - s0) * D);
-            }
+            hipLaunchKernelGGL(dz_best, dim3(G), dim3(256), 0, s, d_chunks, c0, D, tot, t, cfg,
+                               (const u32*)(w + y.off_prev), m2 + (u64)(c0 - s0) * D);
         }
         // a parse that does not run leaves every chunk failed, so the kernels
         // after it never read an unset record
-        if (fast || !ZDZ_ONDEMAND) {
-            if (hipError_t e = hipMemsetAsync(cst, 0xFF, sizeof(DzChunk) * (size_t)scnt, s); e != hipSuccess) return e;
-        }
+        if (hipError_t e = hipMemsetAsync(cst, 0xFF, sizeof(DzChunk) * (size_t)scnt, s); e != hipSuccess) return e;
         if (fast) {
-            if (ring)
-                hipLaunchKernelGGL(dz_parse_fast<true>, dim3(scnt), dim3(64), DZF_LDS_RING, s, d_chunks, s0, scnt, D, t,
-                                   cfg, (u32*)w, y.off_m2 / 4, cst, blks, y.nbmax);
-            else
-                hipLaunchKernelGGL(dz_parse_fast<false>, dim3(scnt), dim3(64), DZF_LDS, s, d_chunks, s0, scnt, D, t,
-                                   cfg, (u32*)w, y.off_m2 / 4, cst, blks, y.nbmax);
+            hipLaunchKernelGGL(dz_parse_fast, dim3(scnt), dim3(64), DZF_LDS_RING, s, d_chunks, s0, scnt, D, t, cfg,
+                               (u32*)w, y.off_m2 / 4, cst, blks, y.nbmax);
             if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
-        } else if (!ZDZ_ONDEMAND) {
+        } else {
             hipLaunchKernelGGL(dz_parse, dim3(scnt), dim3(64), 0, s, d_chunks, s0, scnt, D, t, cfg, (u32*)w,
                                y.off_m2 / 4, y.off_sym / 4, y.off_pos / 4, y.off_bm / 4, y.off_tail / 4, cst, blks,
-                               y.nbmax, (const u32*)nullptr, 0u);
+                               y.nbmax);
         }
         const u64 nbk = (u64)scnt * y.nbmax;
         hipLaunchKernelGGL(dz_plan, dim3((u32)nbk), dim3(64), 0, s, scnt, cst, blks, y.nbmax, (const u32*)w, D);

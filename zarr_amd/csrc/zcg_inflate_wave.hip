@@ -59,9 +59,6 @@
 #define ZIW_DBG 0  // 1: debug counters compiled in (ZCG_FLAG_DEBUG_COUNTERS; tools/iw_stats.py cycle
                    // shares).  Out by default: their checks cost 1.4 % of the C2 launch (22.05 -> 21.74 ms)
 #endif
-#ifndef ZIW_NEARX
-#define ZIW_NEARX 1  // near batches: tagged markers (no clear) and a first read that settles final sources
-#endif
 
 namespace zcg {
 
@@ -73,27 +70,6 @@ constexpr u32 IW_SEGMIN = 128;   // bits per lane segment
 constexpr u32 IW_SEGMAX = 4096;
 constexpr u32 IW_K = 4;          // decode steps between staged-token / mark flushes
 constexpr u32 IW_KH = 2;         // flush periods per outer step (reader loads at its top, absorbs at its bottom)
-#ifndef ZIW_BCAST
-#define ZIW_BCAST 1  // wave scans finish with DPP row_bcast:15/31 (0: lane 15/31/47 readlanes and selects)
-#endif
-#ifndef ZIW_S1
-#define ZIW_S1 1  // chain member successors' first tokens shifted into the member's lane once per round
-#endif
-#ifndef ZIW_FARV1
-#define ZIW_FARV1 1  // far tokens: the second 16-byte piece loaded unconditionally
-#endif
-#ifndef ZIW_MUL24
-#define ZIW_MUL24 1  // token-list addresses with the 24-bit multiply
-#endif
-#ifndef ZIW_SCUR
-#define ZIW_SCUR 1  // group cursor walks on scalar registers
-#endif
-#ifndef ZIW_DEC32
-#define ZIW_DEC32 1  // token decode on 32-bit fields (one v_alignbit instead of 64-bit shifts)
-#endif
-#ifndef ZIW_GRB
-#define ZIW_GRB 1  // stream reader: bit cursor + barrel select (0: round-4 shifted 96-bit window)
-#endif
 #ifndef ZIW_G
 #define ZIW_G 4
 #endif
@@ -104,12 +80,8 @@ static_assert(IW_TSTR % 4 == 0 && 64 % IW_G == 0, "list blocks");
 // are interleaved by aligned 4-word blocks, so one flush of those lanes fills
 // whole cache lines ([lane / G][j / 4][lane % G][j % 4]; G = 1: [lane][j])
 __device__ __forceinline__ u32 iw_ta(u32 l, u32 j) {
-#if ZIW_MUL24
     // (< 2^24 operands: the full-rate 24-bit multiply, not the quarter-rate 32-bit one)
     return __umul24(l / IW_G, IW_G * IW_TSTR) + (((j >> 2) * IW_G + (l % IW_G)) << 2) + (j & 3);
-#else
-    return (l / IW_G) * (IW_G * IW_TSTR) + (((j >> 2) * IW_G + (l % IW_G)) << 2) + (j & 3);
-#endif
 }
 constexpr u32 IW_MWIN = 8;                       // mark words a lane keeps in LDS between flushes
 #ifndef ZIW_MARKW
@@ -191,6 +163,7 @@ struct IwLds {
 };
 static_assert(sizeof(IwLds) + 32 <= 10240, "16 chunks per CU");
 static_assert(2 * IW_S + 512 >= sizeof(decltype(IwLds::u)::Hr), "batch markers lie past the H-round scratch");
+static_assert(2 * IW_S + 512 >= sizeof(((IwLds*)nullptr)->u.h), "batch markers lie past the header scratch");
 
 // wave-local ordering point for LDS (and the compiler): a wave's LDS
 // operations are performed in issue order, so a fence at wavefront scope is
@@ -206,18 +179,10 @@ __device__ __forceinline__ u32 iw_incl_scan(u32 v) {
     v += (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
     v += (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
     v += (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
-#if ZIW_BCAST
     // rows -> wave: lane 15 into rows 1 and 3, then lane 31 into rows 2 and 3
     v += (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15
     v += (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
     return v;
-#else
-    const u32 t0 = (u32)__builtin_amdgcn_readlane((int)v, 15);
-    const u32 t1 = t0 + (u32)__builtin_amdgcn_readlane((int)v, 31);
-    const u32 t2 = t1 + (u32)__builtin_amdgcn_readlane((int)v, 47);
-    const u32 lane = (u32)lane_id();
-    return v + (lane < 16 ? 0u : (lane < 32 ? t0 : (lane < 48 ? t1 : t2)));
-#endif
 }
 
 __device__ __forceinline__ u32 iw_wave_sum(u32 v) {
@@ -241,7 +206,6 @@ __device__ __forceinline__ u32 iw_wave_sum(u32 v) {
 // every step; a loop-carried register in flight is copied at the loop header,
 // which waits as well; and a flat (generic) load would also hold every LDS
 // table lookup.
-#if ZIW_GRB
 // Round 5: a bit cursor bp into the 256 bits of A:B instead of a shifted
 // window.  Each step selects the three words from bp >> 5 by a 3-level
 // barrel select (11 selects) and funnel-shifts them (2 v_alignbit), so a
@@ -295,77 +259,6 @@ __device__ __forceinline__ void gr_init(GRd& s, const u8* base, u32 nvec, u32 qa
     s.bp = qa & 127;
     s.lo = 0;
 }
-#else
-struct GRd {
-    u64 lo;
-    u32 hi;
-    u32 nb;
-    u32x4 A, B;
-    u32 wi;  // next word of A:B to append (0..8)
-    u32 vc;  // vector index after B
-};
-
-typedef __attribute__((address_space(1))) u32x4 gu32x4;
-__device__ __forceinline__ u32x4 gr_vec(const u8* base, u32 nvec, u32 v) {
-    const u32 vc = v < nvec ? v : (nvec ? nvec - 1 : 0u);
-    return *(const gu32x4*)((const gu8*)base + 16ull * vc);
-}
-
-__device__ __forceinline__ void gr_word(GRd& s) {
-    const u32x4 X = s.wi < 4 ? s.A : s.B;
-    const u32 k = s.wi & 3;
-    const u32 w = k == 0 ? X.x : k == 1 ? X.y : k == 2 ? X.z : X.w;
-    if (s.nb < 64) {
-        s.lo |= (u64)w << s.nb;
-        s.hi = s.nb > 32 ? w >> (64 - s.nb) : 0u;
-    } else {
-        s.hi = w;
-    }
-    s.nb += 32;
-    s.wi++;
-}
-
-// >= 48 valid bits in lo afterwards (one token's worst case), unless A:B ran
-// dry: then the lane sits out the steps until the next refill
-__device__ __forceinline__ bool gr_fill(GRd& s) {
-    if (s.nb <= 64 && s.wi < 8) gr_word(s);
-    if (s.nb < 48 && s.wi < 8) gr_word(s);
-    return s.nb >= 48;
-}
-
-__device__ __forceinline__ void gr_drop(GRd& s, u32 k) {  // 0 < k <= 48
-    s.lo = (s.lo >> k) | ((u64)s.hi << (64 - k));
-    s.hi = k >= 32 ? 0u : (s.hi >> k);
-    s.nb -= k;
-}
-
-// every lane, wave-uniform, branch-free: C, D = the two vectors after B
-// (loaded at the top of the outer step) replace the used-up vectors of A:B
-__device__ __forceinline__ void gr_absorb(GRd& s, const u32x4& C, const u32x4& D) {
-    const u32 sh = s.wi >= 8 ? 2u : s.wi >= 4 ? 1u : 0u;
-    s.A = sh == 2 ? C : sh == 1 ? s.B : s.A;
-    s.B = sh == 2 ? D : sh == 1 ? C : s.B;
-    s.vc += sh;
-    s.wi -= 4 * sh;
-}
-
-// qa = bit position relative to base (every lane; waits for its first vectors)
-__device__ __forceinline__ void gr_init(GRd& s, const u8* base, u32 nvec, u32 qa) {
-    const u32 v0 = qa >> 7;
-    s.A = gr_vec(base, nvec, v0);
-    s.B = gr_vec(base, nvec, v0 + 1);
-    s.vc = v0 + 2;
-    s.wi = (qa >> 5) & 3;
-    s.lo = 0;
-    s.hi = 0;
-    s.nb = 0;
-    gr_word(s);
-    gr_word(s);
-    gr_word(s);
-    const u32 k = qa & 31;
-    if (k) gr_drop(s, k);
-}
-#endif
 
 // Decode one token from >= 48 valid bits: both table lookups always run, so
 // lanes holding different token kinds do not serialise.
@@ -375,7 +268,6 @@ __device__ __forceinline__ u32 iw_decode(const IwLds& L, u64 v, u32* adv) {
         e = L.ltab[(e & 0xFFFF) + (((u32)v >> W_LB) & ((1u << ((e >> 16) & 0xFF)) - 1))];
     const u32 l = e >> 28, kind = (e >> 24) & 15, ex = (e >> 16) & 0xFF;
     const u32 t = l + ex;
-#if ZIW_DEC32
     // 32-bit fields only: the length code and its extra bits end by bit 20,
     // and the distance code and its extra bits take <= 28 bits from t
     const u32 vd = __builtin_amdgcn_alignbit((u32)(v >> 32), (u32)v, t);
@@ -385,15 +277,6 @@ __device__ __forceinline__ u32 iw_decode(const IwLds& L, u64 v, u32* adv) {
     const u32 dl = de >> 28, dex = (de >> 16) & 0xFF;
     const u32 len = (e & 0xFFFF) + (((u32)v >> l) & ((1u << ex) - 1));
     const u32 dist = (de & 0xFFFF) + ((vd >> dl) & ((1u << dex) - 1));
-#else
-    const u64 vd = v >> t;
-    u32 de = L.dtab[(u32)vd & ((1u << W_DB) - 1)];
-    if (((de >> 24) & 15) == K_SUB)
-        de = L.dtab[(de & 0xFFFF) + (((u32)vd >> W_DB) & ((1u << ((de >> 16) & 0xFF)) - 1))];
-    const u32 dl = de >> 28, dex = (de >> 16) & 0xFF;
-    const u32 len = (e & 0xFFFF) + ((u32)(v >> l) & ((1u << ex) - 1));
-    const u32 dist = (de & 0xFFFF) + ((u32)(vd >> dl) & ((1u << dex) - 1));
-#endif
     const u32 madv = t + dl + dex;
     const bool dok = ((de >> 24) & 15) == K_DIST;
     u32 a = l ? l : 1;
@@ -410,6 +293,15 @@ __device__ __forceinline__ u32 iw_decode(const IwLds& L, u64 v, u32* adv) {
 
 typedef __attribute__((address_space(1))) u32x4 gu32x4_a4 __attribute__((aligned(4)));
 typedef __attribute__((address_space(1))) u32x4 gu32x4_a16 __attribute__((aligned(16)));
+typedef __attribute__((address_space(1))) u64 gu64_ua __attribute__((aligned(1)));
+// LDS stores at 2-byte alignment (gfx950 DS accepts unaligned addresses:
+// tools/probe/lds_unaligned.hip)
+typedef u32x4 u32x4_l2 __attribute__((aligned(2)));
+typedef u32 __attribute__((ext_vector_type(2))) u32x2_l2 __attribute__((aligned(2)));
+typedef u32 u32_l2 __attribute__((aligned(2)));
+// two source bytes (0-1 / 2-3 of w) as two final stage entries
+__device__ __forceinline__ u32 ie_lo(u32 w) { return __builtin_amdgcn_perm(0xFFFFFFFFu, w, 0x04010400u); }
+__device__ __forceinline__ u32 ie_hi(u32 w) { return __builtin_amdgcn_perm(0xFFFFFFFFu, w, 0x04030402u); }
 
 // tokens of a lane's list that start before word wi of its bitmap, plus the
 // marks in `part` (the bits of word wi below the position)
@@ -430,13 +322,17 @@ __device__ __forceinline__ u32 iw_pos(const gu32* gl, u32 lm, u32 j, u32 seg0) {
 
 // Flush resolved stage bytes [from, to) to dst (byte-order transform fused,
 // bool deferred to the end of the chunk: the committed bytes are the window).
+// The stage starting at output position S holds position q at ring entry
+// q - (S & ~15): 16-byte-aligned output pieces are 16-entry-aligned in the
+// ring, and a stage of at most IW_S - 16 bytes never wraps.
 __device__ void iw_commit(IwLds& L, u8* dst, u64 from, u64 to, DType t) {
     const u32 lane = (u32)lane_id();
     wsync();
+    const u64 base = from & ~15ull;
     const u64 a16 = (from + 15) & ~15ull, b16 = to & ~15ull;
     if (a16 < b16) {
         for (u64 p = a16 + (u64)lane * 16; p < b16; p += 64 * 16) {
-            const u32 i = (u32)(p & (IW_S - 1));
+            const u32 i = (u32)(p - base);
             const u32x4 lo = *(const u32x4*)(L.u.st.ptr + i);
             const u32x4 hi = *(const u32x4*)(L.u.st.ptr + i + 8);
             auto pk = [](u32 a, u32 b) -> u32 { return __builtin_amdgcn_perm(b, a, 0x06040200u); };
@@ -445,9 +341,9 @@ __device__ void iw_commit(IwLds& L, u8* dst, u64 from, u64 to, DType t) {
         }
     }
     const u64 e0 = a16 < b16 ? a16 : to;
-    for (u64 q = from + lane; q < e0; q += 64) dst[swap_pos(q, t)] = (u8)L.u.st.ptr[q & (IW_S - 1)];
+    for (u64 q = from + lane; q < e0; q += 64) dst[swap_pos(q, t)] = (u8)L.u.st.ptr[q - base];
     if (a16 < b16)
-        for (u64 q = b16 + lane; q < to; q += 64) dst[swap_pos(q, t)] = (u8)L.u.st.ptr[q & (IW_S - 1)];
+        for (u64 q = b16 + lane; q < to; q += 64) dst[swap_pos(q, t)] = (u8)L.u.st.ptr[q - base];
     // the next stage's far reads come back through this CU's L1/L2: wait
     // for the stores (same-CU stores refresh the L1)
     __syncthreads();
@@ -484,17 +380,9 @@ __device__ __forceinline__ int iw_incl_max(int v) {
     v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x112, 0xf, 0xf, false));  // row_shr:2
     v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x114, 0xf, 0xf, false));  // row_shr:4
     v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x118, 0xf, 0xf, false));  // row_shr:8
-#if ZIW_BCAST
     v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x142, 0xa, 0xf, false));  // row_bcast:15
     v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x143, 0xc, 0xf, false));  // row_bcast:31
     return v;
-#else
-    const int t0 = __builtin_amdgcn_readlane(v, 15);
-    const int t1 = max(t0, __builtin_amdgcn_readlane(v, 31));
-    const int t2 = max(t1, __builtin_amdgcn_readlane(v, 47));
-    const u32 lane = (u32)lane_id();
-    return lane < 16 ? v : max(v, lane < 32 ? t0 : (lane < 48 ? t1 : t2));
-#endif
 }
 
 __device__ __forceinline__ u32 swap_pos32(u32 p, const DType& t) {
@@ -528,7 +416,7 @@ __device__ __attribute__((always_inline)) int read_dynamic_wave(BitIn& b, u8* le
         const u64 by = wb + 8ull * lane;
         u64 w = 0;
         if (by + 8 <= nbytes) {
-            w = *(const __attribute__((address_space(1))) u64 __attribute__((aligned(1)))*)(src + by);
+            w = *(const gu64_ua*)(src + by);
         } else {
             for (u32 k = 0; k < 8; k++)
                 if (by + k < nbytes) w |= (u64)src[by + k] << (8 * k);
@@ -542,7 +430,7 @@ __device__ __attribute__((always_inline)) int read_dynamic_wave(BitIn& b, u8* le
     auto bits32 = [&](u64 q) -> u32 {
         const u32 r = (u32)(q - 8 * wb);
         const u32 wi = r >> 5;
-        if (wi + 1 < 130) {
+        if (wi + 1 < 128) {  // (hwin[128..129] are padding, not stream bytes)
             const u64 x = ((u64)hwin[wi + 1] << 32) | hwin[wi];
             return (u32)(x >> (r & 31));
         }
@@ -694,7 +582,7 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
     int r = R_OK;
     u32 est = IW_EST0;
     L.u.st.mk[lane] = 0;  // batch tags start at 1
-    u32 ntag = 0;
+    u32 ntag = (vflags & ZCG_FLAG_DEBUG_TAG_WRAP) ? 0xFFFFF0u : 0u;  // (tests: wrap within the first batches)
     if (dbg) {
         if (lane < IW_NDBG) L.dbgc[lane] = 0;
         wsync();
@@ -722,11 +610,11 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
             u32 done = 0;
             while (done < slen && P < D) {
                 u32 k = slen - done;
-                if (k > IW_S) k = IW_S;
+                if (k > IW_S - 16) k = IW_S - 16;
                 if ((u64)k > D - P) k = (u32)(D - P);
                 if (in0 + k > n_ds) { r = R_EXHAUSTED; break; }
                 wsync();
-                for (u32 i = lane; i < k; i += 64) L.u.st.ptr[(P + i) & (IW_S - 1)] = (u16)(IE_VAL | ds[in0 + i]);
+                for (u32 i = lane; i < k; i += 64) L.u.st.ptr[(P & 15) + i] = (u16)(IE_VAL | ds[in0 + i]);
                 iw_commit(L, dst, P, P + k, tw);
                 P += k; in0 += k; done += k;
             }
@@ -924,16 +812,11 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
             // lane's token at the cursor + lane (a member's list may end inside a group)
             auto mL = [&](u32 m) -> u32 { return (u32)__builtin_amdgcn_readlane((int)chL, (int)m); };
             auto mE = [&](u32 m) -> u32 { return (u32)__builtin_amdgcn_readlane((int)chE, (int)m); };
-#if ZIW_S1
             // member m's successor's first valid token, in lane m (0 past the chain)
             const u32 chSn = (u32)__shfl_down((int)chS, 1, 64);  // (every lane: a lane reads an active lane)
             const u32 chS1 = lane + 1 < ncm ? chSn : 0u;
             auto mS1 = [&](u32 m) -> u32 { return (u32)__builtin_amdgcn_readlane((int)chS1, (int)m); };
-#else
-            auto mS1 = [&](u32 m) -> u32 { return m + 1 < ncm ? (u32)__builtin_amdgcn_readlane((int)chS, (int)(m + 1)) : 0u; };
-#endif
             auto advance = [&](u32& cm0, u32& cj0, u32 k) {
-#if ZIW_SCUR
                 // (wave-uniform: kept in scalar registers)
                 u32 m = (u32)__builtin_amdgcn_readfirstlane((int)cm0), j = (u32)__builtin_amdgcn_readfirstlane((int)(cj0 + k));
                 while (m < ncm) {
@@ -944,15 +827,6 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
                 }
                 cm0 = m;
                 cj0 = j;
-#else
-                cj0 += k;
-                while (cm0 < ncm) {
-                    const u32 e = mE(cm0);
-                    if (cj0 < e) break;
-                    cj0 = cj0 - e + mS1(cm0);
-                    cm0++;
-                }
-#endif
             };
             // The token words of the next IW_GK groups are in flight while a
             // group is placed (the lists sit in MALL/HBM: ~2 K cycles away).
@@ -971,11 +845,7 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
             // register, even a select, waits for it.
             auto fetch2 = [&](u32 cm0, u32 cj0, u32& ta, u32& tb, u32& ok) {
                 u32 ja = cj0 + 2 * lane, jb = ja + 1, la = 0xFFFFFFFFu, lb = 0xFFFFFFFFu, pa = 0, pb = 0;
-#if ZIW_SCUR
                 for (u32 m = (u32)__builtin_amdgcn_readfirstlane((int)cm0); m < ncm; m++) {
-#else
-                for (u32 m = cm0; m < ncm; m++) {
-#endif
                     const u32 e = mE(m), ln = mL(m), s1 = mS1(m);
                     if (la == 0xFFFFFFFFu && ja < e) { la = ln; pa = ja; }
                     if (lb == 0xFFFFFFFFu && jb < e) { lb = ln; pb = jb; }
@@ -1005,7 +875,7 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
             while (!round_done && r == R_OK) {
                 const u64 S = P;
                 const u64 room = D - P;
-                const u32 capS = IW_S;
+                const u32 capS = IW_S - 16;  // (S & 15) + cap <= IW_S: the stage never wraps the ring
                 const u32 cap = room < capS ? (u32)room : capS;
                 const bool fin = (u64)cap == room;
                 // Token-granular stage.  The ring is cleared, then every kept
@@ -1031,6 +901,7 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
                 // a far token ends before S + 16 <= D
                 const bool wide_ok = !tw.swap && room >= 16;
                 const u32 S32 = (u32)S;  // (D < 2^32)
+                const u32 s0 = S32 & 15u;  // ring entry of the stage's first byte
                 struct Tk {
                     u32 kind, o, L, d;  // kind 0 none, 1 literal (d = byte), 2 far, 3 near; L clipped at cap
                 };
@@ -1050,9 +921,8 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
                     }
                     t.L = (fin && o + len > cap) ? cap - o : len;
                     t.d = d;
-                    // far: the whole source lies before the stage, and the first
-                    // piece (from the aligned quad before the token) is in the output
-                    t.kind = (wide_ok && o + len <= d && S32 + o - d >= 3u) ? 2u : 3u;
+                    // far: the whole source lies before the stage
+                    t.kind = (wide_ok && o + len <= d) ? 2u : 3u;
                     return t;
                 };
                 auto group2 = [&](u32& tqa, u32& tqb, u32& okq) -> bool {
@@ -1073,22 +943,23 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
                     const u32 ntk = (u32)__popcll(__ballot(ka)) + (u32)__popcll(__ballot(kb));
                     IW_T(IWT_PLACE);
                     const Tk A = classify(ta, oa, la, ka), B = classify(tb, ob, lb, kb);
-                    if (A.kind == 1u) L.u.st.ptr[(S32 + A.o) & (IW_S - 1)] = (u16)(IE_VAL | A.d);
-                    if (B.kind == 1u) L.u.st.ptr[(S32 + B.o) & (IW_S - 1)] = (u16)(IE_VAL | B.d);
+                    if (A.kind == 1u) L.u.st.ptr[s0 + A.o] = (u16)(IE_VAL | A.d);
+                    if (B.kind == 1u) L.u.st.ptr[s0 + B.o] = (u16)(IE_VAL | B.d);
                     IW_T(IWT_CLASSIFY);
                     // far tokens, compacted one per lane (rank in token order):
-                    // 16-byte source pieces from the aligned quad before the
-                    // token, one quad of entries OR-ed per source dword (entries
-                    // outside the token OR-ed as zero)
+                    // 16-byte source pieces from the token's first source byte,
+                    // widened to entries by v_perm and stored exactly with
+                    // unaligned ds_write_b128 (8 entries; a token's last < 8
+                    // entries by b64 / b32 / b16), so tokens never share a store
                     {
                         const bool fA = A.kind == 2u, fB = B.kind == 2u;
                         const u64 bA = __ballot(fA), bB = __ballot(fB);
                         const u64 below = (1ull << lane) - 1ull;
                         const u32 rkA = (u32)__popcll(bA & below) + (u32)__popcll(bB & below), rkB = rkA + (fA ? 1u : 0u);
                         const u32 NF = (u32)__popcll(bA) + (u32)__popcll(bB);
+                        // source byte | (ring entry of the first byte | length << 16) << 32
                         auto fdesc = [&](const Tk& t) -> u64 {
-                            const u32 y = S32 + t.o, r = y & 3u;
-                            return (u64)(y - t.d - r) | ((u64)(((y - r) & (IW_S - 1)) | (r << 11) | (t.L << 16)) << 32);
+                            return (u64)(S32 + t.o - t.d) | ((u64)((s0 + t.o) | (t.L << 16)) << 32);
                         };
                         for (u32 f0 = 0; f0 < NF; f0 += 64) {
                             if (fA && rkA - f0 < 64u) L.u.st.fd[rkA - f0] = fdesc(A);
@@ -1097,32 +968,30 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
                             if (f0 + lane < NF) {
                                 const u64 fdw = L.u.st.fd[lane];
                                 const u32 src = (u32)fdw, hi = (u32)(fdw >> 32);
-                                const u32 qb = hi & (IW_S - 1), r = (hi >> 11) & 3u, e = r + (hi >> 16);
+                                const u32 qi = hi & 0xFFFFu, e = hi >> 16;
                                 const u32 np = (e + 15) >> 4;
                                 const u32x4 V0 = *(const gu32x4_ua*)(gd + src);
-#if ZIW_FARV1
                                 // unconditional (a second read of the first piece when
                                 // there is one piece): a load kept under a branch waited
                                 // for the first one before issuing
                                 const u32x4 V1 = *(const gu32x4_ua*)(gd + src + (np > 1 ? 16u : 0u));
-#else
-                                u32x4 V1 = V0;
-                                if (np > 1) V1 = *(const gu32x4_ua*)(gd + src + 16);
-#endif
-                                auto piece = [&](const u32x4& V, u32 p) {
-#pragma unroll
-                                    for (u32 q = 0; q < 4; q++) {
-                                        const u32 K = 4 * p + q;
-                                        const int bq = (int)e - 4 * (int)K;
-                                        if (bq > 0) {
-                                            const u32 w = q == 0 ? V.x : q == 1 ? V.y : q == 2 ? V.z : V.w;
-                                            u64 m = bq >= 4 ? ~0ull : ((1ull << (16 * bq)) - 1ull);
-                                            if (K == 0) m &= ~0ull << (16 * r);
-                                            const u64 val = ((u64)__builtin_amdgcn_perm(0xFFFFFFFFu, w, 0x04030402u) << 32) |
-                                                            (u64)__builtin_amdgcn_perm(0xFFFFFFFFu, w, 0x04010400u);
-                                            atomicOr((unsigned long long*)(L.u.st.ptr + ((qb + 4 * K) & (IW_S - 1))), val & m);
-                                        }
+                                // n (1..8) entries at ring entry k from source bytes w0:w1
+                                auto put = [&](u32 k, u32 n, u32 w0, u32 w1) {
+                                    u16* pe = L.u.st.ptr + k;
+                                    if (n >= 8) {
+                                        *(u32x4_l2*)pe = u32x4{ie_lo(w0), ie_hi(w0), ie_lo(w1), ie_hi(w1)};
+                                        return;
                                     }
+                                    if (n & 4u) *(u32x2_l2*)pe = u32x2{ie_lo(w0), ie_hi(w0)};
+                                    const u32 rw = (n & 4u) ? w1 : w0;
+                                    u16* pt = pe + (n & 4u);
+                                    if (n & 2u) *(u32_l2*)pt = ie_lo(rw);
+                                    if (n & 1u) pt[n & 2u] = (u16)(IE_VAL | (((n & 2u) ? rw >> 16 : rw) & 0xFFu));
+                                };
+                                auto piece = [&](const u32x4& V, u32 p) {
+                                    const u32 b0 = 16 * p;  // < e
+                                    put(qi + b0, e - b0, V.x, V.y);
+                                    if (e > b0 + 8) put(qi + b0 + 8, e - b0 - 8, V.z, V.w);
                                 };
                                 piece(V0, 0);
                                 if (np > 1) piece(V1, 1);
@@ -1148,21 +1017,17 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
                     // byte n0 + i; its token is the last one whose first byte in
                     // the batch is at or before it (marker + max scan)
                     for (u32 n0 = 0; n0 < NB; n0 += 64) {
-#if ZIW_NEARX
-                        const u32 tag = ++ntag << 8;
+                        if ((++ntag & 0xFFFFFFu) == 0) {  // 24-bit tags wrapped: forget every older marker
+                            L.u.st.mk[lane] = 0;
+                            wsync();
+                            ntag = 1;
+                        }
+                        const u32 tag = ntag << 8;
                         if (nla && na < n0 + 64 && na + nla > n0) L.u.st.mk[na > n0 ? na - n0 : 0u] = tag | (ia + 1);
                         if (nlb && nb < n0 + 64 && nb + nlb > n0) L.u.st.mk[nb > n0 ? nb - n0 : 0u] = tag | (ib + 1);
                         wsync();
                         const u32 mv = L.u.st.mk[lane];
                         const int tid = iw_incl_max((mv & ~0xFFu) == tag ? (int)(mv & 0xFFu) : 0) - 1;
-#else
-                        L.u.st.mk[lane] = 0;
-                        wsync();
-                        if (nla && na < n0 + 64 && na + nla > n0) L.u.st.mk[na > n0 ? na - n0 : 0u] = (u8)(ia + 1);
-                        if (nlb && nb < n0 + 64 && nb + nlb > n0) L.u.st.mk[nb > n0 ? nb - n0 : 0u] = (u8)(ib + 1);
-                        wsync();
-                        const int tid = iw_incl_max((int)L.u.st.mk[lane]) - 1;
-#endif
                         const u32 i = n0 + lane;
                         bool done = i >= NB, strad = false;
                         u32 pos = 0, cur = 0;
@@ -1170,11 +1035,10 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
                             const u32 dsc = L.u.st.desc[tid];
                             const u32 p = (dsc & 0xFFFFu) + i;
                             const u32 d = dsc >> 16;
-                            pos = (S32 + p) & (IW_S - 1);
-                            if (p >= d) cur = (S32 + p - d) & (IW_S - 1);
+                            pos = s0 + p;
+                            if (p >= d) cur = s0 + p - d;
                             else cur = IE_VAL | (u32)gd[swap_pos32(S32 + p - d, tw)];  // before the stage
                             strad = p < d;
-#if ZIW_NEARX
                             // a source that is already final settles the byte now: the
                             // read precedes this batch's writes, and an entry of this
                             // batch still reads as a pointer (zero or older), so only
@@ -1183,10 +1047,6 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
                             done = v0 >= IE_VAL;
                             if (done) cur = v0;
                             L.u.st.ptr[pos] = (u16)cur;
-#else
-                            L.u.st.ptr[pos] = (u16)cur;
-                            done = cur >= IE_VAL;
-#endif
                         }
                         wsync();
                         IW_ADD(IWD_NBATCH, 1);

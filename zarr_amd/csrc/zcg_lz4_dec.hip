@@ -754,6 +754,8 @@ constexpr u32 LZ_LWG = 64;          // lanes per workgroup of the lane kernel
 #ifndef LZ_LPW_THRESH
 #define LZ_LPW_THRESH 262144
 #endif
+static_assert(LZ_LPW_SMALL >= 1 && LZ_LPW_SMALL <= LZ_LWG && LZ_LPW_CORUN >= 1 && LZ_LPW_CORUN <= LZ_LWG,
+              "blocks per wave: the lane kernel launches LZ_LWG lanes per workgroup");
 constexpr u64 LZ_LANE_MIN_BLOCKS = 131072;
 // From 131 072 blocks (measured at 8 192 C4 chunks: lanes 50.6 ms, waves 54.3
 // ms, 55 % lanes + 45 % waves side by side 45.0 ms) both kernels run at once on
@@ -1168,7 +1170,8 @@ hipError_t launch_lz4_decode(const zcg_array* a, const zcg_chunk* d_chunks, uint
 }
 
 const char* cfg_lz4_dec() {
-    return "lz4_dec:CORUN=" ZCG_STR(LZ_CORUN_PCT) "/" ZCG_STR(LZ_CORUN_LO) "/" ZCG_STR(LZ_CORUN_HI);
+    return "lz4_dec:CORUN=" ZCG_STR(LZ_CORUN_PCT) "/" ZCG_STR(LZ_CORUN_LO) "/" ZCG_STR(LZ_CORUN_HI) ",LPW="
+        ZCG_STR(LZ_LPW_SMALL) "/" ZCG_STR(LZ_LPW_CORUN) "/" ZCG_STR(LZ_LPW_THRESH);
 }
 
 }  // namespace zcg

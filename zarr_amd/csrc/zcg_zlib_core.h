@@ -86,10 +86,6 @@ ZZ_INL Config level_config(int level) {
     }
 }
 
-#ifndef ZZ_PIPE_LINKS
-#define ZZ_PIPE_LINKS 1
-#endif
-
 ZZ_INL uint32_t hash3(uint32_t b0, uint32_t b1, uint32_t b2) { return ((b0 << 10) ^ (b1 << 5) ^ b2) & 0x7FFFu; }
 
 // Window slides fill_window has done by the loop top at q (input fully
@@ -127,19 +123,12 @@ ZZ_FN Match2 search(uint32_t p, uint32_t D, const Config& cfg, const BYTE4& byte
     bool red_done = false;
     // the next link is read as soon as a candidate is known, so on the GPU
     // its load is in flight together with the candidate's byte loads
-#if ZZ_PIPE_LINKS
     uint32_t cn = prev(c);
-#endif
     for (uint32_t k = 0; k < cfg.chain; k++) {
         if (k > 0) {
-#if ZZ_PIPE_LINKS
             c = cn;
             if (c == NONE || c <= lim) break;
             cn = prev(c);
-#else
-            c = prev(c);
-            if (c == NONE || c <= lim) break;
-#endif
         }
         // a candidate beats best only if bytes 0..best all match: the four
         // ending at best are checked first (zlib's scan_end test, widened)
