@@ -105,10 +105,6 @@ enum zcg_status {
  * ended by an empty stored block; the stream inflates to the same data, but
  * its bytes differ from zlib's).  Level 0 always uses the segmented coder. */
 #define ZCG_FLAG_GZIP_SEGMENTED 0x8000u
-/* Test hook: the inflate wave kernel starts its 24-bit near-batch marker
- * tags just below the wrap, so the wrap path runs within the first batches
- * of every chunk (the decoded bytes are the same). */
-#define ZCG_FLAG_DEBUG_TAG_WRAP 0x10000u
 
 /* CompressionType + its configuration (camelCase JSON keys in the reference). */
 typedef struct zcg_compression {

@@ -223,17 +223,15 @@ def test_gzip_large(data, variant):
 
 
 @pytest.mark.parametrize("data", ["zeros", "text_like", "quant_f4", "randwalk_i2"])
-def test_inflate_wave_near_tag_wrap(data):
-    """The wave kernel tags its near-batch markers with a 24-bit counter
-    (zcg_inflate_wave.hip); when it wraps, every older marker is cleared.
-    ZCG_FLAG_DEBUG_TAG_WRAP starts the counter 16 below the wrap, so the wrap
-    runs in the first batches of each chunk; the bytes must not change."""
-    from zarr_amd._native import FLAG_DEBUG_TAG_WRAP
+def test_inflate_wave_near_batches(data):
+    """The wave kernel resolves near bytes in batches of 64 whose markers are
+    cleared per batch (no tag that could wrap): long near runs
+    (zeros: 258-byte dist-1 matches), short-period repeats (text) and the C2
+    data decode to the input."""
     payload = DATASETS[data]()
     st, s = zref.encode(zref.GZIP, 6, np.frombuffer(payload, np.uint8))
     assert st == 0
-    for flags in (FLAG_INFLATE_WAVE, FLAG_INFLATE_WAVE | FLAG_DEBUG_TAG_WRAP):
-        assert gpu_decode("gzip", s, "u1", len(payload), flags=flags) == ("Ok", payload), flags
+    assert gpu_decode("gzip", s, "u1", len(payload), flags=FLAG_INFLATE_WAVE) == ("Ok", payload)
 
 
 @pytest.mark.parametrize("dt", ["<i2", ">i2", ">f4", ">u8", "bool"])

@@ -67,10 +67,10 @@ fn(out.ctypes.data, 1)
 names = {0: "rounds", 1: "blocks", 2: "stages", 3: "groups", 4: "p1_lane_it", 5: "p2_lane_it", 6: "chain",
          7: "spare", 8: "caps", 9: "rounds_no_eob", 10: "cyc_hdr", 11: "cyc_p1", 12: "cyc_p2",
          13: "cyc_chain", 14: "cyc_classify", 15: "cyc_far", 16: "cyc_near", 17: "cyc_place", 18: "cyc_commit",
-         19: "cyc_total", 20: "far_iters", 21: "near_batches", 22: "near_passes", 23: "near_straddle_batches", 24: "cyc_hdr_tables"}
+         19: "cyc_total", 20: "far_iters", 21: "near_batches", 22: "near_passes", 23: "near_straddle_batches", 24: "cyc_hdr_tables", 25: "cyc_refetch", 26: "cyc_eob", 27: "cyc_hdr_walk"}
 d = {v: int(out[k]) for k, v in names.items()}
 res["per_chunk"] = {k: round(v / packed.n, 1) for k, v in d.items()}
-cyc = {k: v for k, v in d.items() if k.startswith("cyc_") and k not in ("cyc_total", "cyc_hdr_tables")}
+cyc = {k: v for k, v in d.items() if k.startswith("cyc_") and k not in ("cyc_total", "cyc_hdr_tables", "cyc_hdr_walk")}
 tot = max(1, sum(cyc.values()))
 res["cycle_share"] = {k: round(v / tot, 3) for k, v in cyc.items()}
 res["kcyc_per_chunk_total"] = round(d["cyc_total"] / packed.n / 1e3, 1)

@@ -23,7 +23,6 @@ FLAG_SERIAL_INFLATE = 0x100
 FLAG_DEBUG_COUNTERS = 0x200
 FLAG_INFLATE_BLOCK_PAR = 0x2000
 FLAG_INFLATE_WAVE = 0x4000
-FLAG_DEBUG_TAG_WRAP = 0x10000  # test hook: near-batch marker tags start just below their 24-bit wrap
 
 STATUS_NAMES = {OK: "Ok", UNEXPECTED_EOF: "UnexpectedEof", INVALID_DATA: "InvalidData",
                 INVALID_INPUT: "InvalidInput", UNSUPPORTED: "Unsupported",

@@ -789,7 +789,7 @@ struct DzChunk {
 struct DzLayout {
     u32 m, sb, nbmax;
     u64 tot, cub_bytes, outcap;
-    u64 off_ka, off_kb, off_va, off_vb, off_prev, off_cub, off_m2, off_sym, off_pos, off_bm, off_tail, off_ch, off_blk,
+    u64 off_ka, off_kb, off_va, off_vb, off_cub, off_m2, off_sym, off_pos, off_bm, off_tail, off_ch, off_blk,
         off_out, total;
 };
 
@@ -818,7 +818,6 @@ DzLayout dz_layout(u64 D, u32 n) {
     y.off_kb = take(4 * y.tot);
     y.off_va = take(4 * y.tot);
     y.off_vb = take(4 * y.tot);
-    y.off_prev = take(4 * y.tot);
     y.off_cub = take(y.cub_bytes);
     y.off_m2 = take(8 * (u64)y.sb * D + 4096);   // match results; then the final symbols + positions
     y.off_sym = take(4 * (u64)y.sb * D + 4096);  // per-segment symbols (pass 1)
@@ -850,33 +849,43 @@ __global__ void dz_keys(const zcg_chunk* __restrict__ chunks, u32 c0, u64 D, u64
     vals[g] = (u32)g;
 }
 
-__global__ void dz_chain(u64 tot, const u32* __restrict__ keys, const u32* __restrict__ vals,
-                         u32* __restrict__ prev) {
+// zz::search at every position of the sub-batch: m2[g] = {full, red}, one
+// thread per position in the ORDER OF THE SORTED KEYS.  The stable sort of
+// (chunk, hash) with ascending positions lays every hash chain out
+// contiguously: position vals[j]'s chain is vals[j-1], vals[j-2], ... while
+// the key stays the same -- exactly zlib's prev[] walk -- so a candidate is a
+// coalesced load at a known index instead of a dependent load of prev[c] at
+// a random address, and neighbouring threads walk overlapping candidate
+// lists (their byte loads hit the same lines).  The result is scattered back
+// to m2[vals[j]].
+// (An LDS-staged variant of the prev[] walk -- each workgroup's 40 KB search
+// window of bytes and u16 chain links in LDS -- measured slower: 48.9 vs
+// 45.2 ms per 128 C5 chunks.)
+__global__ void dz_best(const zcg_chunk* __restrict__ chunks, u32 c0, u64 D, u64 tot, DType t, zz::Config cfg,
+                        const u32* __restrict__ keys, const u32* __restrict__ vals, uint2* __restrict__ m2) {
     const u64 j = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= tot) return;
-    prev[vals[j]] = (j > 0 && keys[j] == keys[j - 1]) ? vals[j - 1] : 0xFFFFFFFFu;
-}
-
-// zz::search at every position of the sub-batch: m2[g] = {full, red}.
-// (An LDS-staged variant -- each workgroup's 40 KB search window of bytes and
-// u16 chain links in LDS -- measured slower: 48.9 vs 45.2 ms per 128 C5
-// chunks, one 122 KB workgroup per CU could not hide its fill.)
-__global__ void dz_best(const zcg_chunk* __restrict__ chunks, u32 c0, u64 D, u64 tot, DType t, zz::Config cfg,
-                        const u32* __restrict__ prev, uint2* __restrict__ m2) {
-    const u64 g = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= tot) return;
+    const u32 kj = keys[j];
+    const u32 g = vals[j];
     const u32 cl = (u32)(g / D);
     const u32 p = (u32)(g - (u64)cl * D);
     zz::Match2 r{0u, 0u};
     const zcg_chunk ch = chunks[c0 + cl];
-    if (ch.src_len >= D) {
+    if (ch.src_len >= D && (kj & 0x8000u) == 0) {
         const u8* src = (const u8*)ch.src;
-        const u64 cbase = (u64)cl * D;
+        const u32 cbase = (u32)((u64)cl * D);
         auto b1 = [&](u32 i) -> u32 { return df_ser1(src, i, t); };
         auto b4 = [&](u32 i) -> u32 { return df_ser4(src, i, t); };
-        auto pv = [&](u32 i) -> u32 {
-            const u32 q = prev[cbase + i];
-            return q == 0xFFFFFFFFu ? zz::NONE : (u32)(q - cbase);
+        // zz::search asks for the chain in order (the head p, then each
+        // candidate once): the next entry of the sorted run, NONE past it
+        u64 jj = j;
+        auto pv = [&](u32) -> u32 {
+            if (jj == 0 || keys[jj - 1] != kj) {
+                jj = 0;
+                return zz::NONE;
+            }
+            jj--;
+            return vals[jj] - cbase;
         };
         r = zz::search(p, (u32)D, cfg, b4, b1, pv);
     }
@@ -1611,10 +1620,8 @@ static hipError_t launch_deflate_exact(const zcg_array* a, const zcg_chunk* d_ch
             hipError_t e = hipcub::DeviceRadixSort::SortPairs(w + y.off_cub, cb, dk, dv, (int)tot, 0,
                                                               (int)(16 + cbits), s);
             if (e != hipSuccess) return e;
-            hipLaunchKernelGGL(dz_chain, dim3(G), dim3(256), 0, s, tot, dk.Current(), dv.Current(),
-                               (u32*)(w + y.off_prev));
             hipLaunchKernelGGL(dz_best, dim3(G), dim3(256), 0, s, d_chunks, c0, D, tot, t, cfg,
-                               (const u32*)(w + y.off_prev), m2 + (u64)(c0 - s0) * D);
+                               (const u32*)dk.Current(), (const u32*)dv.Current(), m2 + (u64)(c0 - s0) * D);
         }
         // a parse that does not run leaves every chunk failed, so the kernels
         // after it never read an unset record

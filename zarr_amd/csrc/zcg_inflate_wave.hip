@@ -38,6 +38,7 @@
 // (zcg_inflate.hip) and the 256-lane round kernel (zcg_inflate_par.hip);
 // tests/ compare all three against the oracle.
 #include <climits>
+#include <type_traits>
 
 #include "zcg_inflate_common.h"
 
@@ -84,6 +85,7 @@ __device__ __forceinline__ u32 iw_ta(u32 l, u32 j) {
     return __umul24(l / IW_G, IW_G * IW_TSTR) + (((j >> 2) * IW_G + (l % IW_G)) << 2) + (j & 3);
 }
 constexpr u32 IW_MWIN = 8;                       // mark words a lane keeps in LDS between flushes
+constexpr u32 IW_EMW = 2;                        // a segment's first mark words kept in LDS for pass 2
 #ifndef ZIW_MARKW
 #define ZIW_MARKW 32
 #endif
@@ -125,12 +127,12 @@ constexpr u32 W_LCAP = 852;
 constexpr int W_DB = 8;
 constexpr u32 W_DCAP = 432;  // >= enough(30, 8, 15) = 402
 
-constexpr u32 IW_NDBG = 26;
+constexpr u32 IW_NDBG = 28;
 __device__ unsigned long long g_iw_dbg[32];
 enum { IWD_ROUNDS, IWD_BLOCKS, IWD_STAGES, IWD_GROUPS, IWD_P1_IT, IWD_P2_IT, IWD_CHAIN, IWD_SPARE7, IWD_CAPS,
        IWD_NOEOB, IWT_HDR, IWT_P1, IWT_P2, IWT_CHAIN, IWT_CLASSIFY, IWT_FAR, IWT_NEAR, IWT_PLACE,
-       IWT_COMMIT, IWT_TOTAL, IWD_FARIT, IWD_NBATCH, IWD_NPASS, IWD_NSTRAD, IWT_HTAB };
-static_assert(IWT_HTAB < IW_NDBG, "debug slots");
+       IWT_COMMIT, IWT_TOTAL, IWD_FARIT, IWD_NBATCH, IWD_NPASS, IWD_NSTRAD, IWT_HTAB, IWT_REFETCH, IWT_EOB, IWT_HWALK };
+static_assert(IWT_HWALK < IW_NDBG, "debug slots");
 
 struct IwLds {
     u32 ltab[W_LCAP];
@@ -143,27 +145,22 @@ struct IwLds {
             u32 hwin[130];  // 512 stream bytes from the code-length codes on (dynamic header)
         } h;
         struct Hr {    // H round: marked extent (bits) of each segment, staged tokens, mark windows
-            u32 mlim[65];
+            u32 mlim[64];
             u32 tst[2 * IW_K][64];  // ring of two aligned list blocks (slot = token index % 8)
             u32 mwin[IW_MWIN][64];
+            u32 em[IW_EMW][64];     // each segment's first IW_EMW mark words (pass 2 reads them here)
         } hr;
         struct {       // L phase: the stage ring, near-token descriptors and batch markers
             u16 ptr[IW_S];
-            union {
-                u32 desc[128];  // near token 2l + slot of the group: (offset - first near index) | dist << 16
-                u64 fd[64];     // far tokens of the group by rank: source of the first quad | (quad, r, L) << 32
-            };
-            // near batch: batch tag << 8 | token id + 1 at the lane of the
-            // token's first byte in the batch (other slots hold older tags);
-            // past every other member of the union, so it is zeroed once per chunk
+            u64 fd[64];  // far parts of the group by rank: source byte | (ring entry | length << 16) << 32
+            // near batch: slot << 26 | part descriptor at the slot of each
+            // part's first byte in the batch, 0 elsewhere (cleared per batch)
             u32 mk[64];
         } st;
     } u;
     u32 dbgc[IW_NDBG];
 };
 static_assert(sizeof(IwLds) + 32 <= 10240, "16 chunks per CU");
-static_assert(2 * IW_S + 512 >= sizeof(decltype(IwLds::u)::Hr), "batch markers lie past the H-round scratch");
-static_assert(2 * IW_S + 512 >= sizeof(((IwLds*)nullptr)->u.h), "batch markers lie past the header scratch");
 
 // wave-local ordering point for LDS (and the compiler): a wave's LDS
 // operations are performed in issue order, so a fence at wavefront scope is
@@ -299,16 +296,28 @@ typedef __attribute__((address_space(1))) u64 gu64_ua __attribute__((aligned(1))
 typedef u32x4 u32x4_l2 __attribute__((aligned(2)));
 typedef u32 __attribute__((ext_vector_type(2))) u32x2_l2 __attribute__((aligned(2)));
 typedef u32 u32_l2 __attribute__((aligned(2)));
+// n (1..8) stage entries e0..e7 (two per word) stored exactly at pe
+__device__ __forceinline__ void iw_put(u16* pe, u32 n, u32 x, u32 y, u32 z, u32 w) {
+    if (n >= 8) {
+        *(u32x4_l2*)pe = u32x4{x, y, z, w};
+        return;
+    }
+    if (n & 4u) *(u32x2_l2*)pe = u32x2{x, y};
+    const u32 a = (n & 4u) ? z : x, b = (n & 4u) ? w : y;
+    u16* pt = pe + (n & 4u);
+    if (n & 2u) *(u32_l2*)pt = a;
+    if (n & 1u) pt[n & 2u] = (u16)((n & 2u) ? b : a);
+}
 // two source bytes (0-1 / 2-3 of w) as two final stage entries
 __device__ __forceinline__ u32 ie_lo(u32 w) { return __builtin_amdgcn_perm(0xFFFFFFFFu, w, 0x04010400u); }
 __device__ __forceinline__ u32 ie_hi(u32 w) { return __builtin_amdgcn_perm(0xFFFFFFFFu, w, 0x04030402u); }
 
 // tokens of a lane's list that start before word wi of its bitmap, plus the
 // marks in `part` (the bits of word wi below the position)
-__device__ __forceinline__ u32 iw_rank(const gu32* mw, u32 wi, u32 part) {
+__device__ __forceinline__ u32 iw_rank(const IwLds& L, u32 ks, const gu32* mw, u32 wi, u32 part) {
     u32 c = __popc(part);
 #pragma unroll 8
-    for (u32 w = 0; w < wi; w++) c += __popc(mw[w]);
+    for (u32 w = 0; w < wi; w++) c += __popc(w < IW_EMW ? L.u.hr.em[w][ks] : mw[w]);
     return c;
 }
 
@@ -374,14 +383,14 @@ __device__ void iw_bool_norm(u8* dst, u64 D) {
     } while (0)
 #define IW_ADD(slot, v) do { if (dbg && lane == 0) L.dbgc[slot] += (u32)(v); } while (0)
 
-// inclusive max over the wave (DPP row shifts, then the row maxima)
-__device__ __forceinline__ int iw_incl_max(int v) {
-    v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x111, 0xf, 0xf, false));  // row_shr:1
-    v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x112, 0xf, 0xf, false));  // row_shr:2
-    v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x114, 0xf, 0xf, false));  // row_shr:4
-    v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x118, 0xf, 0xf, false));  // row_shr:8
-    v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x142, 0xa, 0xf, false));  // row_bcast:15
-    v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x143, 0xc, 0xf, false));  // row_bcast:31
+// inclusive unsigned max over the wave (DPP row shifts, then the row maxima)
+__device__ __forceinline__ u32 iw_incl_umax(u32 v) {
+    v = max(v, (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false));  // row_shr:1
+    v = max(v, (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false));  // row_shr:2
+    v = max(v, (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false));  // row_shr:4
+    v = max(v, (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false));  // row_shr:8
+    v = max(v, (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false));  // row_bcast:15
+    v = max(v, (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false));  // row_bcast:31
     return v;
 }
 
@@ -402,6 +411,7 @@ template <int LB, u32 LCAP, int DB, u32 DCAP>
 __device__ __attribute__((always_inline)) int read_dynamic_wave(BitIn& b, u8* lens, HuffLds* lh, u32* ltab,
                                                                 HuffLds* dh, u32* dtab, u32* hwin, u32* tcyc) {
     const u32 lane = (u32)lane_id();
+    const u64 t_hdr0 = tcyc ? __builtin_readcyclecounter() : 0ull;
     if (!bi_has(b, 14)) return R_EXHAUSTED;
     const u32 nlen = bi_bits(b, 5) + 257, ndist = bi_bits(b, 5) + 1, ncode = bi_bits(b, 4) + 4;
     if (nlen > 286 || ndist > 30) return R_INVALID;  // "too many length or distance symbols"
@@ -463,9 +473,13 @@ __device__ __attribute__((always_inline)) int read_dynamic_wave(BitIn& b, u8* le
     const u64 lim = b.limit;
     u64 pos = c0 + 3 * ncode;  // wave-uniform reader position
     u32 idx = 0, prev = 0;
-    int r = R_OK;
+    // lens[0, total) starts at zero, so only the symbols with a nonzero value
+    // write (one length, or a 16's 3-6 repeats); 17 / 18 write nothing
+    for (u32 i = lane; i < 320; i += 64) lens[i] = 0;
+    __syncthreads();
     while (idx < total) {
-        // records of the 64 bit positions [pos, pos + 64): adv | l << 4 | sym << 8 | cnt << 16
+        // every lane decodes at bit pos + lane: code bits l, symbol, bits
+        // consumed with the extra bits (adv), lengths written (cnt)
         const u64 q = pos + lane;
         const u32 v = bits32(q);
         const u32 e = ltab[v & 127];
@@ -473,29 +487,54 @@ __device__ __attribute__((always_inline)) int read_dynamic_wave(BitIn& b, u8* le
         const u32 x = v >> l;
         const u32 adv = sym == 16 ? l + 2 : sym == 17 ? l + 3 : sym == 18 ? l + 7 : l;
         const u32 cnt = sym == 16 ? 3 + (x & 3) : sym == 17 ? 3 + (x & 7) : sym == 18 ? 11 + (x & 127) : 1;
-        const u32 rec = adv | (l << 4) | (sym << 8) | (cnt << 16);
+        // the true symbol starts in the window: a scalar walk of adv (l >= 1)
+        u64 mem = 0;
         u32 rel = 0;
-        while (rel < 64 && idx < total) {
-            const u32 f = (u32)__builtin_amdgcn_readlane((int)rec, (int)rel);
-            const u32 fa = f & 15, fl = (f >> 4) & 15, fs = (f >> 8) & 31, fc = f >> 16;
-            const u64 at = pos + rel;
-            // zlib's checks in read_dynamic's order: code bits, repeat at 0, extra bits, overflow
-            if (at + fl > lim) { r = R_EXHAUSTED; break; }
-            if (fs == 16 && idx == 0) { r = R_INVALID; break; }
-            if (at + fa > lim) { r = R_EXHAUSTED; break; }
-            if (idx + fc > total) { r = R_INVALID; break; }
-            const u32 val = fs < 16 ? fs : fs == 16 ? prev : 0u;
-            for (u32 k = lane; k < fc; k += 64) lens[idx + k] = (u8)val;
-            prev = val;
-            idx += fc;
-            rel += fa;
+        while (rel < 64) {
+            mem |= 1ull << rel;
+            rel += (u32)__builtin_amdgcn_readlane((int)adv, (int)rel);
         }
-        if (r != R_OK) return r;
-        pos += rel;
+        // every member at once: its first length index (prefix sum of the
+        // counts), valid while that is below total (later members are the
+        // block body)
+        const bool m = ((mem >> lane) & 1ull) != 0;
+        const u32 c = m ? cnt : 0u;
+        const u32 incl = iw_incl_scan(c);
+        const u32 is = idx + incl - c;
+        const bool valid = m && is < total;
+        // zlib's checks in read_dynamic's order (code bits, repeat at 0, extra
+        // bits, overflow); the first member, in stream order, that fails decides
+        const u64 at = pos + lane;
+        u32 err = 0;
+        if (valid) {
+            if (at + l > lim) err = R_EXHAUSTED;
+            else if (sym == 16 && is == 0) err = R_INVALID;
+            else if (at + adv > lim) err = R_EXHAUSTED;
+            else if (is + cnt > total) err = R_INVALID;
+        }
+        const u64 eb = __ballot(err != 0);
+        if (eb) return (int)__builtin_amdgcn_readlane((int)err, (int)__builtin_ctzll(eb));
+        // values: a literal length, 0 for 17 / 18, and for 16 the value of the
+        // last non-16 member before it (the window's, or the previous window's)
+        const u32 own = sym < 16 ? sym : 0u;
+        const u32 lsrc = iw_incl_umax(valid && sym != 16 ? lane + 1 : 0u);
+        const u32 pv = (u32)__shfl((int)own, (int)(lsrc ? lsrc - 1 : 0u), 64);
+        const u32 val = sym == 16 ? (lsrc ? pv : prev) : own;
+        if (valid && val)
+            for (u32 k = 0; k < cnt; k++) lens[is + k] = (u8)val;  // (cnt <= 6 here)
+        const u64 vb = __ballot(valid);
+        const u32 lastm = 63u - (u32)__builtin_clzll(vb);
+        idx = (u32)__builtin_amdgcn_readlane((int)(is + c), (int)lastm);
+        prev = (u32)__builtin_amdgcn_readlane((int)val, (int)lastm);
+        // next window: after the last member, or at the first member past the
+        // code lengths (the block body starts there)
+        const u64 rest = mem & ~vb;
+        pos += rest ? (u32)__builtin_ctzll(rest) : rel;
     }
     b.cbase = ~0ull;
     bi_seek(b, pos);
     const u64 t_tab = tcyc ? __builtin_readcyclecounter() : 0ull;
+    if (tcyc && lane == 0) tcyc[IWT_HWALK - IWT_HTAB] += (u32)(t_tab - t_hdr0);
     __syncthreads();
     u8 dl = 0;
     if (lane < ndist) dl = lens[nlen + lane];
@@ -581,8 +620,6 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
     bool last = false, boundary = false, after_stored = false;
     int r = R_OK;
     u32 est = IW_EST0;
-    L.u.st.mk[lane] = 0;  // batch tags start at 1
-    u32 ntag = (vflags & ZCG_FLAG_DEBUG_TAG_WRAP) ? 0xFFFFF0u : 0u;  // (tests: wrap within the first batches)
     if (dbg) {
         if (lane < IW_NDBG) L.dbgc[lane] = 0;
         wsync();
@@ -706,6 +743,15 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
                     *(gu32x4_a4*)(mk + w0) = u32x4{mv[0], mv[1], mv[2], mv[3]};
                     *(gu32x4_a4*)(mk + w0 + 4) = u32x4{mv[4], mv[5], mv[6], mv[7]};
                 }
+                // the first IW_EMW words also into LDS (rewritten until the
+                // window has moved past them: then they are final)
+                static_assert(IW_EMW == 2, "early mark words");
+                if (w0 == 0) {
+                    L.u.hr.em[0][lane] = mv[0];
+                    L.u.hr.em[1][lane] = mv[1];
+                } else if (w0 == 1) {
+                    L.u.hr.em[1][lane] = mv[0];
+                }
                 // slide the window to the word of my next token start (< 8 words on)
                 const u32 w1 = (q - p) >> 5, dw = w1 - w0;
 #pragma unroll
@@ -726,12 +772,11 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
                 const u32 ext = !active ? 0u : nxt == S_NONE ? seg : (q - p) + (nxt == S_MARKER ? 1u : 0u);
                 L.u.hr.mlim[lane] = ext < 32 * IW_MARKW ? ext : 32 * IW_MARKW;
             }
-            if (lane == 0) L.u.hr.mlim[64] = 0;
             __syncthreads();  // every lane's marks and list are stored
             IW_T(IWT_P1);
             // pass 2: follow my path until it meets a token start a later lane marked
             u32 ks = lane + 1, pk = pend, it2 = 0;
-            u32 lim = L.u.hr.mlim[ks];
+            u32 lim = ks < 64 ? L.u.hr.mlim[ks] : 0u;  // (no segment past lane 63)
             u32 cwi = 0xFFFFFFFFu, cwv = 0;
             bool run2 = nxt == S_NONE;
             while (__ballot(run2) != 0) {
@@ -739,13 +784,13 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
                 for (u32 k = 0; k < IW_K * IW_KH; k++) {
                     if (!run2) continue;
                     if (q >= round_hi) { nxt = S_ROUND_END; run2 = false; continue; }
-                    if (q >= pk + seg) { ks++; pk += seg; lim = L.u.hr.mlim[ks]; cwi = 0xFFFFFFFFu; }
+                    if (q >= pk + seg) { ks++; pk += seg; lim = ks < 64 ? L.u.hr.mlim[ks] : 0u; cwi = 0xFFFFFFFFu; }
                     const u32 off = q - pk;
                     if (off < lim) {
                         const u32 wi = off >> 5;
-                        if (wi != cwi) { cwv = marks[(u64)ks * IW_MWORDS + wi]; cwi = wi; }
+                        if (wi != cwi) { cwv = wi < IW_EMW ? L.u.hr.em[wi][ks] : marks[(u64)ks * IW_MWORDS + wi]; cwi = wi; }
                         if ((cwv >> (off & 31)) & 1u) {
-                            give = iw_rank(marks + (u64)ks * IW_MWORDS, wi, cwv & ((1u << (off & 31)) - 1u));
+                            give = iw_rank(L, ks, marks + (u64)ks * IW_MWORDS, wi, cwv & ((1u << (off & 31)) - 1u));
                             nxt = ks;
                             run2 = false;
                             continue;
@@ -903,10 +948,14 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
                 const u32 S32 = (u32)S;  // (D < 2^32)
                 const u32 s0 = S32 & 15u;  // ring entry of the stage's first byte
                 struct Tk {
-                    u32 kind, o, L, d;  // kind 0 none, 1 literal (d = byte), 2 far, 3 near; L clipped at cap
+                    // kind 0 none, 1 literal (d = byte), 2 match; L clipped at cap;
+                    // fl: the far part, the first bytes whose source lies before
+                    // the stage (copied from the committed output); the rest of
+                    // the match is its near part (source inside the stage)
+                    u32 kind, o, L, d, fl;
                 };
                 auto classify = [&](u32 tk, u32 o, u32 len, bool keep) -> Tk {
-                    Tk t{0u, o, 0u, 0u};
+                    Tk t{0u, o, 0u, 0u, 0u};
                     if (!keep) return t;
                     if (!(tk & W_MATCH)) {
                         t.kind = 1u;
@@ -921,123 +970,45 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
                     }
                     t.L = (fin && o + len > cap) ? cap - o : len;
                     t.d = d;
-                    // far: the whole source lies before the stage
-                    t.kind = (wide_ok && o + len <= d) ? 2u : 3u;
+                    t.kind = 2u;
+                    if (wide_ok && o < d) t.fl = d - o < t.L ? d - o : t.L;
                     return t;
                 };
-                auto group2 = [&](u32& tqa, u32& tqb, u32& okq) -> bool {
-                    IW_ADD(IWD_GROUPS, 1);
-                    const u32 ta = (okq & 1u) ? tqa : (W_MARK | M_END), tb = (okq & 2u) ? tqb : (W_MARK | M_END);
-                    fetch2(pcm, pcj, tqa, tqb, okq);
-                    advance(pcm, pcj, 128);
-                    const u64 ma = __ballot(w_marker(ta)), mb = __ballot(w_marker(tb));
-                    const u32 fa = ma ? 2 * (u32)__builtin_ctzll(ma) : 128u, fb = mb ? 2 * (u32)__builtin_ctzll(mb) + 1 : 128u;
-                    const u32 fm = fa < fb ? fa : fb;  // first marker, in token order
-                    const u32 ia = 2 * lane, ib = ia + 1;
-                    const u32 la = ia < fm ? w_len(ta) : 0u, lb = ib < fm ? w_len(tb) : 0u;
-                    const u32 ps = la + lb;
-                    const u32 incl = iw_incl_scan(ps);
-                    const u32 oa = emitted + incl - ps, ob = oa + la;
-                    const bool ka = ia < fm && (fin ? oa < cap : oa + la <= cap);
-                    const bool kb = ib < fm && (fin ? ob < cap : ob + lb <= cap);
-                    const u32 ntk = (u32)__popcll(__ballot(ka)) + (u32)__popcll(__ballot(kb));
-                    IW_T(IWT_PLACE);
-                    const Tk A = classify(ta, oa, la, ka), B = classify(tb, ob, lb, kb);
-                    if (A.kind == 1u) L.u.st.ptr[s0 + A.o] = (u16)(IE_VAL | A.d);
-                    if (B.kind == 1u) L.u.st.ptr[s0 + B.o] = (u16)(IE_VAL | B.d);
-                    IW_T(IWT_CLASSIFY);
-                    // far tokens, compacted one per lane (rank in token order):
-                    // 16-byte source pieces from the token's first source byte,
-                    // widened to entries by v_perm and stored exactly with
-                    // unaligned ds_write_b128 (8 entries; a token's last < 8
-                    // entries by b64 / b32 / b16), so tokens never share a store
-                    {
-                        const bool fA = A.kind == 2u, fB = B.kind == 2u;
-                        const u64 bA = __ballot(fA), bB = __ballot(fB);
-                        const u64 below = (1ull << lane) - 1ull;
-                        const u32 rkA = (u32)__popcll(bA & below) + (u32)__popcll(bB & below), rkB = rkA + (fA ? 1u : 0u);
-                        const u32 NF = (u32)__popcll(bA) + (u32)__popcll(bB);
-                        // source byte | (ring entry of the first byte | length << 16) << 32
-                        auto fdesc = [&](const Tk& t) -> u64 {
-                            return (u64)(S32 + t.o - t.d) | ((u64)((s0 + t.o) | (t.L << 16)) << 32);
-                        };
-                        for (u32 f0 = 0; f0 < NF; f0 += 64) {
-                            if (fA && rkA - f0 < 64u) L.u.st.fd[rkA - f0] = fdesc(A);
-                            if (fB && rkB - f0 < 64u) L.u.st.fd[rkB - f0] = fdesc(B);
-                            wsync();
-                            if (f0 + lane < NF) {
-                                const u64 fdw = L.u.st.fd[lane];
-                                const u32 src = (u32)fdw, hi = (u32)(fdw >> 32);
-                                const u32 qi = hi & 0xFFFFu, e = hi >> 16;
-                                const u32 np = (e + 15) >> 4;
-                                const u32x4 V0 = *(const gu32x4_ua*)(gd + src);
-                                // unconditional (a second read of the first piece when
-                                // there is one piece): a load kept under a branch waited
-                                // for the first one before issuing
-                                const u32x4 V1 = *(const gu32x4_ua*)(gd + src + (np > 1 ? 16u : 0u));
-                                // n (1..8) entries at ring entry k from source bytes w0:w1
-                                auto put = [&](u32 k, u32 n, u32 w0, u32 w1) {
-                                    u16* pe = L.u.st.ptr + k;
-                                    if (n >= 8) {
-                                        *(u32x4_l2*)pe = u32x4{ie_lo(w0), ie_hi(w0), ie_lo(w1), ie_hi(w1)};
-                                        return;
-                                    }
-                                    if (n & 4u) *(u32x2_l2*)pe = u32x2{ie_lo(w0), ie_hi(w0)};
-                                    const u32 rw = (n & 4u) ? w1 : w0;
-                                    u16* pt = pe + (n & 4u);
-                                    if (n & 2u) *(u32_l2*)pt = ie_lo(rw);
-                                    if (n & 1u) pt[n & 2u] = (u16)(IE_VAL | (((n & 2u) ? rw >> 16 : rw) & 0xFFu));
-                                };
-                                auto piece = [&](const u32x4& V, u32 p) {
-                                    const u32 b0 = 16 * p;  // < e
-                                    put(qi + b0, e - b0, V.x, V.y);
-                                    if (e > b0 + 8) put(qi + b0 + 8, e - b0 - 8, V.z, V.w);
-                                };
-                                piece(V0, 0);
-                                if (np > 1) piece(V1, 1);
-                                for (u32 p = 2; p < np; p++) {
-                                    IW_ADD(IWD_FARIT, 1);
-                                    const u32x4 Vp = *(const gu32x4_ua*)(gd + src + 16 * p);
-                                    piece(Vp, p);
-                                }
-                            }
-                            wsync();
-                        }
-                    }
-                    IW_T(IWT_FAR);
-                    // near bytes: index in the group's ordered near list
-                    const u32 nla = A.kind == 3u ? A.L : 0u, nlb = B.kind == 3u ? B.L : 0u;
-                    const u32 nps = nla + nlb;
-                    const u32 nincl = iw_incl_scan(nps);
-                    const u32 na = nincl - nps, nb = na + nla;
-                    const u32 NB = (u32)__builtin_amdgcn_readlane((int)nincl, 63);
-                    if (nla) L.u.st.desc[ia] = (A.o - na) | (A.d << 16);
-                    if (nlb) L.u.st.desc[ib] = (B.o - nb) | (B.d << 16);
+                // near parts of the group before, resolved while the far loads
+                // of the current group are in flight (their sources lie in
+                // earlier groups or in themselves; the far and literal entries
+                // of the current group are disjoint from them)
+                u32 pn_nla = 0, pn_nlb = 0, pn_na = 0, pn_nb = 0, pn_dsa = 0, pn_dsb = 0, pn_NB = 0;
+                auto near_run = [&]() {
                     // near batches of 64 bytes in output order: lane i takes near
-                    // byte n0 + i; its token is the last one whose first byte in
-                    // the batch is at or before it (marker + max scan)
-                    for (u32 n0 = 0; n0 < NB; n0 += 64) {
-                        if ((++ntag & 0xFFFFFFu) == 0) {  // 24-bit tags wrapped: forget every older marker
-                            L.u.st.mk[lane] = 0;
-                            wsync();
-                            ntag = 1;
-                        }
-                        const u32 tag = ntag << 8;
-                        if (nla && na < n0 + 64 && na + nla > n0) L.u.st.mk[na > n0 ? na - n0 : 0u] = tag | (ia + 1);
-                        if (nlb && nb < n0 + 64 && nb + nlb > n0) L.u.st.mk[nb > n0 ? nb - n0 : 0u] = tag | (ib + 1);
+                    // byte n0 + i; its part is the last one whose first byte in
+                    // the batch is at or before it.  Each part of the batch puts
+                    // slot << 26 | descriptor at the slot of its first byte there
+                    // (slot 0 for the part running into the batch), so one
+                    // unsigned max scan over the cleared slots hands every lane
+                    // its part's descriptor.
+                    for (u32 n0 = 0; n0 < pn_NB; n0 += 64) {
+                        L.u.st.mk[lane] = 0;
                         wsync();
-                        const u32 mv = L.u.st.mk[lane];
-                        const int tid = iw_incl_max((mv & ~0xFFu) == tag ? (int)(mv & 0xFFu) : 0) - 1;
+                        if (pn_nla && pn_na < n0 + 64 && pn_na + pn_nla > n0) {
+                            const u32 sl = pn_na > n0 ? pn_na - n0 : 0u;
+                            L.u.st.mk[sl] = (sl << 26) | pn_dsa;
+                        }
+                        if (pn_nlb && pn_nb < n0 + 64 && pn_nb + pn_nlb > n0) {
+                            const u32 sl = pn_nb > n0 ? pn_nb - n0 : 0u;
+                            L.u.st.mk[sl] = (sl << 26) | pn_dsb;
+                        }
+                        wsync();
+                        const u32 dsc = iw_incl_umax(L.u.st.mk[lane]) & 0x3FFFFFFu;
                         const u32 i = n0 + lane;
-                        bool done = i >= NB, strad = false;
+                        bool done = i >= pn_NB, strad = false;
                         u32 pos = 0, cur = 0;
                         if (!done) {
-                            const u32 dsc = L.u.st.desc[tid];
-                            const u32 p = (dsc & 0xFFFFu) + i;
-                            const u32 d = dsc >> 16;
+                            const u32 p = (dsc & 0x7FFu) + i;
+                            const u32 d = (dsc >> 11) + 1u;
                             pos = s0 + p;
                             if (p >= d) cur = s0 + p - d;
-                            else cur = IE_VAL | (u32)gd[swap_pos32(S32 + p - d, tw)];  // before the stage
+                            else cur = IE_VAL | (u32)gd[swap_pos32(S32 + p - d, tw)];  // before the stage (!wide_ok only)
                             strad = p < d;
                             // a source that is already final settles the byte now: the
                             // read precedes this batch's writes, and an entry of this
@@ -1068,6 +1039,116 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
                             wsync();
                         }
                     }
+                    pn_NB = 0;
+                };
+                auto group2 = [&](u32& tqa, u32& tqb, u32& okq) -> bool {
+                    IW_ADD(IWD_GROUPS, 1);
+                    const u32 ta = (okq & 1u) ? tqa : (W_MARK | M_END), tb = (okq & 2u) ? tqb : (W_MARK | M_END);
+                    const u64 ma = __ballot(w_marker(ta)), mb = __ballot(w_marker(tb));
+                    const u32 fa = ma ? 2 * (u32)__builtin_ctzll(ma) : 128u, fb = mb ? 2 * (u32)__builtin_ctzll(mb) + 1 : 128u;
+                    const u32 fm = fa < fb ? fa : fb;  // first marker, in token order
+                    const u32 ia = 2 * lane, ib = ia + 1;
+                    const u32 la = ia < fm ? w_len(ta) : 0u, lb = ib < fm ? w_len(tb) : 0u;
+                    const u32 ps = la + lb;
+                    const u32 incl = iw_incl_scan(ps);
+                    const u32 oa = emitted + incl - ps, ob = oa + la;
+                    const bool ka = ia < fm && (fin ? oa < cap : oa + la <= cap);
+                    const bool kb = ib < fm && (fin ? ob < cap : ob + lb <= cap);
+                    const u32 ntk = (u32)__popcll(__ballot(ka)) + (u32)__popcll(__ballot(kb));
+                    IW_T(IWT_PLACE);
+                    const Tk A = classify(ta, oa, la, ka), B = classify(tb, ob, lb, kb);
+                    if (A.kind == 1u) L.u.st.ptr[s0 + A.o] = (u16)(IE_VAL | A.d);
+                    if (B.kind == 1u) L.u.st.ptr[s0 + B.o] = (u16)(IE_VAL | B.d);
+                    IW_T(IWT_CLASSIFY);
+                    // far parts, compacted one per lane (rank in token order):
+                    // 16-byte source pieces from the part's first source byte,
+                    // widened to entries by v_perm and stored exactly with
+                    // unaligned ds_write_b128 (8 entries; a part's last < 8
+                    // entries by b64 / b32 / b16), so tokens never share a store.
+                    // The token words of the group IW_GK ahead are fetched right
+                    // after the far loads: vmcnt is in order, so the far data can
+                    // then be waited for with the prefetch still in flight.
+                    {
+                        const bool fA = A.fl != 0u, fB = B.fl != 0u;
+                        const u64 bA = __ballot(fA), bB = __ballot(fB);
+                        const u64 below = (1ull << lane) - 1ull;
+                        const u32 rkA = (u32)__popcll(bA & below) + (u32)__popcll(bB & below), rkB = rkA + (fA ? 1u : 0u);
+                        const u32 NF = (u32)__popcll(bA) + (u32)__popcll(bB);
+                        // source byte | (ring entry of the first byte | length << 16) << 32
+                        auto fdesc = [&](const Tk& t) -> u64 {
+                            return (u64)(S32 + t.o - t.d) | ((u64)((s0 + t.o) | (t.fl << 16)) << 32);
+                        };
+                        // one batch of <= 64 far parts; the first one issues the prefetch
+                        auto far_batch = [&](u32 f0, auto with_prefetch) {
+                            if (fA && rkA - f0 < 64u) L.u.st.fd[rkA - f0] = fdesc(A);
+                            if (fB && rkB - f0 < 64u) L.u.st.fd[rkB - f0] = fdesc(B);
+                            wsync();
+                            const bool fl = f0 + lane < NF;
+                            const u64 fdw = L.u.st.fd[lane];
+                            const u32 src = (u32)fdw, hi = (u32)(fdw >> 32);
+                            const u32 qi = hi & 0xFFFFu, e = hi >> 16;
+                            const u32 np = (e + 15) >> 4;
+                            u32x4 V0 = u32x4{0u, 0u, 0u, 0u}, V1 = V0;
+                            if (fl) {
+                                V0 = *(const gu32x4_ua*)(gd + src);
+                                // unconditional (a second read of the first piece when
+                                // there is one piece): a load kept under a branch waited
+                                // for the first one before issuing
+                                V1 = *(const gu32x4_ua*)(gd + src + (np > 1 ? 16u : 0u));
+                            }
+                            if constexpr (decltype(with_prefetch)::value) {
+                                fetch2(pcm, pcj, tqa, tqb, okq);
+                                advance(pcm, pcj, 128);
+                                if (pn_NB) near_run();
+                            }
+                            // both pieces waited for here, on every path: vmcnt(2)
+                            // with the prefetch still in flight (a wait where the
+                            // registers are next written would be vmcnt(0))
+                            asm volatile("" ::"v"(V0), "v"(V1));
+                            if (fl) {
+                                auto piece = [&](const u32x4& V, u32 p) {
+                                    const u32 b0 = 16 * p;  // < e
+                                    iw_put(L.u.st.ptr + qi + b0, e - b0, ie_lo(V.x), ie_hi(V.x), ie_lo(V.y), ie_hi(V.y));
+                                    if (e > b0 + 8)
+                                        iw_put(L.u.st.ptr + qi + b0 + 8, e - b0 - 8, ie_lo(V.z), ie_hi(V.z), ie_lo(V.w),
+                                               ie_hi(V.w));
+                                };
+                                piece(V0, 0);
+                                if (np > 1) piece(V1, 1);
+                                for (u32 p = 2; p < np; p++) {
+                                    IW_ADD(IWD_FARIT, 1);
+                                    const u32x4 Vp = *(const gu32x4_ua*)(gd + src + 16 * p);
+                                    piece(Vp, p);
+                                }
+                            }
+                            wsync();
+                        };
+                        far_batch(0u, std::true_type{});
+                        for (u32 f0 = 64; f0 < NF; f0 += 64) far_batch(f0, std::false_type{});
+                    }
+                    IW_T(IWT_FAR);
+                    // near parts: one pointer per byte, resolved in ordered
+                    // batches of 64 by pointer jumping (index in the group's
+                    // ordered list of near bytes).  (Token-level copies of whole
+                    // near parts, in rounds until their sources are final, took
+                    // 27.1 vs 21.6 ms per C2 launch: 8 entries at 2-byte
+                    // alignment are an unaligned LDS access, 256 instead of 72
+                    // cycles per read, tools/probe/lds_unaligned_perf.hip.)
+                    const u32 noa = A.o + A.fl, nob = B.o + B.fl;
+                    const u32 nla = A.kind == 2u ? A.L - A.fl : 0u, nlb = B.kind == 2u ? B.L - B.fl : 0u;
+                    const u32 nps = nla + nlb;
+                    const u32 nincl = iw_incl_scan(nps);
+                    const u32 na = nincl - nps, nb = na + nla;
+                    const u32 NB = (u32)__builtin_amdgcn_readlane((int)nincl, 63);
+                    // a part's descriptor: (its first offset - its first near index) | (d - 1) << 11
+                    const u32 dsa = (noa - na) | ((A.d - 1u) << 11), dsb = (nob - nb) | ((B.d - 1u) << 11);
+                    pn_nla = nla;
+                    pn_nlb = nlb;
+                    pn_na = na;
+                    pn_nb = nb;
+                    pn_dsa = dsa;
+                    pn_dsb = dsb;
+                    pn_NB = NB;
                     IW_T(IWT_NEAR);
                     if (ntk) {
                         const u32 t = ntk - 1;  // the last taken token: lane t / 2, slot t % 2
@@ -1092,7 +1173,10 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
                     if (group2(tq1a, tq1b, ok1)) break;
                     if (group2(tq2a, tq2b, ok2)) break;
                 }
+                if (pn_NB) near_run();  // the stage's last group
+                IW_T(IWT_NEAR);
                 refetch();  // the next stage starts at the cursor
+                IW_T(IWT_REFETCH);
                 IW_ADD(IWD_STAGES, 1);
                 if (__ballot(bad) != 0) { r = R_INVALID; break; }
                 const u32 emit = emitted < cap ? emitted : cap;  // a token may cross N: clip
@@ -1126,6 +1210,7 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
                     } else if (mcode == M_EOB) {
                         const u32 lm = mL(cm);
                         const u32 qe = iw_pos(gl, lm, cj + 1, R0 + lm * seg);  // after the EOB code
+                        IW_T(IWT_EOB);
                         block_end = true;
                         b.cbase = ~0ull;
                         bi_seek(b, qe);
