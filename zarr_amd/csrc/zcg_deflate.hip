@@ -849,6 +849,111 @@ __global__ void dz_keys(const zcg_chunk* __restrict__ chunks, u32 c0, u64 D, u64
     vals[g] = (u32)g;
 }
 
+// zz::search (zcg_zlib_core.h, the host reference) for native-order bytes and
+// p + 32 <= D, over the sorted run: the chain of p = entry j is entries j-1,
+// j-2, ... while the key is kj.  p's first 32 bytes stay in registers; the
+// candidates come 4 at a time (their keys and positions by two 16-byte loads,
+// then their first 16 bytes by four loads in flight together), and are then
+// compared in chain order, so a thread waits two memory latencies per four
+// candidates instead of one or two per candidate.  Same candidates, order,
+// ties (the first candidate reaching a longer match), NIL and window rules,
+// nice cut and reduced-budget snapshot as zz::search; its scan_end test only
+// skips candidates that cannot beat `best`, so leaving it out changes no result.
+__device__ zz::Match2 dz_search_run(u32 p, u32 D, const zz::Config& cfg, const u8* src, const u32* __restrict__ keys,
+                                    const u32* __restrict__ vals, u64 j, u32 kj, u32 cbase) {
+    zz::Match2 r{0u, 0u};
+    const gu8* g = (const gu8*)src;
+    typedef __attribute__((address_space(1))) u32x4 gu32x4_a4 __attribute__((aligned(4)));
+    auto b4 = [&](u32 i) -> u32 { return *(const df_gu32_ua*)(g + i); };
+    auto pre16 = [](u32x4 A, u32x4 B) -> u32 {
+        const u32 x0 = A.x ^ B.x, x1 = A.y ^ B.y, x2 = A.z ^ B.z, x3 = A.w ^ B.w;
+        if (x0) return (u32)__builtin_ctz(x0) >> 3;
+        if (x1) return 4 + ((u32)__builtin_ctz(x1) >> 3);
+        if (x2) return 8 + ((u32)__builtin_ctz(x2) >> 3);
+        if (x3) return 12 + ((u32)__builtin_ctz(x3) >> 3);
+        return 16u;
+    };
+    const u32 look = D - p;
+    const u32 mx = look < zz::MAX_MATCH ? look : zz::MAX_MATCH;  // >= 32
+    const u32 nice = cfg.nice < look ? cfg.nice : look;
+    const u32 lim = p > zz::MAX_DIST ? p - zz::MAX_DIST : 0u;
+    const u32 nred = cfg.chain >> 2;
+    const u32x4 P0 = *(const gu32x4_ua*)(g + p), P1 = *(const gu32x4_ua*)(g + p + 16);
+    u32 best = 0, bstart = 0, k = 0;
+    bool red_done = false;
+    // entries jj-4 .. jj-1 per block (jj >= 4 here: a shorter rest reads the
+    // entries before the array start from index 0 and marks them invalid)
+    for (u64 jj = j; k < cfg.chain; jj -= 4) {
+        const u64 b = jj >= 4 ? jj - 4 : 0;
+        const u32x4 K = *(const gu32x4_a4*)(keys + b), V = *(const gu32x4_a4*)(vals + b);
+        // candidate i (chain order) = entry jj-1-i = component 3-i of the block (when jj >= 4)
+        u32 cc[4];
+        bool ok[4];
+#pragma unroll
+        for (u32 i = 0; i < 4; i++) {
+            const u64 e = jj - 1 - i;  // (wraps when jj <= i: invalid)
+            const u32 lane4 = (u32)(e - b);
+            const u32 kv = lane4 == 0 ? K.x : lane4 == 1 ? K.y : lane4 == 2 ? K.z : K.w;
+            const u32 vv = lane4 == 0 ? V.x : lane4 == 1 ? V.y : lane4 == 2 ? V.z : V.w;
+            ok[i] = jj > i && kv == kj;
+            cc[i] = vv - cbase;
+        }
+        u32x4 C[4];
+#pragma unroll
+        for (u32 i = 0; i < 4; i++) C[i] = *(const gu32x4_ua*)(g + (ok[i] && cc[i] < p ? cc[i] : p));
+        bool stop = false;
+#pragma unroll
+        for (u32 i = 0; i < 4; i++) {
+            const u32 c = cc[i];
+            if (k == 0) {
+                // hash_head != NIL && strstart - hash_head <= MAX_DIST; the
+                // window-relative head at the slid window's base reads as NIL
+                if (!ok[i] || c == zz::slides_at(p, D) * zz::WSIZE || p - c > zz::MAX_DIST) return r;
+            } else if (!ok[i] || c <= lim) {
+                stop = true;
+                break;
+            }
+            u32 len = pre16(P0, C[i]);
+            if (len == 16) {
+                const u32x4 C1 = *(const gu32x4_ua*)(g + c + 16);
+                len += pre16(P1, C1);
+                if (len == 32) {
+                    while (len + 4 <= mx) {
+                        const u32 x = b4(p + len) ^ b4(c + len);
+                        if (x) {
+                            len += (u32)__builtin_ctz(x) >> 3;
+                            goto done;
+                        }
+                        len += 4;
+                    }
+                    while (len < mx && g[p + len] == g[c + len]) len++;
+                }
+            }
+        done:
+            if (len > best) {
+                best = len;
+                bstart = c;
+                if (best >= nice) {
+                    stop = true;
+                    break;
+                }
+            }
+            if (k + 1 == nred) {
+                r.red = best ? (best | ((p - bstart) << 9)) : 0u;
+                red_done = true;
+            }
+            if (++k == cfg.chain) {
+                stop = true;
+                break;
+            }
+        }
+        if (stop) break;
+    }
+    r.full = best ? (best | ((p - bstart) << 9)) : 0u;
+    if (!red_done) r.red = r.full;
+    return r;
+}
+
 // zz::search at every position of the sub-batch: m2[g] = {full, red}, one
 // thread per position in the ORDER OF THE SORTED KEYS.  The stable sort of
 // (chunk, hash) with ascending positions lays every hash chain out
@@ -887,7 +992,8 @@ __global__ void dz_best(const zcg_chunk* __restrict__ chunks, u32 c0, u64 D, u64
             jj--;
             return vals[jj] - cbase;
         };
-        r = zz::search(p, (u32)D, cfg, b4, b1, pv);
+        if (!t.swap && !t.isbool && (u64)p + 32 <= D) r = dz_search_run(p, (u32)D, cfg, src, keys, vals, j, kj, cbase);
+        else r = zz::search(p, (u32)D, cfg, b4, b1, pv);
     }
     m2[g] = make_uint2(r.full, r.red);
 }
@@ -1580,7 +1686,7 @@ __global__ __launch_bounds__(256) void dz_final(const zcg_chunk* __restrict__ ch
 uint64_t deflate_exact_ws_bytes(const zcg_array* a, uint32_t n) {
     const DType t = make_dtype(a->dtype);
     const u64 D = a->chunk_num_elements * (u64)t.es;
-    if (n == 0) return 0;
+    if (n == 0 || D >= (1ull << 31)) return 0;  // (chunks of >= 2 GiB: per-chunk UNSUPPORTED)
     return dz_layout(D, n).total;
 }
 
@@ -1591,8 +1697,13 @@ static hipError_t launch_deflate_exact(const zcg_array* a, const zcg_chunk* d_ch
     const u64 D = a->chunk_num_elements * (u64)t.es;
     const u32 xfl = level >= 9 ? 2u : (level <= 1 ? 4u : 0u);
     const u64 bound = zcg_encode_bound(&a->compression, D);
+    if (D >= (1ull << 31)) {  // u32 positions: every chunk UNSUPPORTED, the launch itself succeeds
+        if (hipError_t e = hipMemsetD32Async((hipDeviceptr_t)d_status, ZCG_ERR_UNSUPPORTED, n, s); e != hipSuccess)
+            return e;
+        return hipMemsetAsync(d_out_len, 0, sizeof(uint64_t) * (size_t)n, s);
+    }
     const DzLayout y = dz_layout(D, n);
-    if (ws_bytes < y.total || y.tot >= (1ull << 31) || D >= (1ull << 31)) return hipErrorInvalidValue;
+    if (ws_bytes < y.total || y.tot >= (1ull << 31)) return hipErrorInvalidValue;
     const zz::Config cfg = zz::level_config((int)level);
     u8* w = (u8*)ws;
     uint2* m2 = (uint2*)(w + y.off_m2);

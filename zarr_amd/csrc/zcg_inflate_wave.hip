@@ -74,6 +74,7 @@ constexpr u32 IW_KH = 2;         // flush periods per outer step (reader loads a
 #ifndef ZIW_G
 #define ZIW_G 4
 #endif
+
 constexpr u32 IW_G = ZIW_G;                      // lanes whose lists are interleaved by 16-byte blocks
 constexpr u32 IW_TSTR = IW_TCAP + 2 * IW_K;      // token list stride (a flush writes up to two aligned blocks)
 static_assert(IW_TSTR % 4 == 0 && 64 % IW_G == 0, "list blocks");
@@ -904,14 +905,39 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
             };
             u32 tq0a, tq0b, tq1a, tq1b, tq2a, tq2b, ok0, ok1, ok2;
             u32 pcm = 0, pcj = 0;  // prefetch cursor: IW_GK groups past the cursor (groups inside a stage are whole)
+            // the IW_GK groups from the cursor in one walk over the chain
+            // members (tokens cj + 128 g + 2 l + {0, 1} of group g)
             auto refetch = [&]() {
+                static_assert(IW_GK == 3, "three group slots");
+                u32 jt[6], lt[6], pt[6];
+#pragma unroll
+                for (u32 t = 0; t < 6; t++) {
+                    jt[t] = cj + 128 * (t >> 1) + 2 * lane + (t & 1);
+                    lt[t] = 0xFFFFFFFFu;
+                    pt[t] = 0;
+                }
+                for (u32 m = (u32)__builtin_amdgcn_readfirstlane((int)cm); m < ncm; m++) {
+                    const u32 e = mE(m), ln = mL(m), s1 = mS1(m);
+                    bool open = false;
+#pragma unroll
+                    for (u32 t = 0; t < 6; t++) {
+                        if (lt[t] == 0xFFFFFFFFu && jt[t] < e) { lt[t] = ln; pt[t] = jt[t]; }
+                        open |= lt[t] == 0xFFFFFFFFu;
+                    }
+                    if (__ballot(open) == 0) break;
+#pragma unroll
+                    for (u32 t = 0; t < 6; t++)
+                        if (lt[t] == 0xFFFFFFFFu) jt[t] = jt[t] - e + s1;
+                }
+                auto ld = [&](u32 t) -> u32 { return gl[lt[t] != 0xFFFFFFFFu ? iw_ta(lt[t], pt[t]) : 0u]; };
+                auto okm = [&](u32 t) -> u32 {
+                    return (lt[t] != 0xFFFFFFFFu ? 1u : 0u) | (lt[t + 1] != 0xFFFFFFFFu ? 2u : 0u);
+                };
+                tq0a = ld(0); tq0b = ld(1); ok0 = okm(0);
+                tq1a = ld(2); tq1b = ld(3); ok1 = okm(2);
+                tq2a = ld(4); tq2b = ld(5); ok2 = okm(4);
                 u32 cm1 = cm, cj1 = cj;
-                fetch2(cm1, cj1, tq0a, tq0b, ok0);
-                advance(cm1, cj1, 128);
-                fetch2(cm1, cj1, tq1a, tq1b, ok1);
-                advance(cm1, cj1, 128);
-                fetch2(cm1, cj1, tq2a, tq2b, ok2);
-                advance(cm1, cj1, 128);
+                advance(cm1, cj1, 128 * IW_GK);
                 pcm = cm1;
                 pcj = cj1;
             };
@@ -1173,10 +1199,10 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
                     if (group2(tq1a, tq1b, ok1)) break;
                     if (group2(tq2a, tq2b, ok2)) break;
                 }
+                refetch();  // the next stage starts at the cursor (its loads fly during the last near batches)
+                IW_T(IWT_REFETCH);
                 if (pn_NB) near_run();  // the stage's last group
                 IW_T(IWT_NEAR);
-                refetch();  // the next stage starts at the cursor
-                IW_T(IWT_REFETCH);
                 IW_ADD(IWD_STAGES, 1);
                 if (__ballot(bad) != 0) { r = R_INVALID; break; }
                 const u32 emit = emitted < cap ? emitted : cap;  // a token may cross N: clip
