@@ -372,7 +372,8 @@ int zcg_encode_batch(zcg_ctx* ctx, const zcg_array* a, const zcg_chunk* d_chunks
         zcg_ctx::Ws* w = nullptr;
         const int r = stream_ws(ctx, stream, deflate_ws_bytes(a, n), &w);
         if (r != ZCG_OK) return r;
-        e = launch_deflate(a, d_chunks, n, d_out_len, d_status, w->p, w->bytes, s);
+        ws_side(w);
+        e = launch_deflate(a, d_chunks, n, d_out_len, d_status, w->p, w->bytes, s, w->side, w->fork, w->join);
         break;
     }
     case ZCG_CODEC_XZ: {

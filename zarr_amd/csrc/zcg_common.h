@@ -278,9 +278,13 @@ uint64_t inflate_par_ws_bytes(const zcg_array* a, uint32_t n);
 hipError_t launch_inflate_wave(const zcg_array* a, const zcg_chunk* d_chunks, uint32_t n,
                                int32_t* d_status, void* ws, uint64_t ws_bytes, hipStream_t s);
 uint64_t inflate_wave_ws_bytes(const zcg_array* a, uint32_t n);
+// side/fork/join (optional, nullptr: one stream): the lazy parse of each
+// sub-batch runs on the side stream while the next sub-batch's match search
+// runs on s (the workspace's side stream, as the LZ4 decoder uses it)
 hipError_t launch_deflate(const zcg_array* a, const zcg_chunk* d_chunks, uint32_t n,
                           uint64_t* d_out_len, int32_t* d_status, void* ws, uint64_t ws_bytes,
-                          hipStream_t s);
+                          hipStream_t s, hipStream_t side = nullptr, hipEvent_t fork = nullptr,
+                          hipEvent_t join = nullptr);
 uint64_t deflate_ws_bytes(const zcg_array* a, uint32_t n);
 hipError_t launch_bzip2_decode(const zcg_array* a, const zcg_chunk* d_chunks, uint32_t n,
                                int32_t* d_status, void* ws, uint64_t ws_bytes, hipStream_t s);

@@ -1016,10 +1016,10 @@ __global__ void dz_best(const zcg_chunk* __restrict__ chunks, u32 c0, u64 D, u64
 __global__ __launch_bounds__(64) void dz_parse(const zcg_chunk* __restrict__ chunks, u32 c0, u32 nc, u64 D, DType t,
                                               zz::Config cfg, u32* __restrict__ wbase, u64 off_m2, u64 off_sym,
                                               u64 off_pos, u64 off_bm, u64 off_tail, DzChunk* __restrict__ cst,
-                                              DzBlock* __restrict__ blks, u32 nbmax) {
-    const u32 cl = blockIdx.x;  // chunk of this launch
+                                              DzBlock* __restrict__ blks, u32 nbmax, u32 cb) {
+    const u32 cl = blockIdx.x;  // chunk of this launch (chunks[c0 + cl]; its records at cb + cl)
     if (cl >= nc) return;
-    const u32 c = cl;
+    const u32 c = cb + cl;
     const u32 lane = threadIdx.x;
     const zcg_chunk ch = chunks[c0 + cl];
     DzChunk* cs = cst + c;
@@ -1692,7 +1692,7 @@ uint64_t deflate_exact_ws_bytes(const zcg_array* a, uint32_t n) {
 
 static hipError_t launch_deflate_exact(const zcg_array* a, const zcg_chunk* d_chunks, uint32_t n, u32 level,
                                        uint64_t* d_out_len, int32_t* d_status, void* ws, uint64_t ws_bytes,
-                                       hipStream_t s) {
+                                       hipStream_t s, hipStream_t side, hipEvent_t fork, hipEvent_t join) {
     const DType t = make_dtype(a->dtype);
     const u64 D = a->chunk_num_elements * (u64)t.es;
     const u32 xfl = level >= 9 ? 2u : (level <= 1 ? 4u : 0u);
@@ -1715,8 +1715,12 @@ static hipError_t launch_deflate_exact(const zcg_array* a, const zcg_chunk* d_ch
     if (fast) {
         if (hipError_t e = lds_attr_once((const void*)dz_parse_fast, (int)DZF_LDS_RING); e != hipSuccess) return e;
     }
+    const bool two = side && fork && join && !fast;  // the parse of each sub-batch on the side stream
     for (u32 s0 = 0; s0 < n; s0 += y.sb) {
         const u32 scnt = (n - s0) < y.sb ? (n - s0) : y.sb;
+        // a parse that does not run leaves every chunk failed, so the kernels
+        // after it never read an unset record
+        if (hipError_t e = hipMemsetAsync(cst, 0xFF, sizeof(DzChunk) * (size_t)scnt, s); e != hipSuccess) return e;
         for (u32 c0 = s0; c0 < s0 + scnt && D > 0 && !fast; c0 += y.m) {
             const u32 cnt = (s0 + scnt - c0) < y.m ? (s0 + scnt - c0) : y.m;
             const u64 tot = (u64)cnt * D;
@@ -1733,18 +1737,33 @@ static hipError_t launch_deflate_exact(const zcg_array* a, const zcg_chunk* d_ch
             if (e != hipSuccess) return e;
             hipLaunchKernelGGL(dz_best, dim3(G), dim3(256), 0, s, d_chunks, c0, D, tot, t, cfg,
                                (const u32*)dk.Current(), (const u32*)dv.Current(), m2 + (u64)(c0 - s0) * D);
+            // the sub-batch's lazy parse (one wave per chunk: a few waves per
+            // CU) runs beside the next sub-batch's sort and match search
+            hipStream_t ps = s;
+            if (two) {
+                if ((e = hipEventRecord(fork, s)) != hipSuccess) return e;
+                if ((e = hipStreamWaitEvent(side, fork, 0)) != hipSuccess) return e;
+                ps = side;
+            }
+            hipLaunchKernelGGL(dz_parse, dim3(cnt), dim3(64), 0, ps, d_chunks, c0, cnt, D, t, cfg, (u32*)w,
+                               y.off_m2 / 4, y.off_sym / 4, y.off_pos / 4, y.off_bm / 4, y.off_tail / 4, cst, blks,
+                               y.nbmax, c0 - s0);
+            if ((e = hipGetLastError()) != hipSuccess) return e;
         }
-        // a parse that does not run leaves every chunk failed, so the kernels
-        // after it never read an unset record
-        if (hipError_t e = hipMemsetAsync(cst, 0xFF, sizeof(DzChunk) * (size_t)scnt, s); e != hipSuccess) return e;
+        if (two) {
+            if (hipError_t e = hipEventRecord(join, side); e != hipSuccess) return e;
+            if (hipError_t e = hipStreamWaitEvent(s, join, 0); e != hipSuccess) return e;
+        }
         if (fast) {
             hipLaunchKernelGGL(dz_parse_fast, dim3(scnt), dim3(64), DZF_LDS_RING, s, d_chunks, s0, scnt, D, t, cfg,
                                (u32*)w, y.off_m2 / 4, cst, blks, y.nbmax);
             if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
-        } else {
+        }
+        if (!fast && D == 0) {  // (empty chunks: the parse writes their empty streams)
             hipLaunchKernelGGL(dz_parse, dim3(scnt), dim3(64), 0, s, d_chunks, s0, scnt, D, t, cfg, (u32*)w,
                                y.off_m2 / 4, y.off_sym / 4, y.off_pos / 4, y.off_bm / 4, y.off_tail / 4, cst, blks,
-                               y.nbmax);
+                               y.nbmax, 0u);
+            if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
         }
         const u64 nbk = (u64)scnt * y.nbmax;
         hipLaunchKernelGGL(dz_plan, dim3((u32)nbk), dim3(64), 0, s, scnt, cst, blks, y.nbmax, (const u32*)w, D);
@@ -1785,12 +1804,13 @@ const char* cfg_deflate() { return "deflate:CHAIN6=" ZCG_STR(ZCG_DF_CHAIN6); }
 
 hipError_t launch_deflate(const zcg_array* a, const zcg_chunk* d_chunks, uint32_t n,
                           uint64_t* d_out_len, int32_t* d_status, void* ws, uint64_t ws_bytes,
-                          hipStream_t s) {
+                          hipStream_t s, hipStream_t side, hipEvent_t fork, hipEvent_t join) {
     if (n == 0) return hipSuccess;
     const DType t = make_dtype(a->dtype);
     const u64 D = a->chunk_num_elements * (u64)t.es;
     const u32 level = (u32)zcg_effective_gzip_level(a->compression.gzip_level);
-    if (deflate_exact_level(a)) return launch_deflate_exact(a, d_chunks, n, level, d_out_len, d_status, ws, ws_bytes, s);
+    if (deflate_exact_level(a))
+        return launch_deflate_exact(a, d_chunks, n, level, d_out_len, d_status, ws, ws_bytes, s, side, fork, join);
     const u32 xfl = level >= 9 ? 2u : (level <= 1 ? 4u : 0u);
     const u32 nseg = (u32)((D + DF_SEG - 1) / DF_SEG);
     const u64 bound = zcg_encode_bound(&a->compression, D);

@@ -942,6 +942,7 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
                 pcj = cj1;
             };
             refetch();
+            u32 gslot = 0;  // the group slot the next group is in
             bool round_done = false;
             while (!round_done && r == R_OK) {
                 const u64 S = P;
@@ -964,6 +965,7 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
                 }
                 wsync();
                 u32 emitted = 0;
+                bool rej = false;  // the stage ended before a group that did not fit whole
                 bool bad = false;  // a distance before the output start
                 u32 why = 0;       // 1 final cut, 2 marker / round end, 3 capacity
                 u32 mcode = 0;
@@ -1081,6 +1083,15 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
                     const bool ka = ia < fm && (fin ? oa < cap : oa + la <= cap);
                     const bool kb = ib < fm && (fin ? ob < cap : ob + lb <= cap);
                     const u32 ntk = (u32)__popcll(__ballot(ka)) + (u32)__popcll(__ballot(kb));
+                    // a group that does not fit whole into a stage that has
+                    // bytes already starts the next stage instead: the token
+                    // slots stay valid (nothing was prefetched into this one),
+                    // so no refetch is needed there
+                    if (!fin && emitted != 0 && ntk < fm) {
+                        rej = true;
+                        why = 3;
+                        return true;
+                    }
                     IW_T(IWT_PLACE);
                     const Tk A = classify(ta, oa, la, ka), B = classify(tb, ob, lb, kb);
                     if (A.kind == 1u) L.u.st.ptr[s0 + A.o] = (u16)(IE_VAL | A.d);
@@ -1195,11 +1206,17 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
                     return false;
                 };
                 for (;;) {
-                    if (group2(tq0a, tq0b, ok0)) break;
-                    if (group2(tq1a, tq1b, ok1)) break;
-                    if (group2(tq2a, tq2b, ok2)) break;
+                    bool end;
+                    if (gslot == 0) end = group2(tq0a, tq0b, ok0);
+                    else if (gslot == 1) end = group2(tq1a, tq1b, ok1);
+                    else end = group2(tq2a, tq2b, ok2);
+                    if (!rej) gslot = gslot == IW_GK - 1 ? 0u : gslot + 1;
+                    if (end) break;
                 }
-                refetch();  // the next stage starts at the cursor (its loads fly during the last near batches)
+                if (!rej) {  // the stage ended inside a group: the next one starts at the cursor
+                    refetch();  // (its loads fly during the last near batches)
+                    gslot = 0;
+                }
                 IW_T(IWT_REFETCH);
                 if (pn_NB) near_run();  // the stage's last group
                 IW_T(IWT_NEAR);
