@@ -1111,8 +1111,23 @@ __global__ __launch_bounds__(64) void dz_parse(const zcg_chunk* __restrict__ chu
     u64 fsel_sy = (u64)(fsy - wbase), fsel_ps = (u64)(fps - wbase);
     if (!any_ovf) {
         // ---- stitch (wave-uniform chain walk, cooperative copies) ----
+        // (8 pieces per lane in flight: a copy waits one load latency per 512 symbols)
         auto copy = [&](const u32* ssy, const u32* sps, u32 n) {
-            for (u32 i = lane; i < n; i += 64) {
+            u32 i = lane;
+            for (; i + 7 * 64 < n; i += 8 * 64) {
+                u32 a[8], b[8];
+#pragma unroll
+                for (u32 k = 0; k < 8; k++) {
+                    a[k] = ssy[i + 64 * k];
+                    b[k] = sps[i + 64 * k];
+                }
+#pragma unroll
+                for (u32 k = 0; k < 8; k++) {
+                    fsy[nsym + i + 64 * k] = a[k];
+                    fps[nsym + i + 64 * k] = b[k];
+                }
+            }
+            for (; i < n; i += 64) {
                 fsy[nsym + i] = ssy[i];
                 fps[nsym + i] = sps[i];
             }
