@@ -13,10 +13,10 @@ import os, subprocess, sys
 R = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 C = os.path.join(R, "zarr_amd", "csrc")
 SRC = open(os.path.join(C, "zcg_inflate_wave.hip")).read()
-FAR = [("const u32x4 V0 = *(const gu32x4_ua*)(gd + src);", "const u32x4 V0 = u32x4{src, src ^ 1u, src ^ 2u, src ^ 3u};"),
-       ("const u32x4 V1 = *(const gu32x4_ua*)(gd + src + (np > 1 ? 16u : 0u));", "const u32x4 V1 = V0;"),
+FAR = [("V0 = *(const gu32x4_ua*)(gd + src);", "V0 = u32x4{src, src ^ 1u, src ^ 2u, src ^ 3u};"),
+       ("V1 = *(const gu32x4_ua*)(gd + src + (np > 1 ? 16u : 0u));", "V1 = V0;"),
        ("const u32x4 Vp = *(const gu32x4_ua*)(gd + src + 16 * p);", "const u32x4 Vp = V0 + p;")]
-NSRC = [("else cur = IE_VAL | (u32)gd[swap_pos32(S32 + p - d, tw)];", "else cur = IE_VAL | (p & 0xFFu);")]
+NSRC = [("else cur = IE_VAL | (u32)gd[swap_pos32(S32 + p - d, tw)];", "else cur = IE_VAL | (p & 0xFFu);")]  # (!wide_ok only since round 6)
 VARIANTS = {"nofar": FAR, "nonsrc": NSRC, "nofs": FAR + NSRC}
 
 
