@@ -559,11 +559,14 @@ struct CrcShift { u32 m[32]; };
 
 // 64 lanes per chunk: lane l CRCs slice l (the remainder goes to slice 0), then
 // lane 0 folds them with the operator that advances a register over Lsl bytes.
+// With crc_out set, only the CRC of each chunk's input is stored there (for
+// the trailer dz_final writes; status and out_len are not read).
 __global__ __launch_bounds__(64) void gzip_crc32(const zcg_chunk* __restrict__ chunks, u32 n, u64 D,
                                                  u64 Lsl, CrcShift op, const u64* __restrict__ out_len,
-                                                 const i32* __restrict__ status, DType t) {
+                                                 const i32* __restrict__ status, DType t, u32* __restrict__ crc_out) {
     const u32 c = blockIdx.x, lane = threadIdx.x;
-    if (c >= n || status[c] != ZCG_OK) return;
+    if (c >= n) return;
+    if (crc_out ? chunks[c].src_len < D : status[c] != ZCG_OK) return;
     const u8* src = (const u8*)chunks[c].src;
     const u64 rem = D - 64 * Lsl;  // slice 0 length = Lsl + rem
     const u64 a = lane == 0 ? 0 : rem + lane * Lsl;
@@ -591,6 +594,10 @@ __global__ __launch_bounds__(64) void gzip_crc32(const zcg_chunk* __restrict__ c
     u32 r = s_crc[0];
     for (u32 l = 1; l < 64; l++) r = gf2_times(op.m, r) ^ s_crc[l];
     r ^= 0xFFFFFFFFu;
+    if (crc_out) {
+        crc_out[c] = r;
+        return;
+    }
     u8* o = (u8*)chunks[c].dst + out_len[c] - 8;
     o[0] = (u8)r; o[1] = (u8)(r >> 8); o[2] = (u8)(r >> 16); o[3] = (u8)(r >> 24);
     const u32 isz = (u32)D;
@@ -790,7 +797,7 @@ struct DzLayout {
     u32 m, sb, nbmax;
     u64 tot, cub_bytes, outcap;
     u64 off_ka, off_kb, off_va, off_vb, off_cub, off_m2, off_sym, off_pos, off_bm, off_tail, off_ch, off_blk,
-        off_out, total;
+        off_out, off_crc, total;
 };
 
 DzLayout dz_layout(u64 D, u32 n) {
@@ -827,12 +834,17 @@ DzLayout dz_layout(u64 D, u32 n) {
     y.off_ch = take(sizeof(DzChunk) * (u64)y.sb);
     y.off_blk = take(sizeof(DzBlock) * (u64)y.sb * y.nbmax);
     y.off_out = take(y.outcap * y.sb);
+    y.off_crc = take(4ull * y.sb);  // the super-batch's input CRC32s (dz_final writes the trailers)
     y.total = p;
     return y;
 }
 
 // keys: chunk id << 16 | zlib's 15-bit hash of the serialised bytes p..p+2
-// (positions past D-3 are never inserted: a group of their own)
+// (positions past D-3 are never inserted: a group of their own).  (Hash-only
+// keys sort in two radix passes instead of three and a stable sort still
+// leaves each (hash, chunk) chain contiguous, but the chunks' runs then
+// interleave: dz_best lost locality, 24.4 vs 23.2 ms per 128 C5 chunks, more
+// than the pass saved.)
 __global__ void dz_keys(const zcg_chunk* __restrict__ chunks, u32 c0, u64 D, u64 tot, DType t,
                         u32* __restrict__ keys, u32* __restrict__ vals) {
     const u64 g = (u64)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1665,10 +1677,11 @@ __global__ __launch_bounds__(64) void dz_emit(const zcg_chunk* __restrict__ chun
     flush_to(0, true);
 }
 
-// Per chunk: gzip header, the stream, CRC32/ISIZE (gzip_crc32 after it).
+// Per chunk: gzip header, the stream, CRC32/ISIZE (the CRC from gzip_crc32 crc_out mode, run before).
 __global__ __launch_bounds__(256) void dz_final(const zcg_chunk* __restrict__ chunks, u32 c0, u32 nc, u64 D,
                                                u64 bound, u32 xfl, const DzChunk* __restrict__ cst, const u8* out,
-                                               u64 outcap, u64* __restrict__ out_len, i32* __restrict__ status) {
+                                               u64 outcap, u64* __restrict__ out_len, i32* __restrict__ status,
+                                               const u32* __restrict__ crc) {
     const u32 c = blockIdx.x, tid = threadIdx.x;
     if (c >= nc) return;
     const zcg_chunk ch = chunks[c0 + c];
@@ -1691,6 +1704,11 @@ __global__ __launch_bounds__(256) void dz_final(const zcg_chunk* __restrict__ ch
         else for (u64 j = i; j < n; j++) dst[DF_HDR + j] = o[j];
     }
     if (tid == 0) {
+        const u32 r = crc[c], isz = (u32)D;
+        u8* tr = dst + DF_HDR + n;
+        const u8 t8[8] = {(u8)r, (u8)(r >> 8), (u8)(r >> 16), (u8)(r >> 24),
+                          (u8)isz, (u8)(isz >> 8), (u8)(isz >> 16), (u8)(isz >> 24)};
+        for (u32 i = 0; i < 8; i++) tr[i] = t8[i];
         out_len[c0 + c] = DF_HDR + n + 8;
         status[c0 + c] = ZCG_OK;
     }
@@ -1731,11 +1749,48 @@ static hipError_t launch_deflate_exact(const zcg_array* a, const zcg_chunk* d_ch
         if (hipError_t e = lds_attr_once((const void*)dz_parse_fast, (int)DZF_LDS_RING); e != hipSuccess) return e;
     }
     const bool two = side && fork && join && !fast;  // the parse of each sub-batch on the side stream
+    const u64 Lsl = D / 64;
+    CrcShift op;
+    crc_shift_op(Lsl, op.m);
+    u32* crcb = (u32*)(w + y.off_crc);
+    // blocks (trees, header bits), their bit offsets, the bits, the container
+    // with its CRC32 trailer: for the chunks [s0 + cb, s0 + cb + cnt) of the
+    // super-batch at s0
+    auto tail = [&](u32 s0, u32 cb, u32 cnt, hipStream_t ts) -> hipError_t {
+        const u64 nbk = (u64)cnt * y.nbmax;
+        DzChunk* cs = cst + cb;
+        DzBlock* bk = blks + (u64)cb * y.nbmax;
+        u8* ot = out + (u64)cb * y.outcap;
+        hipLaunchKernelGGL(dz_plan, dim3((u32)nbk), dim3(64), 0, ts, cnt, cs, bk, y.nbmax, (const u32*)w, D);
+        hipLaunchKernelGGL(dz_offsets, dim3((cnt + 63) / 64), dim3(64), 0, ts, cnt, cs, bk, y.nbmax, ot, y.outcap);
+        hipLaunchKernelGGL(dz_emit, dim3((u32)nbk), dim3(64), 0, ts, d_chunks, s0 + cb, cnt, D, t, (const DzChunk*)cs,
+                           (const DzBlock*)bk, y.nbmax, (const u32*)w, ot, y.outcap);
+        hipLaunchKernelGGL(dz_final, dim3(cnt), dim3(256), 0, ts, d_chunks, s0 + cb, cnt, D, bound, xfl,
+                           (const DzChunk*)cs, (const u8*)ot, y.outcap, (u64*)d_out_len, (i32*)d_status,
+                           (const u32*)crcb + cb);
+        return hipGetLastError();
+    };
     for (u32 s0 = 0; s0 < n; s0 += y.sb) {
         const u32 scnt = (n - s0) < y.sb ? (n - s0) : y.sb;
         // a parse that does not run leaves every chunk failed, so the kernels
         // after it never read an unset record
         if (hipError_t e = hipMemsetAsync(cst, 0xFF, sizeof(DzChunk) * (size_t)scnt, s); e != hipSuccess) return e;
+        // the inputs' CRC32s: on the side stream (idle until the first parse)
+        // beside the first match search, else in line.  (Sorting sub-batch
+        // i + 1 on the side stream beside match search i measured slower,
+        // 133.7 vs 126.0 ms per C5 call: the search takes the CUs, the sort
+        // beside it ran 20 instead of 3 ms and held back the parses.)
+        {
+            hipStream_t cs = s;
+            if (two && D > 0) {
+                if (hipError_t e = hipEventRecord(fork, s); e != hipSuccess) return e;
+                if (hipError_t e = hipStreamWaitEvent(side, fork, 0); e != hipSuccess) return e;
+                cs = side;
+            }
+            hipLaunchKernelGGL(gzip_crc32, dim3(scnt), dim3(64), 0, cs, d_chunks + s0, scnt, D, Lsl, op,
+                               (const u64*)nullptr, (const i32*)nullptr, t, crcb);
+            if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
+        }
         for (u32 c0 = s0; c0 < s0 + scnt && D > 0 && !fast; c0 += y.m) {
             const u32 cnt = (s0 + scnt - c0) < y.m ? (s0 + scnt - c0) : y.m;
             const u64 tot = (u64)cnt * D;
@@ -1764,6 +1819,8 @@ static hipError_t launch_deflate_exact(const zcg_array* a, const zcg_chunk* d_ch
                                y.off_m2 / 4, y.off_sym / 4, y.off_pos / 4, y.off_bm / 4, y.off_tail / 4, cst, blks,
                                y.nbmax, c0 - s0);
             if ((e = hipGetLastError()) != hipSuccess) return e;
+            // and the rest of the sub-batch's encode right behind it
+            if (two && (e = tail(s0, c0 - s0, cnt, side)) != hipSuccess) return e;
         }
         if (two) {
             if (hipError_t e = hipEventRecord(join, side); e != hipSuccess) return e;
@@ -1780,21 +1837,11 @@ static hipError_t launch_deflate_exact(const zcg_array* a, const zcg_chunk* d_ch
                                y.nbmax, 0u);
             if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
         }
-        const u64 nbk = (u64)scnt * y.nbmax;
-        hipLaunchKernelGGL(dz_plan, dim3((u32)nbk), dim3(64), 0, s, scnt, cst, blks, y.nbmax, (const u32*)w, D);
-        hipLaunchKernelGGL(dz_offsets, dim3((scnt + 63) / 64), dim3(64), 0, s, scnt, cst, blks, y.nbmax, out,
-                           y.outcap);
-        hipLaunchKernelGGL(dz_emit, dim3((u32)nbk), dim3(64), 0, s, d_chunks, s0, scnt, D, t, (const DzChunk*)cst,
-                           (const DzBlock*)blks, y.nbmax, (const u32*)w, out, y.outcap);
-        hipLaunchKernelGGL(dz_final, dim3(scnt), dim3(256), 0, s, d_chunks, s0, scnt, D, bound, xfl,
-                           (const DzChunk*)cst, (const u8*)out, y.outcap, (u64*)d_out_len, (i32*)d_status);
+        if (!two || D == 0) {
+            if (hipError_t e = tail(s0, 0, scnt, s); e != hipSuccess) return e;
+        }
     }
-    const u64 Lsl = D / 64;
-    CrcShift op;
-    crc_shift_op(Lsl, op.m);
-    hipLaunchKernelGGL(gzip_crc32, dim3(n), dim3(64), 0, s, d_chunks, n, D, Lsl, op, (const u64*)d_out_len,
-                       (const i32*)d_status, t);
-    return hipGetLastError();
+    return hipSuccess;
 }
 
 // levels 1-9 reproduce zlib's bytes (1-3 deflate_fast, 4-9 deflate_slow);
@@ -1874,7 +1921,7 @@ hipError_t launch_deflate(const zcg_array* a, const zcg_chunk* d_chunks, uint32_
     CrcShift op;
     crc_shift_op(Lsl, op.m);
     hipLaunchKernelGGL(gzip_crc32, dim3(n), dim3(64), 0, s, d_chunks, n, D, Lsl, op,
-                       (const u64*)d_out_len, (const i32*)d_status, t);
+                       (const u64*)d_out_len, (const i32*)d_status, t, (u32*)nullptr);
     return hipGetLastError();
 }
 

@@ -716,22 +716,19 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
                     it1++;
                     if (q >= pend) run = false;
                 }
-                // flush: the aligned block holding token nt0 (its words before
-                // nt0 are still in the ring from the last flush) and, when this
-                // period crossed into it, the next block (words past nt are
-                // overwritten later); then the mark window (words past my
-                // position are still zero)
+                // flush: the aligned block holding token nt0 once it is complete
+                // (each block is stored once: its first words stay in the ring
+                // until then, <= 3 + IW_K < 8 entries); then the mark window
+                // (words past my position are still zero)
                 {
                     const u32 a0 = nt0 & ~3u, sb = a0 & 4u;
-                    *(gu32x4_a16*)(gl + iw_ta(lane, a0)) =
-                        u32x4{L.u.hr.tst[sb][lane], L.u.hr.tst[sb + 1][lane], L.u.hr.tst[sb + 2][lane],
-                              L.u.hr.tst[sb + 3][lane]};
-                    if (nt > a0 + 4)
-                        *(gu32x4_a16*)(gl + iw_ta(lane, a0 + 4)) =
-                            u32x4{L.u.hr.tst[sb ^ 4][lane], L.u.hr.tst[(sb ^ 4) + 1][lane],
-                                  L.u.hr.tst[(sb ^ 4) + 2][lane], L.u.hr.tst[(sb ^ 4) + 3][lane]};
+                    if (nt >= a0 + 4) {
+                        *(gu32x4_a16*)(gl + iw_ta(lane, a0)) =
+                            u32x4{L.u.hr.tst[sb][lane], L.u.hr.tst[sb + 1][lane], L.u.hr.tst[sb + 2][lane],
+                                  L.u.hr.tst[sb + 3][lane]};
+                        nt0 = nt;
+                    }
                 }
-                nt0 = nt;
                 u32 mv[IW_MWIN];
 #pragma unroll
                 for (u32 j = 0; j < IW_MWIN; j++) mv[j] = L.u.hr.mwin[j][lane];
@@ -740,9 +737,15 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
                 // flushes store nothing (stores to a dummy slot instead cost
                 // 14 GB of writes and 11 % of the time per C2 launch: the slot
                 // lines do not stay in L2 under 4 096 chunks' token lists)
+                // Only words w0 .. w1 (the word of my next token start) can hold
+                // marks yet, and w1 - w0 < 4 in almost every period: the second
+                // half of the window is stored only when the lane got that far
+                // (its zero words are stored when the window has slid onto them;
+                // pass 2 and iw_rank read no word past the marked extent)
+                const u32 w1 = (q - p) >> 5;
                 if (w0 < IW_MARKW) {
                     *(gu32x4_a4*)(mk + w0) = u32x4{mv[0], mv[1], mv[2], mv[3]};
-                    *(gu32x4_a4*)(mk + w0 + 4) = u32x4{mv[4], mv[5], mv[6], mv[7]};
+                    if (w1 >= w0 + 4) *(gu32x4_a4*)(mk + w0 + 4) = u32x4{mv[4], mv[5], mv[6], mv[7]};
                 }
                 // the first IW_EMW words also into LDS (rewritten until the
                 // window has moved past them: then they are final)
@@ -754,7 +757,7 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
                     L.u.hr.em[1][lane] = mv[0];
                 }
                 // slide the window to the word of my next token start (< 8 words on)
-                const u32 w1 = (q - p) >> 5, dw = w1 - w0;
+                const u32 dw = w1 - w0;
 #pragma unroll
                 for (u32 sb = 1; sb < IW_MWIN; sb <<= 1) {
                     const bool t = (dw & sb) != 0;
@@ -768,6 +771,13 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
               gr_absorb(bs, vC, vD);
             }
             static_assert(IW_K == 4 && IW_MWIN == 8, "flush layout");
+            // the last, incomplete block (an inactive lane's list never went through the ring)
+            if (active && nt > (nt0 & ~3u)) {
+                const u32 a0 = nt0 & ~3u, sb = a0 & 4u;
+                *(gu32x4_a16*)(gl + iw_ta(lane, a0)) =
+                    u32x4{L.u.hr.tst[sb][lane], L.u.hr.tst[sb + 1][lane], L.u.hr.tst[sb + 2][lane],
+                          L.u.hr.tst[sb + 3][lane]};
+            }
             // marked extent: the whole segment, or up to where the lane stopped
             {
                 const u32 ext = !active ? 0u : nxt == S_NONE ? seg : (q - p) + (nxt == S_MARKER ? 1u : 0u);
