@@ -46,7 +46,7 @@ def test_abi_version_and_pure_helpers():
 # The product build's tuning constants (A/B builds under tools/ pass -D
 # overrides; the shipped library must not be one of them).
 DEFAULT_BUILD_CONFIG = ("inflate_wave:S=2048,TCAP=768,WPE=4,EST_PCT=108,MARKW=32,G=4,DBG=0;"
-                        "inflate_par:PF=16,FU=16,WPE=3;deflate:CHAIN6=32;raw:VPT=1;region:U=4;"
+                        "inflate_par:PF=16,FU=16,WPE=3;deflate:CHAIN6=32,SUB=128;raw:VPT=1;region:U=4;"
                         "lz4_dec:CORUN=55/131072/196608,LPW=64/64/262144;xz_opt:SEG_KB=256,WPE=4,PROF=0;bz2:KMUL=4")
 
 

@@ -773,6 +773,10 @@ __global__ void df_best(const zcg_chunk* __restrict__ chunks, u32 c0, u64 D, u64
 namespace {
 
 constexpr u64 DZ_SUPER_BYTES = 512ull << 20;  // input bytes per super-batch (match results kept for all)
+#ifndef ZDZ_SUB_MIB
+#define ZDZ_SUB_MIB 128  // (256: 125.7 vs 125.6-126.0 ms per C5 call; 512: 130.4)
+#endif
+constexpr u64 DZ_SUB_BYTES = (u64)ZDZ_SUB_MIB << 20;  // input bytes per match-search sub-batch (zlib-exact coder)
 constexpr u32 DZ_TAILCAP = 2048;               // symbols a segment's parse may run past its end before syncing
 constexpr u32 DZ_HDRW = 96;                 // header bit-string words per block (<= 14 + 57 + 316 * 14 bits)
 
@@ -802,7 +806,7 @@ struct DzLayout {
 
 DzLayout dz_layout(u64 D, u32 n) {
     DzLayout y{};
-    u64 m = D ? DF_SUB_BYTES / D : n;
+    u64 m = D ? DZ_SUB_BYTES / D : n;
     if (m < 1) m = 1;
     if (m > n) m = n;
     if (m > 65536) m = 65536;  // chunk id + 16 key bits fit 32
@@ -1862,7 +1866,7 @@ uint64_t deflate_ws_bytes(const zcg_array* a, uint32_t n) {
 #ifndef ZCG_DF_CHAIN6
 #define ZCG_DF_CHAIN6 32
 #endif
-const char* cfg_deflate() { return "deflate:CHAIN6=" ZCG_STR(ZCG_DF_CHAIN6); }
+const char* cfg_deflate() { return "deflate:CHAIN6=" ZCG_STR(ZCG_DF_CHAIN6) ",SUB=" ZCG_STR(ZDZ_SUB_MIB); }
 
 hipError_t launch_deflate(const zcg_array* a, const zcg_chunk* d_chunks, uint32_t n,
                           uint64_t* d_out_len, int32_t* d_status, void* ws, uint64_t ws_bytes,
