@@ -72,7 +72,7 @@ LEG = {"gzip": {"pool": 64, "batch": 4096, "strong": False},
 ENCODE_LEG = {"gzip": (512, 2), "lz4": (1024, 3), "xz": (1024, 2), "bzip2": (512, 2)}
 # committed PMC traffic passes, newest first: a leg takes the first file that
 # measured it at the bench's own batch (kernels change between rounds)
-TRAFFIC_FILES = [os.path.join(ROOT, "profiles", f) for f in ("r05_pmc_traffic.json", "r04_pmc_traffic.json", "r03_pmc_traffic.json",
+TRAFFIC_FILES = [os.path.join(ROOT, "profiles", f) for f in ("r06_pmc_traffic.json", "r05_pmc_traffic.json", "r04_pmc_traffic.json", "r03_pmc_traffic.json",
                                                               "r02_pmc_traffic.json")]
 
 
