@@ -166,7 +166,7 @@ int zcg_codec_on_gpu(int32_t codec, int encode);
  * zcg_status for argument/launch errors only — per-chunk results land in
  * d_status.  Workspace is grown on first use of a given batch shape
  * (hipMalloc), so steady-state calls do no allocation and are capturable.
- * The workspace is kept per stream (gzip decode: ~100 MiB at full batch,
+ * The workspace is kept per stream (gzip decode: ~0.9 GB at full batch,
  * zcg_workspace_bytes gives the figure); a context keeps at most 4 streams'
  * workspaces and frees the least recently used one (after a device-wide
  * synchronize) when a fifth stream arrives. */
