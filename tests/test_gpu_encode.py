@@ -706,3 +706,29 @@ def test_lz4_encode_block_count_limit():
     r = ctx.lib.zcg_encode_batch(ctx.handle, ctypes.byref(arr), ctypes.c_void_p(dummy.data_ptr()), 1,
                                  ctypes.c_void_p(ol.data_ptr()), ctypes.c_void_p(st.data_ptr()), None)
     assert r == _native.UNSUPPORTED and "4096" in ctx.last_error()
+
+
+@pytest.mark.gpu
+def test_gzip_encode_huge_chunk_is_per_chunk_unsupported():
+    """A gzip chunk of >= 2 GiB (the zlib-exact coder's u32 positions) is
+    refused per chunk: the launch succeeds, every chunk's status is
+    ZCG_ERR_UNSUPPORTED and its length 0 (before round 6 the
+    whole batch failed with an invalid-value launch error).  The chunk table
+    points at a zeroed dummy and is never read."""
+    import ctypes
+    import torch
+    from zarr_amd import _native
+    from zarr_amd.chunk import abi_array
+    ctx = _native.context(0)
+    D = 1 << 31
+    meta = ArrayMetadata.new([D], [D], "u1", Gzip(6))
+    dummy = torch.zeros(128, dtype=torch.uint8, device="cuda:0")
+    st = torch.full((2,), 77, dtype=torch.int32, device="cuda:0")
+    ol = torch.full((2,), 5, dtype=torch.int64, device="cuda:0")
+    arr = abi_array(meta)
+    r = ctx.lib.zcg_encode_batch(ctx.handle, ctypes.byref(arr), ctypes.c_void_p(dummy.data_ptr()), 2,
+                                 ctypes.c_void_p(ol.data_ptr()), ctypes.c_void_p(st.data_ptr()), None)
+    torch.cuda.synchronize()
+    assert r == _native.OK, ctx.last_error()
+    assert st.cpu().tolist() == [_native.UNSUPPORTED] * 2
+    assert ol.cpu().tolist() == [0, 0]
