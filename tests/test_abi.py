@@ -47,7 +47,7 @@ def test_abi_version_and_pure_helpers():
 # overrides; the shipped library must not be one of them).
 DEFAULT_BUILD_CONFIG = ("inflate_wave:S=2048,TCAP=768,WPE=4,EST_PCT=108,MARKW=32,G=4,DBG=0;"
                         "inflate_par:PF=16,FU=16,WPE=3;deflate:CHAIN6=32,SUB=128;raw:VPT=1;region:U=4;"
-                        "lz4_dec:CORUN=55/131072/196608,LPW=64/64/262144;xz_opt:SEG_KB=256,WPE=4,PROF=0;bz2:KMUL=4")
+                        "lz4_dec:CORUN=55/131072/196608,LPW=64/64/262144;xz_opt:SEG_KB=256,WPE=4,PROF=0;bz2:KMUL=4,GSAFE=1")
 
 
 def test_library_built_with_default_knobs():

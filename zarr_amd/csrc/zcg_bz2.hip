@@ -928,7 +928,7 @@ u32 bz_nb(uint32_t n) { return n < BZ_NB ? n : BZ_NB; }
 constexpr u64 BZ_OWNER_BYTES = 4ull * BZ_NB;
 }  // namespace
 
-const char* cfg_bz2() { return "bz2:KMUL=" ZCG_STR(ZB_KMUL); }
+const char* cfg_bz2() { return "bz2:KMUL=" ZCG_STR(ZB_KMUL) ",GSAFE=" ZCG_STR(ZB_GSAFE); }
 
 // the array's block-size level (9 when the metadata does not say)
 static int bz_level(const zcg_array* a) {
