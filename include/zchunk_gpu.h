@@ -105,6 +105,11 @@ enum zcg_status {
  * ended by an empty stored block; the stream inflates to the same data, but
  * its bytes differ from zlib's).  Level 0 always uses the segmented coder. */
 #define ZCG_FLAG_GZIP_SEGMENTED 0x8000u
+/* Test hook: the one-wave-per-chunk inflate kernel sizes its first segments
+ * at 116 % instead of 108 % of the estimated block bits, which makes the
+ * first round of all-literal 16 383-symbol blocks cap a list and halve the
+ * segment size (the round-6 regression test of that path).  Same output. */
+#define ZCG_FLAG_DEBUG_INFLATE_LONG_SEG 0x10000u
 
 /* CompressionType + its configuration (camelCase JSON keys in the reference). */
 typedef struct zcg_compression {

@@ -531,3 +531,20 @@ def test_gzip_dynamic_header_corruption():
                 variants.append(bytes(bad))
     for flags in (0, FLAG_SERIAL_INFLATE, FLAG_INFLATE_BLOCK_PAR, FLAG_INFLATE_WAVE):
         check_many("gzip", variants, "u1", len(payload), flags)
+
+
+def test_inflate_wave_capped_chain_keeps_block_positions():
+    """Round-6 regression: when the first round's chain runs past a block's
+    EOB and its last member's list is capped, the segment size is halved for
+    the next round; the EOB's bit position (the next header) must still come
+    from this round's segment starts.  All-literal 16 383-symbol blocks with
+    the long-segment test hook (116 %) hit exactly that path; before the fix
+    the next header was read at the halved-segment position (InvalidData)."""
+    payload = DATASETS["randwalk_i2"]()
+    s = gzip_wrap(deflate(payload, 6, zlib.Z_HUFFMAN_ONLY), payload)
+    st, ref = zref.decode(zref.GZIP, s, len(payload), 1, 0, 0)
+    assert st == zref.OK and ref == payload
+    for flags in (FLAG_INFLATE_WAVE | 0x10000, FLAG_INFLATE_WAVE):
+        kind, out = gpu_decode("gzip", s, "u1", len(payload), None, flags)
+        assert kind == "Ok", (kind, flags)
+        assert out == payload, flags

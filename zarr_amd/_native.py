@@ -23,6 +23,7 @@ FLAG_SERIAL_INFLATE = 0x100
 FLAG_DEBUG_COUNTERS = 0x200
 FLAG_INFLATE_BLOCK_PAR = 0x2000
 FLAG_INFLATE_WAVE = 0x4000
+FLAG_DEBUG_INFLATE_LONG_SEG = 0x10000
 
 STATUS_NAMES = {OK: "Ok", UNEXPECTED_EOF: "UnexpectedEof", INVALID_DATA: "InvalidData",
                 INVALID_INPUT: "InvalidInput", UNSUPPORTED: "Unsupported",

@@ -668,7 +668,8 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
         u32 R0 = hdr_end;
         bool block_end = false;
         bool final_cut = false;
-        u32 seg = (u32)(((u64)est * ZIW_EST_PCT / 100 / 64 + 31) & ~31ull);
+        const u32 est_pct = (vflags & ZCG_FLAG_DEBUG_INFLATE_LONG_SEG) ? 116u : (u32)ZIW_EST_PCT;
+        u32 seg = (u32)(((u64)est * est_pct / 100 / 64 + 31) & ~31ull);
         seg = seg < IW_SEGMIN ? IW_SEGMIN : seg > IW_SEGMAX ? IW_SEGMAX : seg;
         while (!block_end && !final_cut && r == R_OK && P < D) {
             // ================= H round: coarse speculative Huffman decode =================
@@ -855,7 +856,8 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
             }
             const u32 endq = (u32)__builtin_amdgcn_readlane((int)q, (int)cur);  // after the last member's list
             if ((u32)__builtin_amdgcn_readlane((int)nxt, (int)cur) == S_CAP && seg > IW_SEGMIN)
-                seg = (seg / 2 + 31) & ~31u;  // lists overflowed: shorter segments next round
+                seg = (seg / 2 + 31) & ~31u;  // lists overflowed: shorter segments next round (this round's
+                                              // positions come from p, computed with the old seg)
             IW_ADD(IWD_CHAIN, ncm);
             // token lists of other lanes are read below: their stores must be done
             __syncthreads();
@@ -1246,7 +1248,9 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
                     round_done = true;
                     if (boundary) {
                         u32 qn = endq;
-                        if (cm < ncm) qn = iw_pos(gl, mL(cm), cj, R0 + mL(cm) * seg);
+                        // (the member's segment start from this round's p: seg may
+                        // already be halved for the next round, after a capped list)
+                        if (cm < ncm) qn = iw_pos(gl, mL(cm), cj, (u32)__builtin_amdgcn_readlane((int)p, (int)mL(cm)));
                         b.cbase = ~0ull;
                         bi_seek(b, qn);
                     }
@@ -1262,7 +1266,10 @@ __global__ __launch_bounds__(64, ZIW_WPE) void inflate_wave_kernel(const zcg_chu
                         seg = sg < IW_SEGMIN ? IW_SEGMIN : sg > IW_SEGMAX ? IW_SEGMAX : sg;
                     } else if (mcode == M_EOB) {
                         const u32 lm = mL(cm);
-                        const u32 qe = iw_pos(gl, lm, cj + 1, R0 + lm * seg);  // after the EOB code
+                        // after the EOB code; the member's segment start is this
+                        // round's p (not R0 + lm * seg: seg may already be halved for
+                        // the next round when the chain's last list was capped)
+                        const u32 qe = iw_pos(gl, lm, cj + 1, (u32)__builtin_amdgcn_readlane((int)p, (int)lm));
                         IW_T(IWT_EOB);
                         block_end = true;
                         b.cbase = ~0ull;
